@@ -1,0 +1,1128 @@
+// fmx_capi.cpp -- C ABI of libfmx: handle lifetime, per-channel parameter
+// mirrors of the reference setters, resampler timing schedules, and the
+// launch sequence that replaces one iteration of the reference's per-block
+// body (src/main.cpp:1239-1308) for every channel of a handle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fmx_internal.h"
+#include "fmx_synth.h"
+
+namespace fmx {
+
+#define HIP_TRY(expr)                                                                                   \
+  do {                                                                                                  \
+    hipError_t e__ = (expr);                                                                            \
+    if (e__ != hipSuccess) {                                                                            \
+      h->err = std::string(#expr) + ": " + hipGetErrorString(e__);                                      \
+      return FMX_E_HIP;                                                                                 \
+    }                                                                                                   \
+  } while (0)
+
+// Timing groups: channels whose resampler timing state is identical share
+// one host-simulated output schedule (the schedule does not depend on the
+// signal, only on the state and the number of inputs).
+struct TimingSet {
+  float del = 1.0f;
+  std::vector<ResampTiming> groups;
+  std::vector<int> chan_group;
+  std::vector<FmxSched> hsched;
+  std::vector<int> hcount;
+  FmxSched *d_sched = nullptr;
+  int *d_count = nullptr;
+  int *d_group = nullptr;
+  int stride = 0, cap_groups = 0;
+  bool group_dirty = true;
+};
+
+struct Handle {
+  fmx_config cfg{};
+  int C = 0, device = 0, M = 1;
+  std::string err;
+  hipStream_t stream = nullptr, stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  FmxDesign *hdes = nullptr;
+  FmxDesign *ddes = nullptr;
+  DesignExtras ex;
+  // parameters
+  std::vector<FmxChanParam> hpar;
+  FmxChanParam *dpar = nullptr;
+  bool par_dirty = true;
+  std::vector<int> w0, bw_mode, agc_ready;
+  // state
+  uint8_t *dec_hist = nullptr;
+  int *dec_valid = nullptr;
+  float *dc_v = nullptr, *agc = nullptr, *fd_prev = nullptr, *clip = nullptr;
+  float2_t *iq_hist = nullptr;
+  float *st_hist = nullptr, *lr_hist = nullptr, *af_win = nullptr, *af_iir = nullptr;
+  float *mono_win = nullptr, *mono_iir = nullptr, *rds_hist = nullptr, *ring = nullptr;
+  FmxStereoState *st = nullptr;
+  FmxRdsState *rds = nullptr;
+  int *reset_mask = nullptr;
+  std::vector<int> hmask;
+  // intermediates
+  float *mpx = nullptr, *pilot = nullptr, *lraw = nullptr, *rraw = nullptr, *rds_in = nullptr;
+  int *rds_count = nullptr, *tmp_count = nullptr, *tmp_int = nullptr;
+  int rds_stride = 0;
+  int st_parity = 0;
+  uint32_t block_index = 0;
+  TimingSet t_af, t_mono, t_rds;
+  // kernel timing
+  bool timing = false;
+  struct Pending {
+    int k;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  double kms[FMX_K_COUNT] = {0, 0, 0, 0};
+  int klaunch[FMX_K_COUNT] = {0, 0, 0, 0};
+  std::vector<void *> allocs;
+};
+
+static int dmalloc(Handle *h, void **p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    h->err = std::string("hipMalloc failed: ") + hipGetErrorString(e);
+    return FMX_E_NOMEM;
+  }
+  hipMemset(*p, 0, bytes);
+  h->allocs.push_back(*p);
+  return FMX_OK;
+}
+template <typename T> static int dalloc(Handle *h, T **p, size_t count) {
+  return dmalloc(h, reinterpret_cast<void **>(p), count * sizeof(T));
+}
+
+static hipEvent_t ev_get(Handle *h) {
+  if (!h->pool.empty()) {
+    hipEvent_t e = h->pool.back();
+    h->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct KTimer {
+  Handle *h;
+  int k;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  KTimer(Handle *hh, int kk, hipStream_t ss) : h(hh), k(kk), s(ss) {
+    if (h->timing) {
+      a = ev_get(h);
+      b = ev_get(h);
+      hipEventRecord(a, s);
+    }
+  }
+  ~KTimer() {
+    if (h->timing) {
+      hipEventRecord(b, s);
+      h->pending.push_back({k, a, b});
+    }
+  }
+};
+
+static void collect_timing(Handle *h) {
+  for (auto &p : h->pending) {
+    float ms = 0.0f;
+    hipEventSynchronize(p.b);
+    hipEventElapsedTime(&ms, p.a, p.b);
+    h->kms[p.k] += ms;
+    h->klaunch[p.k]++;
+    h->pool.push_back(p.a);
+    h->pool.push_back(p.b);
+  }
+  h->pending.clear();
+}
+
+/* ---------------- timing sets ---------------- */
+static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
+  t.del = del;
+  ResampTiming r;
+  timing_reset(r);
+  r.del = del;
+  t.groups.assign(1, r);
+  t.chan_group.assign(static_cast<size_t>(h->C), 0);
+  t.stride = static_cast<int>(std::ceil(static_cast<double>(max_in) / std::max(0.5, (double)del))) + 8;
+  t.cap_groups = 4;
+  t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
+  t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
+  int rc;
+  if ((rc = dalloc(h, &t.d_sched, static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &t.d_count, static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &t.d_group, static_cast<size_t>(h->C))) != FMX_OK) return rc;
+  t.group_dirty = true;
+  return FMX_OK;
+}
+
+// channel c's resampler was reset (liquid resamp_reset): move it to a group
+// in the post-reset state, creating the group if needed; drop empty groups.
+static void tset_reset_channel(TimingSet &t, int c) {
+  ResampTiming fresh;
+  timing_reset(fresh);
+  fresh.del = t.del;
+  int g = -1;
+  for (size_t i = 0; i < t.groups.size(); ++i)
+    if (timing_equal(t.groups[i], fresh)) {
+      g = static_cast<int>(i);
+      break;
+    }
+  if (g < 0) {
+    t.groups.push_back(fresh);
+    g = static_cast<int>(t.groups.size()) - 1;
+  }
+  t.chan_group[static_cast<size_t>(c)] = g;
+  t.group_dirty = true;
+}
+
+static void tset_compact(TimingSet &t) {
+  std::vector<int> used(t.groups.size(), 0);
+  for (int g : t.chan_group) used[static_cast<size_t>(g)] = 1;
+  std::vector<int> remap(t.groups.size(), -1);
+  std::vector<ResampTiming> ng;
+  for (size_t i = 0; i < t.groups.size(); ++i)
+    if (used[i]) {
+      // merge groups whose state became identical
+      int found = -1;
+      for (size_t j = 0; j < ng.size(); ++j)
+        if (timing_equal(ng[j], t.groups[i])) found = static_cast<int>(j);
+      if (found < 0) {
+        ng.push_back(t.groups[i]);
+        found = static_cast<int>(ng.size()) - 1;
+      }
+      remap[i] = found;
+    }
+  if (ng.size() != t.groups.size() || ng.empty()) t.group_dirty = true;
+  for (int &g : t.chan_group) g = remap[static_cast<size_t>(g)];
+  if (ng.empty()) {
+    ResampTiming r;
+    timing_reset(r);
+    r.del = t.del;
+    ng.push_back(r);
+  }
+  t.groups = ng;
+}
+
+// Simulate n inputs for every group, upload schedules; returns max count.
+static int tset_advance(Handle *h, TimingSet &t, int n, int *max_count) {
+  tset_compact(t);
+  const int G = static_cast<int>(t.groups.size());
+  if (G > t.cap_groups) {
+    h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_sched)), h->allocs.end());
+    h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_count)), h->allocs.end());
+    hipFree(t.d_sched);
+    hipFree(t.d_count);
+    t.cap_groups = G * 2;
+    t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
+    t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
+    HIP_TRY(hipMalloc(&t.d_sched, sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.cap_groups));
+    HIP_TRY(hipMalloc(&t.d_count, sizeof(int) * static_cast<size_t>(t.cap_groups)));
+    h->allocs.push_back(t.d_sched);
+    h->allocs.push_back(t.d_count);
+  }
+  int mx = 0;
+  for (int g = 0; g < G; ++g) {
+    const int k = timing_run(t.groups[static_cast<size_t>(g)], n,
+                             t.hsched.data() + static_cast<size_t>(g) * t.stride, t.stride);
+    if (k > t.stride) {
+      h->err = "resampler schedule overflow";
+      return FMX_E_CAPACITY;
+    }
+    t.hcount[static_cast<size_t>(g)] = k;
+    mx = std::max(mx, k);
+  }
+  HIP_TRY(hipMemcpyAsync(t.d_sched, t.hsched.data(), sizeof(FmxSched) * static_cast<size_t>(t.stride) * G,
+                         hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(t.d_count, t.hcount.data(), sizeof(int) * G, hipMemcpyHostToDevice, h->stream));
+  if (t.group_dirty) {
+    HIP_TRY(hipMemcpyAsync(t.d_group, t.chan_group.data(), sizeof(int) * h->C, hipMemcpyHostToDevice,
+                           h->stream));
+    t.group_dirty = false;
+  }
+  // hipMemcpyAsync from pageable memory is staged synchronously, so the host
+  // vectors may be reused immediately.
+  if (max_count) *max_count = mx;
+  return FMX_OK;
+}
+
+static ResetArgs reset_args(Handle *h) {
+  ResetArgs r{};
+  r.des = h->ddes;
+  r.C = h->C;
+  r.mask = h->reset_mask;
+  r.st = h->st;
+  r.rds = h->rds;
+  r.ring = h->ring;
+  r.dec_hist = h->dec_hist;
+  r.dec_valid = h->dec_valid;
+  r.dc_v = h->dc_v;
+  r.iq_hist = h->iq_hist;
+  r.agc = h->agc;
+  r.fd_prev = h->fd_prev;
+  r.st_hist = h->st_hist;
+  r.lr_hist = h->lr_hist;
+  r.af_win = h->af_win;
+  r.af_iir = h->af_iir;
+  r.mono_win = h->mono_win;
+  r.mono_iir = h->mono_iir;
+  r.rds_hist = h->rds_hist;
+  return r;
+}
+
+static int apply_resets(Handle *h) {
+  bool any = false;
+  for (int v : h->hmask) any |= (v != 0);
+  if (!any) return FMX_OK;
+  HIP_TRY(hipMemcpyAsync(h->reset_mask, h->hmask.data(), sizeof(int) * h->C, hipMemcpyHostToDevice, h->stream));
+  int rc = launch_reset(reset_args(h), h->stream);
+  if (rc != FMX_OK) {
+    h->err = "reset kernel launch failed";
+    return rc;
+  }
+  std::fill(h->hmask.begin(), h->hmask.end(), 0);
+  return FMX_OK;
+}
+
+static int sync_params(Handle *h) {
+  if (!h->par_dirty) return FMX_OK;
+  HIP_TRY(hipMemcpyAsync(h->dpar, h->hpar.data(), sizeof(FmxChanParam) * h->C, hipMemcpyHostToDevice, h->stream));
+  h->par_dirty = false;
+  return FMX_OK;
+}
+
+static int prepare(Handle *h) {
+  int rc = sync_params(h);
+  if (rc != FMX_OK) return rc;
+  return apply_resets(h);
+}
+
+/* ---------------- reference setters (host mirrors) ---------------- */
+static void set_bandwidth(Handle *h, int c, int bw) { // fm_demod.cpp:168-204
+  const int sel = bandwidth_select(bw, h->w0[static_cast<size_t>(c)]);
+  if (sel == h->bw_mode[static_cast<size_t>(c)]) return;
+  h->bw_mode[static_cast<size_t>(c)] = sel;
+  h->hpar[static_cast<size_t>(c)].iqsel = sel;
+  h->hmask[static_cast<size_t>(c)] |= RS_IQFIR;
+  h->par_dirty = true;
+}
+static void set_deemph(Handle *h, int c, int code) { // main.cpp:699-708 -> both objects
+  h->hpar[static_cast<size_t>(c)].deemph = code;
+  if (code != FMX_DEEMPH_OFF) h->hmask[static_cast<size_t>(c)] |= RS_DEEMPH;
+  h->par_dirty = true;
+}
+static void set_agc(Handle *h, int c, int mode) { // fm_demod.cpp:210-217
+  h->hpar[static_cast<size_t>(c)].agc = mode;
+  if (mode != FMX_AGC_OFF) {
+    h->agc_ready[static_cast<size_t>(c)] = 1;
+    h->hmask[static_cast<size_t>(c)] |= RS_AGC;
+  }
+  h->par_dirty = true;
+}
+
+static void destroy(Handle *h) {
+  if (!h) return;
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->stream2) hipStreamSynchronize(h->stream2);
+  for (auto &p : h->pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : h->pool) hipEventDestroy(e);
+  for (void *p : h->allocs) hipFree(p);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
+  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->stream2) hipStreamDestroy(h->stream2);
+  delete h->hdes;
+  delete h;
+}
+
+static int create(const fmx_config *cfg, int n, int device, Handle **out) {
+  auto *h = new (std::nothrow) Handle();
+  if (!h) return FMX_E_NOMEM;
+  *out = h;
+  h->cfg = *cfg;
+  h->C = n;
+  h->device = device;
+  if (n <= 0 || cfg->block <= 0 || cfg->block > 32768) {
+    h->err = "n_channels must be > 0 and block in 1..32768";
+    return FMX_E_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    h->err = "no HIP device available";
+    return FMX_E_NODEVICE;
+  }
+  if (device < 0 || device >= ndev) {
+    h->err = "device index out of range";
+    return FMX_E_INVALID;
+  }
+  HIP_TRY(hipSetDevice(device));
+  h->hdes = new FmxDesign();
+  int rc = design_build(*cfg, h->hdes, &h->ex, &h->err);
+  if (rc != FMX_OK) return rc;
+  h->M = h->hdes->M;
+  if (h->M > 1 && !((h->M == 10 && h->hdes->dec_tpp == 28) || (h->M == 8 && h->hdes->dec_tpp == 28) ||
+                    (h->M == 4 && h->hdes->dec_tpp == 20) || (h->M == 2 && h->hdes->dec_tpp == 12))) {
+    h->err = "decimation factor has no kernel instantiation (supported M: 1, 2, 4, 8, 10)";
+    return FMX_E_INVALID;
+  }
+  if (h->hdes->af_del < 3.0f) {
+    h->err = "dsp_rate / out_rate must be >= 3";
+    return FMX_E_INVALID;
+  }
+  HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
+  HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
+  const size_t C = static_cast<size_t>(n);
+  const size_t B = static_cast<size_t>(cfg->block);
+  // parameters: the reference objects as main.cpp:640-710 configures them
+  h->hpar.assign(C, FmxChanParam{});
+  h->w0.assign(C, 194000);
+  h->bw_mode.assign(C, 0);
+  h->agc_ready.assign(C, 0);
+  h->hmask.assign(C, 0);
+  for (size_t c = 0; c < C; ++c) {
+    FmxChanParam &p = h->hpar[c];
+    p.iqsel = FMX_IQ_CTOR;
+    p.agc = 0;
+    p.blend = std::clamp(cfg->blend, 0, 2);
+    p.force_mono = cfg->force_mono;
+    p.force_stereo = cfg->force_stereo;
+    p.deemph = std::clamp(cfg->deemphasis, 0, 2);
+  }
+  if ((rc = dalloc(h, &h->dpar, C)) != FMX_OK) return rc;
+  // state
+  if ((rc = dalloc(h, &h->dec_hist, C * 2 * FMX_MAX_DEC)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->dec_valid, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->dc_v, C * 2)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->agc, C * 2)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->fd_prev, C * 2)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->iq_hist, C * (FMX_IQ_MAXLEN - 1))) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->st_hist, 2 * C * FMX_HIST)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->lr_hist, C * 2 * (FMX_LR_LEN - 1))) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->af_win, C * 64)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->af_iir, C * 4)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->mono_win, C * 32)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->mono_iir, C * 2)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rds_hist, C * 32)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->ring, C * 2 * FMX_RDS_RING)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->st, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rds, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->reset_mask, C)) != FMX_OK) return rc;
+  // intermediates
+  if ((rc = dalloc(h, &h->mpx, C * B)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->pilot, C * B)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->lraw, C * B)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rraw, C * B)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
+  h->rds_stride = h->t_rds.stride;
+  if ((rc = dalloc(h, &h->rds_in, C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rds_count, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->tmp_count, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->tmp_int, C * 2)) != FMX_OK) return rc;
+  // construct every object (RS_CREATE) then apply main.cpp's configuration
+  std::fill(h->hmask.begin(), h->hmask.end(), static_cast<int>(RS_CREATE));
+  for (int c = 0; c < n; ++c) {
+    h->w0[static_cast<size_t>(c)] = std::clamp(cfg->w0_bandwidth_hz, 0, 400000);
+    set_agc(h, c, std::clamp(cfg->dsp_agc, 0, 2));
+    set_deemph(h, c, std::clamp(cfg->deemphasis, 0, 2));
+    if (cfg->bandwidth_hz >= 0) set_bandwidth(h, c, cfg->bandwidth_hz); // -1: keep the ctor filter
+  }
+  rc = prepare(h);
+  if (rc != FMX_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FMX_OK;
+}
+
+static FeArgs fe_args(Handle *h, int n, int mode) {
+  FeArgs a{};
+  a.des = h->ddes;
+  a.par = h->dpar;
+  a.C = h->C;
+  a.n = n;
+  a.in_mode = mode;
+  a.st_parity = h->st_parity;
+  a.dec_hist = h->dec_hist;
+  a.dec_valid = h->dec_valid;
+  a.dc_v = h->dc_v;
+  a.iq_hist = h->iq_hist;
+  a.agc = h->agc;
+  a.fd_prev = h->fd_prev;
+  a.st_hist = h->st_hist;
+  a.rds_hist = h->rds_hist;
+  a.clip_out = h->clip;
+  a.rds_count = h->rds_count;
+  a.rds_sched = h->t_rds.d_sched;
+  a.rds_sched_n = h->t_rds.d_count;
+  a.rds_group = h->t_rds.d_group;
+  a.rds_sched_stride = h->t_rds.stride;
+  return a;
+}
+
+static AudioArgs audio_args(Handle *h, int n, int mode, TimingSet *t) {
+  AudioArgs a{};
+  a.des = h->ddes;
+  a.par = h->dpar;
+  a.C = h->C;
+  a.n = n;
+  a.mode = mode;
+  a.lr_hist = h->lr_hist;
+  a.af_win = h->af_win;
+  a.af_iir = h->af_iir;
+  a.mono_win = h->mono_win;
+  a.mono_iir = h->mono_iir;
+  if (t) {
+    a.sched = t->d_sched;
+    a.sched_n = t->d_count;
+    a.group = t->d_group;
+    a.sched_stride = t->stride;
+  }
+  return a;
+}
+
+static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride) {
+  PllArgs a{};
+  a.des = h->ddes;
+  a.par = h->dpar;
+  a.C = h->C;
+  a.n = n;
+  a.st_parity = h->st_parity;
+  a.pilot = h->pilot;
+  a.pilot_stride = h->cfg.block;
+  a.mpx = mpx;
+  a.mpx_stride = mpx_stride;
+  a.st_hist = h->st_hist;
+  a.lraw = h->lraw;
+  a.rraw = h->rraw;
+  a.lr_stride = h->cfg.block;
+  a.st = h->st;
+  return a;
+}
+
+static RdsArgs rds_args(Handle *h) {
+  RdsArgs a{};
+  a.des = h->ddes;
+  a.C = h->C;
+  a.in = h->rds_in;
+  a.in_stride = h->rds_stride;
+  a.in_count = h->rds_count;
+  a.st = h->rds;
+  a.ring = h->ring;
+  a.block_index = h->block_index;
+  return a;
+}
+
+static int check_n(Handle *h, int n) {
+  if (n < 0 || n > h->cfg.block) {
+    h->err = "n exceeds the handle's block size";
+    return FMX_E_CAPACITY;
+  }
+  return FMX_OK;
+}
+
+static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *o) {
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if (!o || !o->d_pcm_l || !o->d_pcm_r || !o->d_pcm_count || !d_iq) {
+    h->err = "process_block: d_iq, d_pcm_l, d_pcm_r and d_pcm_count are required";
+    return FMX_E_INVALID;
+  }
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  const bool stereo = h->cfg.stereo != 0;
+  const bool rds = h->cfg.rds != 0;
+  if (n == 0) return FMX_OK;
+  if (rds && (rc = tset_advance(h, h->t_rds, n, nullptr)) != FMX_OK) return rc;
+  TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
+  int max_out = 0;
+  if ((rc = tset_advance(h, *tau, n, &max_out)) != FMX_OK) return rc;
+  float *mpx = o->d_mpx ? o->d_mpx : h->mpx;
+  const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
+  // ---- front end ----
+  {
+    FeArgs a = fe_args(h, n, h->M > 1 ? FE_IN_U8_DECIM : FE_IN_U8_DIRECT);
+    a.iq = d_iq;
+    a.iq_stride = iq_stride;
+    a.mpx_out = mpx;
+    a.mpx_stride = mpx_stride;
+    a.do_demod = 1;
+    if (stereo) {
+      a.pilot_out = h->pilot;
+      a.pilot_stride = h->cfg.block;
+    }
+    if (rds) {
+      a.rds_out = h->rds_in;
+      a.rds_stride = h->rds_stride;
+    }
+    a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
+    KTimer t(h, FMX_K_FRONTEND, h->stream);
+    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->stream)) != FMX_OK) {
+      h->err = "frontend launch failed";
+      return rc;
+    }
+  }
+  // ---- RDS on the second stream, concurrent with stereo/audio ----
+  if (rds) {
+    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    RdsArgs a = rds_args(h);
+    a.groups = o->d_groups;
+    a.groups_stride = o->d_groups ? o->groups_stride : 0;
+    a.group_count = o->d_group_count;
+    KTimer t(h, FMX_K_RDS, h->stream2);
+    if ((rc = launch_rds(a, h->stream2)) != FMX_OK) {
+      h->err = "rds launch failed";
+      return rc;
+    }
+  }
+  if (stereo) {
+    {
+      PllArgs a = pll_args(h, n, mpx, mpx_stride);
+      a.stereo_out = o->d_stereo;
+      a.pilot_tenths_out = o->d_pilot_tenths;
+      KTimer t(h, FMX_K_STEREO, h->stream);
+      if ((rc = launch_pll(a, h->stream)) != FMX_OK) {
+        h->err = "pll launch failed";
+        return rc;
+      }
+    }
+    {
+      AudioArgs a = audio_args(h, n, 0, &h->t_af);
+      a.in_l = h->lraw;
+      a.in_r = h->rraw;
+      a.in_stride = h->cfg.block;
+      a.out_l = o->d_pcm_l;
+      a.out_r = o->d_pcm_r;
+      a.out_stride = o->pcm_stride;
+      a.out_count = o->d_pcm_count;
+      a.cap = h->cfg.block;
+      a.clamp = 1;
+      KTimer t(h, FMX_K_AUDIO, h->stream);
+      if ((rc = launch_audio(a, h->stream)) != FMX_OK) {
+        h->err = "audio launch failed";
+        return rc;
+      }
+    }
+    h->st_parity ^= 1;
+  } else {
+    AudioArgs a = audio_args(h, n, 3, &h->t_mono);
+    a.in_l = mpx;
+    a.in_r = nullptr;
+    a.in_stride = mpx_stride;
+    a.out_l = o->d_pcm_l;
+    a.out_r = o->d_pcm_r;
+    a.out_stride = o->pcm_stride;
+    a.out_count = o->d_pcm_count;
+    a.cap = 1 << 30;
+    a.clamp = 1;
+    KTimer t(h, FMX_K_AUDIO, h->stream);
+    if ((rc = launch_audio(a, h->stream)) != FMX_OK) {
+      h->err = "audio launch failed";
+      return rc;
+    }
+  }
+  if (rds) {
+    HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  } else if (o->d_group_count) {
+    HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->stream));
+  }
+  if (!stereo) {
+    if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->stream));
+    if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->stream));
+  }
+  h->block_index++;
+  (void)max_out;
+  return FMX_OK;
+}
+
+} // namespace fmx
+
+using namespace fmx;
+
+static Handle *H(void *p) { return static_cast<Handle *>(p); }
+
+extern "C" {
+
+int fmx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int fmx_create(const fmx_config *cfg, int n_channels, int device, void **handle) {
+  if (!cfg || !handle) return FMX_E_INVALID;
+  Handle *h = nullptr;
+  int rc = create(cfg, n_channels, device, &h);
+  *handle = h;
+  return rc;
+}
+
+int fmx_destroy(void *handle) {
+  destroy(H(handle));
+  return FMX_OK;
+}
+
+const char *fmx_last_error(void *handle) { return handle ? H(handle)->err.c_str() : "null handle"; }
+
+int fmx_sync(void *handle) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(h->stream2));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FMX_OK;
+}
+
+int fmx_num_channels(void *handle) { return handle ? H(handle)->C : 0; }
+
+int fmx_reset(void *handle, int channel) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  if (channel < -1 || channel >= h->C) {
+    h->err = "channel out of range";
+    return FMX_E_INVALID;
+  }
+  const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
+  for (int c = c0; c < c1; ++c) {
+    int m = RS_DECIM | RS_DEMOD | RS_STEREO | RS_AF | RS_RDS;
+    if (h->agc_ready[static_cast<size_t>(c)]) m |= RS_AGC;
+    h->hmask[static_cast<size_t>(c)] |= m;
+    tset_reset_channel(h->t_af, c);
+    tset_reset_channel(h->t_mono, c);
+  }
+  return FMX_OK;
+}
+
+int fmx_set_param(void *handle, int channel, int key, int value) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  if (channel < -1 || channel >= h->C) {
+    h->err = "channel out of range";
+    return FMX_E_INVALID;
+  }
+  const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
+  for (int c = c0; c < c1; ++c) {
+    FmxChanParam &p = h->hpar[static_cast<size_t>(c)];
+    switch (key) {
+      case FMX_PARAM_BANDWIDTH_HZ: set_bandwidth(h, c, value); break;
+      case FMX_PARAM_BANDWIDTH_MODE: set_bandwidth(h, c, tef_bandwidth_hz(value)); break;
+      case FMX_PARAM_W0_HZ: h->w0[static_cast<size_t>(c)] = std::clamp(value, 0, 400000); break;
+      case FMX_PARAM_DEEMPHASIS: set_deemph(h, c, std::clamp(value, 0, 2)); break;
+      case FMX_PARAM_DSP_AGC: set_agc(h, c, std::clamp(value, 0, 2)); break;
+      case FMX_PARAM_BLEND:
+        p.blend = std::clamp(value, 0, 2);
+        h->par_dirty = true;
+        break;
+      case FMX_PARAM_FORCE_MONO:
+        p.force_mono = value != 0;
+        h->par_dirty = true;
+        break;
+      case FMX_PARAM_FORCE_STEREO:
+        p.force_stereo = value != 0;
+        h->par_dirty = true;
+        break;
+      default: h->err = "unknown parameter key"; return FMX_E_INVALID;
+    }
+  }
+  return FMX_OK;
+}
+
+int fmx_process_block(void *handle, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *out) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  return process_block(h, d_iq, iq_stride, n, out);
+}
+
+int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, float *d_out, int out_stride) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n_out)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (n_out == 0) return FMX_OK;
+  if (h->M == 1) {
+    h->err = "fmx_decimate needs iq_rate > dsp_rate";
+    return FMX_E_INVALID;
+  }
+  FeArgs a = fe_args(h, n_out, FE_IN_U8_DECIM);
+  a.iq = d_iq;
+  a.iq_stride = iq_stride;
+  a.bb_out = d_out;
+  a.bb_stride = out_stride;
+  a.do_demod = 0;
+  a.clip_out = nullptr;
+  KTimer t(h, FMX_K_FRONTEND, h->stream);
+  return launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->stream);
+}
+
+int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride, float *d_mono,
+              int mono_stride, int *d_mono_count) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (n == 0) return FMX_OK;
+  float *mpx = d_mpx ? d_mpx : h->mpx;
+  const int ms = d_mpx ? mpx_stride : h->cfg.block;
+  {
+    FeArgs a = fe_args(h, n, FE_IN_CF);
+    a.in_f = d_iq_cf;
+    a.in_stride = in_stride;
+    a.mpx_out = mpx;
+    a.mpx_stride = ms;
+    a.do_demod = 1;
+    KTimer t(h, FMX_K_FRONTEND, h->stream);
+    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+  }
+  if (d_mono) {
+    if ((rc = tset_advance(h, h->t_mono, n, nullptr)) != FMX_OK) return rc;
+    AudioArgs a = audio_args(h, n, 2, &h->t_mono);
+    a.in_l = mpx;
+    a.in_stride = ms;
+    a.out_l = d_mono;
+    a.out_r = d_mono;
+    a.out_stride = mono_stride;
+    a.out_count = d_mono_count;
+    a.cap = 1 << 30;
+    a.clamp = 0;
+    KTimer t(h, FMX_K_AUDIO, h->stream);
+    if ((rc = launch_audio(a, h->stream)) != FMX_OK) return rc;
+  } else if (d_mono_count) {
+    HIP_TRY(hipMemsetAsync(d_mono_count, 0, sizeof(int) * h->C, h->stream));
+  }
+  return FMX_OK;
+}
+
+int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_left, float *d_right, int lr_stride,
+               int *d_stereo, int *d_pilot_tenths) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (n == 0) return FMX_OK;
+  {
+    FeArgs a = fe_args(h, n, FE_IN_MPX);
+    a.in_f = d_mpx;
+    a.in_stride = mpx_stride;
+    a.pilot_out = h->pilot;
+    a.pilot_stride = h->cfg.block;
+    a.do_demod = 0;
+    KTimer t(h, FMX_K_FRONTEND, h->stream);
+    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+  }
+  {
+    PllArgs a = pll_args(h, n, d_mpx, mpx_stride);
+    a.stereo_out = d_stereo;
+    a.pilot_tenths_out = d_pilot_tenths;
+    KTimer t(h, FMX_K_STEREO, h->stream);
+    if ((rc = launch_pll(a, h->stream)) != FMX_OK) return rc;
+  }
+  {
+    AudioArgs a = audio_args(h, n, 4, nullptr);
+    a.in_l = h->lraw;
+    a.in_r = h->rraw;
+    a.in_stride = h->cfg.block;
+    a.lr_out_l = d_left;
+    a.lr_out_r = d_right;
+    a.lr_out_stride = lr_stride;
+    KTimer t(h, FMX_K_AUDIO, h->stream);
+    if ((rc = launch_audio(a, h->stream)) != FMX_OK) return rc;
+  }
+  h->st_parity ^= 1;
+  return FMX_OK;
+}
+
+int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_stride, int n, float *d_out_l,
+               float *d_out_r, int out_stride, int cap, int *d_count) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (n == 0 || cap <= 0) return FMX_OK;
+  // AFPostProcessor::process stops consuming input once outCapacity outputs
+  // are written; only the no-truncation case is supported here.
+  std::vector<ResampTiming> saved = h->t_af.groups;
+  int mx = 0;
+  if ((rc = tset_advance(h, h->t_af, n, &mx)) != FMX_OK) return rc;
+  if (mx > cap) {
+    h->t_af.groups = saved;
+    h->err = "fmx_afpost: outCapacity smaller than the produced sample count is not supported";
+    return FMX_E_CAPACITY;
+  }
+  AudioArgs a = audio_args(h, n, 1, &h->t_af);
+  a.in_l = d_left;
+  a.in_r = d_right;
+  a.in_stride = in_stride;
+  a.out_l = d_out_l;
+  a.out_r = d_out_r;
+  a.out_stride = out_stride;
+  a.out_count = d_count;
+  a.cap = cap;
+  a.clamp = 0;
+  KTimer t(h, FMX_K_AUDIO, h->stream);
+  return launch_audio(a, h->stream);
+}
+
+int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_group *d_groups, int groups_stride,
+            int *d_group_count) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (n == 0) {
+    if (d_group_count) HIP_TRY(hipMemsetAsync(d_group_count, 0, sizeof(int) * h->C, h->stream));
+    return FMX_OK;
+  }
+  if ((rc = tset_advance(h, h->t_rds, n, nullptr)) != FMX_OK) return rc;
+  {
+    FeArgs a = fe_args(h, n, FE_IN_MPX);
+    a.in_f = d_mpx;
+    a.in_stride = mpx_stride;
+    a.rds_out = h->rds_in;
+    a.rds_stride = h->rds_stride;
+    a.do_demod = 0;
+    KTimer t(h, FMX_K_FRONTEND, h->stream);
+    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+  }
+  RdsArgs a = rds_args(h);
+  a.groups = d_groups;
+  a.groups_stride = d_groups ? groups_stride : 0;
+  a.group_count = d_group_count;
+  KTimer t(h, FMX_K_RDS, h->stream);
+  rc = launch_rds(a, h->stream);
+  h->block_index++;
+  return rc;
+}
+
+int fmx_malloc(void *handle, void **d_ptr, size_t bytes) {
+  Handle *h = H(handle);
+  if (!h || !d_ptr) return FMX_E_INVALID;
+  HIP_TRY(hipSetDevice(h->device));
+  hipError_t e = hipMalloc(d_ptr, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    h->err = hipGetErrorString(e);
+    return FMX_E_NOMEM;
+  }
+  return FMX_OK;
+}
+int fmx_free(void *handle, void *d_ptr) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  HIP_TRY(hipFree(d_ptr));
+  return FMX_OK;
+}
+int fmx_memcpy_h2d(void *handle, void *d_dst, const void *h_src, size_t bytes) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FMX_OK;
+}
+int fmx_memcpy_d2h(void *handle, void *h_dst, const void *d_src, size_t bytes) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(h->stream2));
+  HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FMX_OK;
+}
+int fmx_memset(void *handle, void *d_ptr, int value, size_t bytes) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  HIP_TRY(hipMemsetAsync(d_ptr, value, bytes, h->stream));
+  return FMX_OK;
+}
+
+int fmx_timing_enable(void *handle, int enable) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  if (h->timing && !enable) {
+    hipStreamSynchronize(h->stream);
+    hipStreamSynchronize(h->stream2);
+    collect_timing(h);
+  }
+  h->timing = enable != 0;
+  for (int k = 0; k < FMX_K_COUNT; ++k) {
+    h->kms[k] = 0.0;
+    h->klaunch[k] = 0;
+  }
+  return FMX_OK;
+}
+
+int fmx_kernel_times(void *handle, double *ms, int *launches, int n) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  hipStreamSynchronize(h->stream);
+  hipStreamSynchronize(h->stream2);
+  collect_timing(h);
+  for (int k = 0; k < n && k < FMX_K_COUNT; ++k) {
+    if (ms) ms[k] = h->kms[k];
+    if (launches) launches[k] = h->klaunch[k];
+  }
+  return FMX_OK;
+}
+
+/* ---------------- synthetic input ---------------- */
+static uint16_t rds_crc10(uint16_t data) {
+  uint32_t reg = 0;
+  for (int i = 15; i >= 0; --i) {
+    const uint32_t bit = ((data >> i) & 1u) ^ ((reg >> 9) & 1u);
+    reg = (reg << 1) & 0x3FFu;
+    if (bit) reg ^= 0x1B9u; // g(x) = x^10+x^8+x^7+x^5+x^4+x^3+1
+  }
+  return static_cast<uint16_t>(reg);
+}
+
+// Known RDS test groups: PI = 0x1000 + ch, 0A PS groups
+// alternating with 2A RadioText groups.
+static void rds_group_words(uint32_t ch, int g, uint16_t w[4]) {
+  const uint16_t pi = static_cast<uint16_t>(0x1000u + ch);
+  const uint16_t pty = static_cast<uint16_t>(ch % 32u);
+  char ps[9];
+  std::snprintf(ps, sizeof(ps), "FM%05u ", static_cast<unsigned>(ch % 100000u));
+  char rt[96];
+  std::snprintf(rt, sizeof(rt), "MI355X channel %05u radiotext test pattern 0123456789 abcdefghij",
+                static_cast<unsigned>(ch % 100000u));
+  w[0] = pi;
+  if ((g & 1) == 0) { // 0A
+    const int seg = (g / 2) % 4;
+    w[1] = static_cast<uint16_t>((0u << 12) | (0u << 11) | (pty << 5) | (1u << 3) | static_cast<unsigned>(seg));
+    w[2] = 0xE0CD;
+    w[3] = static_cast<uint16_t>((static_cast<uint8_t>(ps[2 * seg]) << 8) | static_cast<uint8_t>(ps[2 * seg + 1]));
+  } else { // 2A
+    const int seg = (g / 2) % 16;
+    w[1] = static_cast<uint16_t>((2u << 12) | (0u << 11) | (pty << 5) | static_cast<unsigned>(seg));
+    w[2] = static_cast<uint16_t>((static_cast<uint8_t>(rt[4 * seg]) << 8) | static_cast<uint8_t>(rt[4 * seg + 1]));
+    w[3] = static_cast<uint16_t>((static_cast<uint8_t>(rt[4 * seg + 2]) << 8) |
+                                 static_cast<uint8_t>(rt[4 * seg + 3]));
+  }
+}
+
+int fmx_synth_rds_bits(const fmx_synth_config *cfg, uint32_t ch0, int n_ch, uint8_t *h_bits, uint16_t *h_groups) {
+  if (!cfg || n_ch < 0 || cfg->n_bits <= 0) return FMX_E_INVALID;
+  static const uint16_t kOffset[4] = {0x0FC, 0x198, 0x168, 0x1B4}; // A, B, C, D
+  const int nb = cfg->n_bits;
+  const int ng = nb / 104 + 1;
+  for (int ci = 0; ci < n_ch; ++ci) {
+    const uint32_t ch = ch0 + static_cast<uint32_t>(ci);
+    uint8_t prev = 0;
+    for (int g = 0; g < ng; ++g) {
+      uint16_t w[4];
+      rds_group_words(ch, g, w);
+      if (h_groups && g < nb / 104)
+        for (int k = 0; k < 4; ++k) h_groups[(static_cast<size_t>(ci) * (nb / 104) + g) * 4 + k] = w[k];
+      for (int blk = 0; blk < 4; ++blk) {
+        const uint32_t word = (static_cast<uint32_t>(w[blk]) << 10) | (rds_crc10(w[blk]) ^ kOffset[blk]);
+        for (int b = 25; b >= 0; --b) {
+          const int idx = g * 104 + blk * 26 + (25 - b);
+          if (idx >= nb) break;
+          const uint8_t d = static_cast<uint8_t>((word >> b) & 1u);
+          prev = static_cast<uint8_t>(d ^ prev); // differential encoding
+          if (h_bits) h_bits[static_cast<size_t>(ci) * nb + idx] = prev;
+        }
+      }
+    }
+  }
+  return FMX_OK;
+}
+
+int fmx_synth_host(const fmx_synth_config *cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
+                   const uint8_t *h_bits, uint8_t *h_out, size_t out_stride, int threads) {
+  if (!cfg || !h_out || n_ch < 0 || n_samples < 0) return FMX_E_INVALID;
+  if (threads < 1) threads = 1;
+  auto work = [&](int t) {
+    for (int ci = t; ci < n_ch; ci += threads) {
+      const uint32_t ch = ch0 + static_cast<uint32_t>(ci);
+      const fmx_synth_chan cp = fmx_synth_channel(cfg, ch);
+      const uint8_t *b = h_bits ? h_bits + static_cast<size_t>(ci) * cfg->n_bits : nullptr;
+      uint8_t *o = h_out + static_cast<size_t>(ci) * out_stride;
+      for (int i = 0; i < n_samples; ++i) fmx_synth_sample(cfg, ch, &cp, sample0 + i, b, o + 2 * static_cast<size_t>(i));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  return FMX_OK;
+}
+
+int fmx_synth_device(void *handle, const fmx_synth_config *cfg, uint32_t ch0, int n_ch, int64_t sample0,
+                     int n_samples, const uint8_t *d_bits, uint8_t *d_out, size_t out_stride) {
+  Handle *h = H(handle);
+  if (!h || !cfg) return FMX_E_INVALID;
+  return launch_synth(*cfg, ch0, n_ch, sample0, n_samples, d_bits, d_out, out_stride, h->stream);
+}
+
+/* ---------------- diagnostics (no GPU needed) ---------------- */
+int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
+  if (!cfg) return FMX_E_INVALID;
+  FmxDesign *d = new FmxDesign();
+  DesignExtras ex;
+  std::string err;
+  int rc = design_build(*cfg, d, &ex, &err);
+  if (rc != FMX_OK) {
+    delete d;
+    return rc;
+  }
+  std::vector<float> v;
+  switch (which) {
+    case 0: v.assign(d->dec_taps_raw, d->dec_taps_raw + d->dec_len); break;
+    case 1: {
+      const int sel = bandwidth_select(cfg->bandwidth_hz, std::clamp(cfg->w0_bandwidth_hz, 0, 400000));
+      const int idx = (sel == 0) ? FMX_IQ_CTOR : sel;
+      v.assign(d->iq_taps[idx], d->iq_taps[idx] + d->iq_len[idx]);
+      break;
+    }
+    case 2: v.assign(d->pilot_taps, d->pilot_taps + d->pilot_len); break;
+    case 3: v.assign(d->lr_taps, d->lr_taps + FMX_LR_LEN); break;
+    case 4: v = ex.proto_af; break;
+    case 5: v = ex.proto_rds; break;
+    case 6: v.assign(d->rds_fir, d->rds_fir + FMX_RDS_FIR); break;
+    case 7: v = ex.rrc; break;
+    case 8: v = ex.rrc_d; break;
+    default: delete d; return FMX_E_INVALID;
+  }
+  delete d;
+  const int n = static_cast<int>(v.size());
+  if (out) std::memcpy(out, v.data(), sizeof(float) * static_cast<size_t>(std::min(n, cap)));
+  return n;
+}
+
+/* host simulation of the resampler schedule (tests) */
+int fmx_resamp_schedule(float del, int n_in, int *packed, float *mu, int cap) {
+  ResampTiming t;
+  timing_reset(t);
+  t.del = del;
+  std::vector<FmxSched> s(static_cast<size_t>(std::max(cap, 1)));
+  int k = timing_run(t, n_in, s.data(), cap);
+  for (int i = 0; i < std::min(k, cap); ++i) {
+    if (packed) packed[i] = s[static_cast<size_t>(i)].packed;
+    if (mu) mu[i] = s[static_cast<size_t>(i)].mu;
+  }
+  return k;
+}
+
+} // extern "C"

@@ -1,0 +1,133 @@
+// fmx_design.h -- filter designs, per-channel parameters and per-channel state
+// layout of the MI355X FM demodulator (shared by host code and HIP kernels).
+//
+// Every constant here is what one reference object computes in its
+// constructor / setter; the host computes them once per handle
+// (fmx_design.cpp) and uploads them to HBM, where all channels share them.
+#ifndef FMX_DESIGN_H
+#define FMX_DESIGN_H
+
+#include <stdint.h>
+
+#define FMX_MAX_DEC 512      // M * taps_per_phase (liquid_primitives.cpp:388)
+#define FMX_IQ_DESIGNS 31    // 30 XDR bandwidth filters + the FMDemod ctor filter
+#define FMX_IQ_CTOR 30       // index of the ctor filter (fm_demod.cpp:103-105)
+#define FMX_IQ_MAXLEN 121
+#define FMX_PILOT_MAX 511    // stereo_decoder.cpp:98 clamp
+#define FMX_LR_LEN 121       // stereo_decoder.cpp:110-111
+#define FMX_NPFB 32          // resamp_rrrf / symsync filter-bank size
+#define FMX_AF_SUB 24        // 2*m, m = 12 (liquid_primitives.h:145)
+#define FMX_RDS_RS_SUB 26    // 2*m, m = 13 (subcarrier.cpp:45)
+#define FMX_RDS_FIR 255      // subcarrier.cpp:101
+#define FMX_RDS_DECIM 24     // subcarrier.hh:205-206
+#define FMX_RDS_NACC 11      // ceil(255 / 24) streaming partial sums
+#define FMX_SS_SUB 18        // (2*32*3*3+1 - 1) / 32
+#define FMX_HIST 512         // stereo MPX history (>= pilot taps - 1 and delay line)
+#define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
+
+typedef struct {
+  float x, y;
+} float2_t;
+
+typedef struct {
+  // rates / geometry
+  int M, fs, out_rate, block;
+  // ComplexDecimator (liquid_primitives.cpp:370-403): taps already multiplied
+  // by the u8 normalisation 1/127.5, plus the firdecim scale 2*fc.
+  int dec_len, dec_tpp;
+  float dec_scale;
+  float dec_taps[FMX_MAX_DEC];
+  float dec_taps_raw[FMX_MAX_DEC];
+  // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
+  int iq_len[FMX_IQ_DESIGNS];
+  float iq_scale[FMX_IQ_DESIGNS];
+  float iq_taps[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN];
+  float fd_ref;          // 1 / (2 pi kf), kf = 75 kHz / Fs
+  float deemph_alpha[2]; // 50 us, 75 us at out_rate (fm_demod.cpp:119-131)
+  // StereoDecoder (stereo_decoder.cpp:25-63)
+  int pilot_len, delay_len; // delay_len = delaySamples + 1 (ring size)
+  float pilot_taps[FMX_PILOT_MAX];
+  float lr_scale;
+  float lr_taps[FMX_LR_LEN];
+  float nominal, pll_min, pll_max, pll_alpha, pll_beta;
+  uint32_t pll_dtheta0;
+  float blend_attack[3], blend_release[3], gate[3];
+  // resamplers: branch-major taps h[b][n] = proto[b + n*32]
+  float af_h[FMX_NPFB * FMX_AF_SUB];
+  float rds_rs_h[FMX_NPFB * FMX_RDS_RS_SUB];
+  float af_del, rds_del;
+  // RDS subcarrier (subcarrier.cpp:94-106, liquid_wrappers.cpp)
+  float rds_fir[FMX_RDS_FIR];
+  float rds_fir_scale;
+  float agc_bw, agc_g0;
+  uint32_t rds_dtheta0;
+  float rds_alpha, rds_beta;
+  float ss_mf[FMX_NPFB * FMX_SS_SUB];  // [b][n] = h[b + n*32]
+  float ss_dmf[FMX_NPFB * FMX_SS_SUB];
+  float ss_b0, ss_a1, ss_a2; // loop filter (normalised by a0; b1 = b2 = 0)
+  float ss_rate_adj;
+  float psk_xr1, psk_xi1; // cexpjf(pi) of the PSK2 modem
+} FmxDesign;
+
+// Per-channel settable parameters (reference setters), uploaded on change.
+typedef struct {
+  int iqsel;       // index into iq_* designs
+  int agc;         // 0 off, 1 fast, 2 slow
+  int blend;       // 0 soft, 1 normal, 2 aggressive
+  int force_mono;
+  int force_stereo;
+  int deemph;      // 0 -> 50us, 1 -> 75us, 2 -> off
+  int pad0, pad1;
+} FmxChanParam;
+
+// StereoDecoder scalars (stereo_decoder.h:27-50)
+typedef struct {
+  uint32_t theta, dtheta; // liquid NCO (fixed point)
+  float pilot_band_mag, mpx_mag, pilot_i, pilot_q, pilot_magnitude, blend;
+  float pll_freq, pll_phase;
+  int pilot_count, loss_count, detected, level;
+} FmxStereoState;
+
+// RDS per-channel state (SubcarrierSet + BlockStream), one lane per channel.
+typedef struct {
+  // NCO + quad-phase wrapper (liquid_wrappers.cpp:271-312), stream 0
+  uint32_t theta, dtheta;
+  float prev_f0, phase0;
+  uint32_t sample_since_reset;
+  uint32_t ring_pos;       // total mixed samples written to the ring
+  int rebuild;             // decimation phase changed by a reset
+  // streaming FIR partial sums for the next 11 decimation instants
+  float acc_re[FMX_RDS_NACC], acc_im[FMX_RDS_NACC];
+  // AGC (agc_crcf)
+  float agc_g, agc_y2p;
+  // symsync
+  float ss_win_re[FMX_SS_SUB], ss_win_im[FMX_SS_SUB];
+  int ss_mf_valid;         // pushes since the matched-filter bank was reset
+  float ss_rate, ss_del, ss_tau, ss_q_hat, ss_v1, ss_v2;
+  int ss_b, ss_decim;
+  // biphase / delta decoders
+  float bi_prev_re, bi_prev_im, bi_even, bi_odd;
+  uint32_t bi_clock, bi_polarity;
+  int delta_prev;
+  // BlockStream
+  uint32_t bs_bitcount, bs_until_next, bs_reg, bs_err_mask_lo, bs_err_mask_hi;
+  int bs_expected, bs_in_sync, bs_err_ptr;
+  uint32_t bs_pulse_pos[4];
+  int bs_pulse_off[4];
+  uint32_t bs_blk_raw[4];
+  uint16_t bs_blk_data[4];
+  uint8_t bs_blk_flags[4]; // bit0 received, bit1 had_errors
+  uint32_t bs_bits_since_lost;
+  uint32_t pad;
+} FmxRdsState;
+
+// Resampler output schedule entry (host-simulated liquid resamp timing):
+// y = (1-mu) * y0 + mu * y1 with
+//   interp  : y0 = branch b of window(i),   y1 = branch b+1 of window(i)
+//   boundary: y0 = branch 31 of window(i-1), y1 = branch 0 of window(i)
+typedef struct {
+  int packed; // i | (b << 16) | (boundary << 24)
+  float mu;
+} FmxSched;
+
+#endif

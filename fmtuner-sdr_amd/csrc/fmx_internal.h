@@ -1,0 +1,169 @@
+// fmx_internal.h -- host-side internals of libfmx (not part of the ABI).
+#ifndef FMX_INTERNAL_H
+#define FMX_INTERNAL_H
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/fmx.h"
+#include "fmx_design.h"
+
+namespace fmx {
+
+// ---- design (fmx_design.cpp) ----
+struct DesignExtras {
+  std::vector<float> proto_af, proto_rds, rrc, rrc_d;
+};
+void firdes_kaiser(unsigned n, float fc, float As, float mu, float *h);
+uint32_t nco_constrain(float theta);
+int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::string *err);
+int bandwidth_select(int bw_hz, int w0);
+int tef_bandwidth_hz(int mode);
+
+// liquid resamp_rrrf timing state (float tau, interp/boundary), simulated on
+// the host because it does not depend on the signal.
+struct ResampTiming {
+  float tau = 0.0f, bf = 0.0f, mu = 0.0f, del = 1.0f;
+  int b = 0, state = 0;
+};
+void timing_reset(ResampTiming &t);
+int timing_run(ResampTiming &t, int n_in, FmxSched *out, int cap);
+bool timing_equal(const ResampTiming &a, const ResampTiming &b);
+
+// ---- kernel argument blocks (fmx_kernels.hip) ----
+enum FeInMode { FE_IN_U8_DECIM = 0, FE_IN_CF = 1, FE_IN_U8_DIRECT = 2, FE_IN_MPX = 3 };
+
+struct FeArgs {
+  const FmxDesign *des;
+  const FmxChanParam *par;
+  int C, n, in_mode;
+  // inputs
+  const uint8_t *iq;
+  size_t iq_stride;
+  const float *in_f; // complex (FE_IN_CF) or mpx (FE_IN_MPX)
+  int in_stride;
+  // outputs
+  float *bb_out;     // complex decimator output (fmx_decimate), may be null
+  int bb_stride;
+  float *mpx_out;
+  int mpx_stride;
+  float *pilot_out;  // null = no pilot BPF
+  int pilot_stride;
+  float *rds_out;    // null = no RDS resampling
+  int rds_stride;
+  int *rds_count;    // [C]
+  float *clip_out;   // [C]
+  // stages
+  int do_demod;      // run DC + IQ FIR + AGC + discriminator
+  int st_parity;     // stereo history ping-pong index (read), writes 1 - parity
+  // state
+  uint8_t *dec_hist;
+  int *dec_valid;
+  float *dc_v;       // [C][2]
+  float2_t *iq_hist; // [C][FMX_IQ_MAXLEN-1]
+  float *agc;        // [C][2]
+  float *fd_prev;    // [C][2]
+  float *st_hist;    // [2][C][FMX_HIST]
+  float *rds_hist;   // [C][32]
+  // schedules
+  const FmxSched *rds_sched; // [groups][rds_sched_stride]
+  const int *rds_sched_n;    // [groups]
+  const int *rds_group;      // [C]
+  int rds_sched_stride;
+};
+
+struct PllArgs {
+  const FmxDesign *des;
+  const FmxChanParam *par;
+  int C, n, st_parity;
+  const float *pilot;
+  int pilot_stride;
+  const float *mpx;
+  int mpx_stride;
+  const float *st_hist; // [2][C][FMX_HIST]
+  float *lraw, *rraw;
+  int lr_stride;
+  FmxStereoState *st;
+  int *stereo_out, *pilot_tenths_out;
+};
+
+struct AudioArgs {
+  const FmxDesign *des;
+  const FmxChanParam *par;
+  int C, n, mode; // mode 0 stereo (LR FIR + AF), 1 AF only, 2 mono (FMDemod), 3 mono pipeline
+  int cap;
+  const float *in_l, *in_r;
+  int in_stride;
+  float *out_l, *out_r;
+  int out_stride;
+  int *out_count;
+  float *lr_hist;  // [C][2][FMX_LR_LEN-1]
+  float *af_win;   // [C][2][32]
+  float *af_iir;   // [C][4]
+  float *mono_win; // [C][32]
+  float *mono_iir; // [C][2]
+  float *lr_out_l, *lr_out_r; // optional filtered L/R at dsp rate (fmx_stereo)
+  int lr_out_stride;
+  const FmxSched *sched; // [groups][sched_stride]
+  const int *sched_n;
+  const int *group; // [C]
+  int sched_stride;
+  int clamp;
+};
+
+struct RdsArgs {
+  const FmxDesign *des;
+  int C;
+  const float *in; // 171 kHz samples
+  int in_stride;
+  const int *in_count; // [C]
+  FmxRdsState *st;
+  float *ring; // [C][FMX_RDS_RING][2]
+  fmx_rds_group *groups;
+  int groups_stride;
+  int *group_count;
+  uint32_t block_index;
+};
+
+// launchers (fmx_kernels.hip); stream is a hipStream_t
+int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream);
+int launch_pll(const PllArgs &a, void *stream);
+int launch_audio(const AudioArgs &a, void *stream);
+int launch_rds(const RdsArgs &a, void *stream);
+int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
+                 const uint8_t *bits, uint8_t *out, size_t out_stride, void *stream);
+struct ResetArgs {
+  const FmxDesign *des;
+  int C;
+  const int *mask; // [C] bitmask of parts to reset
+  FmxStereoState *st;
+  FmxRdsState *rds;
+  float *ring;
+  uint8_t *dec_hist;
+  int *dec_valid;
+  float *dc_v;
+  float2_t *iq_hist;
+  float *agc;
+  float *fd_prev;
+  float *st_hist;
+  float *lr_hist, *af_win, *af_iir, *mono_win, *mono_iir;
+  float *rds_hist;
+};
+enum ResetParts {
+  RS_DECIM = 1,    // ComplexDecimator::reset
+  RS_DEMOD = 2,    // FMDemod::reset (DC, IQ FIR, discriminator, mono chain)
+  RS_AGC = 4,      // AGC re-init (FMDemod::reset when ready, setDspAgcMode)
+  RS_STEREO = 8,   // StereoDecoder::reset
+  RS_AF = 16,      // AFPostProcessor::reset
+  RS_RDS = 32,     // RDSDecoder::reset (symsync + NCO + block stream)
+  RS_IQFIR = 64,   // IQ FIR re-created (setBandwidthHz)
+  RS_DEEMPH = 128, // de-emphasis IIRs re-created (setDeemphasis)
+  RS_CREATE = 256  // object construction (everything, incl. RDS resampler/AGC)
+};
+int launch_reset(const ResetArgs &a, void *stream);
+
+} // namespace fmx
+
+#endif

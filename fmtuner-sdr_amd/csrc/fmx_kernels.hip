@@ -1,0 +1,1480 @@
+// fmx_kernels.hip -- CDNA4 (gfx950) kernels of the many-channel FM demodulator.
+//
+// Four hot kernels per reference block:
+//
+//  k_frontend  one workgroup per channel, 256 threads, the block processed in
+//              chunks of 768 DSP samples; every stage is sample-parallel:
+//                u8 IQ -> ComplexDecimator (M x 28-tap polyphase FIR, IQ staged
+//                in LDS as fp16 pairs in phase-major layout)       liquid_primitives.cpp:461-499
+//                -> DC blockers (affine scan over the chunk)        fm_demod.cpp:186-188
+//                -> IQ FIR 81/121 taps                              fm_demod.cpp:190-191
+//                -> [AGC, serial]  -> discriminator (atan2)         fm_demod.cpp:192-195
+//                -> 19 kHz pilot band-pass (305 taps)               stereo_decoder.cpp:229-230
+//                -> 240k->171k RDS resampler (host timing schedule) subcarrier.cpp:117-147
+//  k_pll       one lane per channel (64 channels per wave): the nonlinear
+//              per-sample recurrences of StereoDecoder::processAudio
+//              (PLL, envelopes, blend) and the L-R matrix              stereo_decoder.cpp:226-288
+//  k_audio     one workgroup per channel: L/R 121-tap FIRs, 32 kHz
+//              resampler, de-emphasis + DC block, clamp               af_post_processor.cpp:47-78
+//  k_rds       one lane per channel: 57 kHz mix-down, 255-tap FIR as 11
+//              streaming partial sums, AGC, symbol sync, PSK2 Costas loop,
+//              biphase/delta decoding and redsea block sync            subcarrier.cpp:153-235,
+//                                                                      block_sync.cpp:254-313
+//
+// Build with -ffp-contract=off: wherever the reference's arithmetic order is
+// reproduced (IIRs, PLL, resamplers, RDS FIR) products and sums must round
+// separately.  The large FIRs use explicit fmaf.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include "fmx_internal.h"
+#include "fmx_synth.h"
+
+namespace fmx {
+
+#define FE_T 768       // DSP samples per frontend chunk (256 threads x 3)
+#define FE_HALO_IQ 120 // >= longest IQ FIR - 1
+#define AU_T 768
+#define AU_HALO 120
+#define AU_RHALO 32
+#define AU_MAXOUT 256
+#define PLL_T 64
+
+static constexpr float kPiF = 3.14159265358979323846f;
+
+/* ------------------------------------------------------------------ */
+/* liquid NCO fixed-point helpers (nco.proto.c restated)               */
+__device__ __forceinline__ uint32_t d_nco_constrain(float x) {
+  const float p = (float)((double)x * 0.159154943091895);
+  float fpart = p - truncf(p);
+  if (fpart < 0.0f) fpart = (float)((double)fpart + 1.0);
+  const float s = fpart * 4294967296.0f;
+  return (s >= 4294967296.0f) ? 0u : (uint32_t)s;
+}
+__device__ __forceinline__ float d_nco_phase(uint32_t theta) {
+  return (float)(6.283185307179586 * (double)(float)theta / 4294967296.0);
+}
+__device__ __forceinline__ float d_clamp(float v, float lo, float hi) {
+  return (v < lo) ? lo : ((hi < v) ? hi : v);
+}
+
+/* ================================================================== */
+/* k_frontend                                                         */
+/* ================================================================== */
+struct FeShared {
+  float carry_i, carry_q; // DC blocker v of the last processed sample
+  float fd_re, fd_im;     // discriminator r_prev (last IQ FIR / AGC output)
+  float wave_a[4], wave_bi[4], wave_bq[4];
+  int clip;
+  int e_begin, e_end;
+};
+
+// Decimator: outputs j = 3*tid + r of the chunk.  inq is phase-major:
+// inq[ph * Q + q] holds input li = q*M + ph.
+template <int M, int TPP>
+__device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const float *__restrict__ taps, int tid,
+                                            float (&ai)[3], float (&aq)[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    ai[r] = 0.0f;
+    aq[r] = 0.0f;
+  }
+#pragma unroll
+  for (int p = 0; p < M; ++p) {
+    const __half2 *row = inq + (M - 1 - p) * Q + 3 * tid + (TPP - 1);
+#pragma unroll
+    for (int s = -(TPP - 1); s <= 2; ++s) {
+      const __half2 hv = row[s];
+      const float xi = __low2float(hv);
+      const float xq = __high2float(hv);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int qq = r - s;
+        if (qq >= 0 && qq < TPP) {
+          const float h = taps[qq * M + p];
+          ai[r] = fmaf(h, xi, ai[r]);
+          aq[r] = fmaf(h, xq, aq[r]);
+        }
+      }
+    }
+  }
+}
+
+// Real-tap FIR on a complex LDS signal: outputs at x[base + 3*tid + r].
+template <int L>
+__device__ __forceinline__ void fir_c3(const float2 *x, int base, const float *__restrict__ h, float (&zr)[3],
+                                       float (&zi)[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    zr[r] = 0.0f;
+    zi[r] = 0.0f;
+  }
+#pragma unroll
+  for (int s = -(L - 1); s <= 2; ++s) {
+    const float2 v = x[base + s];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int k = r - s;
+      if (k >= 0 && k < L) {
+        zr[r] = fmaf(h[k], v.x, zr[r]);
+        zi[r] = fmaf(h[k], v.y, zi[r]);
+      }
+    }
+  }
+}
+
+// Real FIR of runtime length P on a real LDS signal, 3 outputs per thread.
+__device__ __forceinline__ void fir_r3(const float *x, int base, const float *__restrict__ h, int P,
+                                       float (&z)[3]) {
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+  // s = -(P-1), -(P-2): only r = 2 / r >= 1 valid
+  {
+    const float v = x[base - (P - 1)];
+    a2 = fmaf(h[P - 1], v, a2);
+  }
+  {
+    const float v = x[base - (P - 2)];
+    a1 = fmaf(h[P - 1], v, a1);
+    a2 = fmaf(h[P - 2], v, a2);
+  }
+#pragma unroll 8
+  for (int s = -(P - 3); s <= 0; ++s) {
+    const float v = x[base + s];
+    a0 = fmaf(h[-s], v, a0);
+    a1 = fmaf(h[1 - s], v, a1);
+    a2 = fmaf(h[2 - s], v, a2);
+  }
+  {
+    const float v = x[base + 1];
+    a1 = fmaf(h[0], v, a1);
+    a2 = fmaf(h[1], v, a2);
+  }
+  {
+    const float v = x[base + 2];
+    a2 = fmaf(h[0], v, a2);
+  }
+  z[0] = a0;
+  z[1] = a1;
+  z[2] = a2;
+}
+
+// Resampler output from a window accessor; reference dot order (oldest first)
+template <int SUB, typename Get>
+__device__ __forceinline__ float resamp_out(const float *__restrict__ hb, int packed, float mu, Get get) {
+  const int i = packed & 0xFFFF;
+  const int b = (packed >> 16) & 0xFF;
+  const int boundary = (packed >> 24) & 1;
+  float y0 = 0.0f, y1 = 0.0f;
+  if (!boundary) {
+    const float *h0 = hb + b * SUB;
+    const float *h1 = hb + (b + 1) * SUB;
+#pragma unroll
+    for (int m = 0; m < SUB; ++m) {
+      const float v = get(i - (SUB - 1) + m);
+      const float p0 = h0[SUB - 1 - m] * v;
+      const float p1 = h1[SUB - 1 - m] * v;
+      y0 = y0 + p0;
+      y1 = y1 + p1;
+    }
+  } else {
+    const float *h0 = hb + (FMX_NPFB - 1) * SUB;
+    const float *h1 = hb;
+#pragma unroll
+    for (int m = 0; m < SUB; ++m) {
+      const float v0 = get(i - 1 - (SUB - 1) + m);
+      const float v1 = get(i - (SUB - 1) + m);
+      const float p0 = h0[SUB - 1 - m] * v0;
+      const float p1 = h1[SUB - 1 - m] * v1;
+      y0 = y0 + p0;
+      y1 = y1 + p1;
+    }
+  }
+  const float w0 = (1.0f - mu) * y0;
+  const float w1 = mu * y1;
+  return w0 + w1;
+}
+
+__device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((s[mid].packed & 0xFFFF) < i) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int M, int TPP>
+__global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int L = (M > 1) ? M * TPP : 1;
+  constexpr int Q = FE_T + ((M > 1) ? TPP : 1);
+  constexpr int IN_BYTES = (M > 1) ? M * Q * 4 : 0;
+  constexpr int YB_BYTES = (FE_T + 1) * 8;
+  constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
+  __half2 *inq = reinterpret_cast<__half2 *>(smem);
+  float2 *yb = reinterpret_cast<float2 *>(smem);
+  float2 *xin = reinterpret_cast<float2 *>(smem + R0);
+  float *mx = reinterpret_cast<float *>(smem + R0 + (FE_HALO_IQ + FE_T) * 8);
+  FeShared *sh = reinterpret_cast<FeShared *>(smem + R0 + (FE_HALO_IQ + FE_T) * 8 + (FMX_HIST + FE_T) * 4);
+
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const FmxDesign *__restrict__ D = a.des;
+  const int n = a.n;
+  const FmxChanParam par = a.par[c];
+  const int iqL = D->iq_len[par.iqsel];
+  const float *__restrict__ iqh = D->iq_taps[par.iqsel];
+  const float iqscale = D->iq_scale[par.iqsel];
+  const bool demod = a.do_demod != 0;
+  const bool pilot = a.pilot_out != nullptr;
+  const bool rds = a.rds_out != nullptr;
+  const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
+  const float dc_c = -dc_a1;
+
+  // ---- load carried state ----
+  if (demod) {
+    for (int h = tid; h < FE_HALO_IQ; h += 256) {
+      const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
+      xin[h] = make_float2(v.x, v.y);
+    }
+    if (tid == 0) {
+      sh->carry_i = a.dc_v[2 * c];
+      sh->carry_q = a.dc_v[2 * c + 1];
+      sh->fd_re = a.fd_prev[2 * c];
+      sh->fd_im = a.fd_prev[2 * c + 1];
+    }
+  }
+  if (pilot || rds || demod) {
+    const float *hist = a.st_hist + ((size_t)a.st_parity * a.C + c) * FMX_HIST;
+    for (int h = tid; h < FMX_HIST; h += 256) mx[h] = pilot ? hist[h] : 0.0f;
+  }
+  if (tid == 0) sh->clip = 0;
+  float agc_g = 1.0f, agc_y2p = 1.0f;
+  if (demod && par.agc != 0 && tid == 0) {
+    agc_g = a.agc[2 * c];
+    agc_y2p = a.agc[2 * c + 1];
+  }
+  const float agc_bw = (par.agc == 1) ? 0.01f : 0.001f;
+  int dec_valid = 0;
+  if (a.in_mode == FE_IN_U8_DECIM) dec_valid = a.dec_valid[c];
+  const uint16_t *iq16 = reinterpret_cast<const uint16_t *>(a.iq + (size_t)c * a.iq_stride);
+  const uint8_t *dhist = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
+  // RDS schedule of this channel's timing group
+  const FmxSched *sched = nullptr;
+  int sched_n = 0;
+  if (rds) {
+    const int g = a.rds_group[c];
+    sched = a.rds_sched + (size_t)g * a.rds_sched_stride;
+    sched_n = a.rds_sched_n[g];
+  }
+  const float *rhist = a.rds_hist + (size_t)c * 32;
+  int e_pos = 0;
+  __syncthreads();
+
+  for (int n0 = 0; n0 < n; n0 += FE_T) {
+    const int cnt = min(FE_T, n - n0);
+    // ================= baseband x[j] =================
+    if (a.in_mode == FE_IN_U8_DECIM) {
+      if constexpr (M > 1) {
+        const long g0 = (long)n0 * M - (L - 1);
+        const int span = (cnt - 1) * M + L;
+        for (int li = tid; li < span; li += 256) {
+          const long g = g0 + li;
+          float fi = 0.0f, fq = 0.0f;
+          if (g >= 0) {
+            const uint16_t w = iq16[g];
+            fi = (float)(w & 255) - 127.5f;
+            fq = (float)(w >> 8) - 127.5f;
+          } else {
+            const int h = (L - 1) + (int)g;
+            if (h >= (L - 1) - dec_valid) {
+              fi = (float)dhist[2 * h] - 127.5f;
+              fq = (float)dhist[2 * h + 1] - 127.5f;
+            }
+          }
+          inq[(li % M) * Q + li / M] = __floats2half2_rn(fi, fq);
+        }
+        __syncthreads();
+        float ai[3], aq[3];
+        fe_decimate<M, TPP>(inq, Q, D->dec_taps, tid, ai, aq);
+        int myclip = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int j = 3 * tid + r;
+          if (j < cnt) {
+            const float yr = ai[r] * D->dec_scale;
+            const float yi = aq[r] * D->dec_scale;
+            if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
+            xin[FE_HALO_IQ + j] = make_float2(yr, yi);
+            if (a.bb_out) {
+              float *o = a.bb_out + (size_t)c * a.bb_stride + 2 * (size_t)(n0 + j);
+              o[0] = yr;
+              o[1] = yi;
+            }
+          }
+        }
+        if (myclip) atomicAdd(&sh->clip, myclip);
+        __syncthreads(); // inq aliases yb
+      }
+    } else if (a.in_mode == FE_IN_CF) {
+      int myclip = 0;
+      for (int j = tid; j < cnt; j += 256) {
+        const float *p = a.in_f + (size_t)c * a.in_stride + 2 * (size_t)(n0 + j);
+        const float xr = p[0], xi = p[1];
+        if (fabsf(xr) >= 0.995f || fabsf(xi) >= 0.995f) myclip++;
+        xin[FE_HALO_IQ + j] = make_float2(xr, xi);
+      }
+      if (myclip) atomicAdd(&sh->clip, myclip);
+    } else if (a.in_mode == FE_IN_U8_DIRECT) {
+      int myclip = 0;
+      const uint8_t *p = a.iq + (size_t)c * a.iq_stride;
+      for (int j = tid; j < cnt; j += 256) {
+        const uint8_t ib = p[2 * (size_t)(n0 + j)], qb = p[2 * (size_t)(n0 + j) + 1];
+        if (ib == 0 || ib == 255 || qb == 0 || qb == 255) myclip++;
+        xin[FE_HALO_IQ + j] = make_float2(((float)ib - 127.0f) / 127.5f, ((float)qb - 127.0f) / 127.5f);
+      }
+      if (myclip) atomicAdd(&sh->clip, myclip);
+    }
+    __syncthreads();
+
+    if (demod) {
+      // ================= DC blockers: affine scan =================
+      // v_k = x_k - a1 * v_{k-1} (DF-II); y_k = v_k - v_{k-1}
+      float A = 1.0f, BI = 0.0f, BQ = 0.0f;
+      float2 xv[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int j = 3 * tid + r;
+        xv[r] = (j < cnt) ? xin[FE_HALO_IQ + j] : make_float2(0.0f, 0.0f);
+        if (j < cnt) {
+          BI = xv[r].x + dc_c * BI;
+          BQ = xv[r].y + dc_c * BQ;
+          A = dc_c * A;
+        }
+      }
+      // inclusive wave scan of maps (later o earlier)
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float pA = __shfl_up(A, d);
+        const float pI = __shfl_up(BI, d);
+        const float pQ = __shfl_up(BQ, d);
+        if (lane >= d) {
+          BI = A * pI + BI;
+          BQ = A * pQ + BQ;
+          A = A * pA;
+        }
+      }
+      if (lane == 63) {
+        sh->wave_a[wave] = A;
+        sh->wave_bi[wave] = BI;
+        sh->wave_bq[wave] = BQ;
+      }
+      // exclusive within the wave
+      float eA = __shfl_up(A, 1), eI = __shfl_up(BI, 1), eQ = __shfl_up(BQ, 1);
+      if (lane == 0) {
+        eA = 1.0f;
+        eI = 0.0f;
+        eQ = 0.0f;
+      }
+      __syncthreads();
+      // prefix of earlier waves applied to the chunk carry
+      float vI = sh->carry_i, vQ = sh->carry_q;
+      for (int w = 0; w < wave; ++w) {
+        vI = sh->wave_a[w] * vI + sh->wave_bi[w];
+        vQ = sh->wave_a[w] * vQ + sh->wave_bq[w];
+      }
+      vI = eA * vI + eI;
+      vQ = eA * vQ + eQ;
+      // serial recompute in the reference order
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int j = 3 * tid + r;
+        if (j < cnt) {
+          const float tI = dc_a1 * vI;
+          const float tQ = dc_a1 * vQ;
+          const float nI = xv[r].x - tI;
+          const float nQ = xv[r].y - tQ;
+          xin[FE_HALO_IQ + j] = make_float2(nI - vI, nQ - vQ);
+          vI = nI;
+          vQ = nQ;
+          if (j == cnt - 1) {
+            sh->carry_i = nI;
+            sh->carry_q = nQ;
+          }
+        }
+      }
+      __syncthreads();
+      // ================= IQ FIR =================
+      {
+        float zr[3], zi[3];
+        if (iqL == 121) fir_c3<121>(xin, FE_HALO_IQ + 3 * tid, iqh, zr, zi);
+        else fir_c3<81>(xin, FE_HALO_IQ + 3 * tid, iqh, zr, zi);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int j = 3 * tid + r;
+          if (j < cnt) yb[1 + j] = make_float2(zr[r] * iqscale, zi[r] * iqscale);
+        }
+        if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
+      }
+      __syncthreads();
+      // ================= AGC (serial, only when enabled) =================
+      if (par.agc != 0) {
+        if (tid == 0) {
+          for (int j = 0; j < cnt; ++j) {
+            const float2 x = yb[1 + j];
+            const float yr = x.x * agc_g, yi = x.y * agc_g;
+            const float y2 = yr * yr + yi * yi;
+            agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
+            if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
+            if (agc_g > 1e6f) agc_g = 1e6f;
+            yb[1 + j] = make_float2(yr, yi);
+          }
+        }
+        __syncthreads();
+      }
+      // ================= discriminator =================
+      const float ref = D->fd_ref;
+      for (int j = tid; j < cnt; j += 256) {
+        const float2 p = yb[j], r = yb[1 + j];
+        const float re = p.x * r.x + p.y * r.y;
+        const float im = p.x * r.y - p.y * r.x;
+        const float m = atan2f(im, re) * ref;
+        mx[FMX_HIST + j] = m;
+        if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
+      }
+    } else if (a.in_mode == FE_IN_MPX) {
+      for (int j = tid; j < cnt; j += 256) mx[FMX_HIST + j] = a.in_f[(size_t)c * a.in_stride + n0 + j];
+    }
+    __syncthreads();
+
+    // ================= 19 kHz pilot band-pass =================
+    if (pilot) {
+      float z[3];
+      fir_r3(mx, FMX_HIST + 3 * tid, D->pilot_taps, D->pilot_len, z);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int j = 3 * tid + r;
+        if (j < cnt) a.pilot_out[(size_t)c * a.pilot_stride + n0 + j] = z[r];
+      }
+    }
+    // ================= RDS resampler 240k -> 171k =================
+    if (rds) {
+      if (tid == 0) {
+        sh->e_begin = e_pos;
+        sh->e_end = sched_lower_bound(sched, sched_n, n0 + cnt);
+      }
+      __syncthreads();
+      const int eb = sh->e_begin, ee = sh->e_end;
+      for (int e = eb + tid; e < ee; e += 256) {
+        const FmxSched en = sched[e];
+        auto get = [&](int ii) -> float {
+          if (ii >= n0 - FMX_HIST + 1 && (n0 > 0 || ii >= 0)) return mx[FMX_HIST + ii - n0];
+          return rhist[32 + ii];
+        };
+        a.rds_out[(size_t)c * a.rds_stride + e] = resamp_out<FMX_RDS_RS_SUB>(D->rds_rs_h, en.packed, en.mu, get);
+      }
+      e_pos = ee;
+    }
+    __syncthreads();
+    // ================= carry halos to the next chunk =================
+    {
+      float2 cx = make_float2(0.0f, 0.0f);
+      float cm0 = 0.0f, cm1 = 0.0f;
+      if (demod && tid < FE_HALO_IQ) cx = xin[tid + cnt];
+      cm0 = mx[tid + cnt];
+      cm1 = mx[tid + 256 + cnt];
+      const float2 cy = yb[cnt];
+      __syncthreads();
+      if (demod && tid < FE_HALO_IQ) xin[tid] = cx;
+      mx[tid] = cm0;
+      mx[tid + 256] = cm1;
+      if (tid == 0 && demod) {
+        sh->fd_re = cy.x;
+        sh->fd_im = cy.y;
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- write back state ----
+  if (a.in_mode == FE_IN_U8_DECIM && M > 1) {
+    // last L-1 input samples (2 bytes each)
+    const long total = (long)n * M;
+    uint16_t keep[2];
+    int cntk = 0;
+    for (int h = tid; h < L - 1; h += 256) {
+      const long g = total - (L - 1) + h;
+      uint16_t v;
+      if (g >= 0) v = iq16[g];
+      else {
+        const int hh = (L - 1) + (int)g; // old history index
+        v = (uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8);
+      }
+      keep[cntk++] = v;
+    }
+    __syncthreads();
+    cntk = 0;
+    uint8_t *dh = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
+    for (int h = tid; h < L - 1; h += 256) {
+      const uint16_t v = keep[cntk++];
+      dh[2 * h] = (uint8_t)(v & 255);
+      dh[2 * h + 1] = (uint8_t)(v >> 8);
+    }
+    if (tid == 0) {
+      long nv = (long)dec_valid + total;
+      a.dec_valid[c] = (int)(nv > (L - 1) ? (L - 1) : nv);
+    }
+  }
+  if (demod) {
+    for (int h = tid; h < FE_HALO_IQ; h += 256) {
+      const float2 v = xin[h];
+      a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{v.x, v.y};
+    }
+    if (tid == 0) {
+      a.dc_v[2 * c] = sh->carry_i;
+      a.dc_v[2 * c + 1] = sh->carry_q;
+      a.fd_prev[2 * c] = sh->fd_re;
+      a.fd_prev[2 * c + 1] = sh->fd_im;
+      if (par.agc != 0) {
+        a.agc[2 * c] = agc_g;
+        a.agc[2 * c + 1] = agc_y2p;
+      }
+    }
+  }
+  if (pilot) {
+    float *hist = a.st_hist + ((size_t)(1 - a.st_parity) * a.C + c) * FMX_HIST;
+    for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[h];
+  }
+  if (rds) {
+    // new RDS resampler window: last 32 MPX samples
+    float v = 0.0f;
+    if (tid < 32) {
+      const int ii = n - 32 + tid;
+      v = (ii >= 0) ? mx[FMX_HIST - 32 + tid] : rhist[32 + ii];
+    }
+    __syncthreads();
+    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = v;
+    if (tid == 0) a.rds_count[c] = sched_n;
+  }
+  if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
+    a.clip_out[c] = (n > 0) ? (float)sh->clip / (float)n : 0.0f;
+}
+
+/* ================================================================== */
+/* k_pll: StereoDecoder per-sample recurrences, one lane per channel   */
+/* ================================================================== */
+__device__ __forceinline__ float blend_target(float ratio, float coh, float errHz, int mode, bool fmono,
+                                              bool fstereo, bool detected, float gate) {
+  if (fmono) return 0.0f;
+  if (fstereo) return 1.0f;
+  const float ratioQ = d_clamp((ratio - 0.022f) / fmaxf(0.040f - 0.022f, 1e-4f), 0.0f, 1.0f);
+  const float cohQ = d_clamp((coh - 0.11f) / fmaxf(0.18f - 0.11f, 1e-4f), 0.0f, 1.0f);
+  const float pllQ = d_clamp((320.0f - errHz) / fmaxf(320.0f - 180.0f, 1e-3f), 0.0f, 1.0f);
+  const float quality = fminf(ratioQ, fminf(cohQ, pllQ));
+  float shaped = quality * quality;
+  if (mode == 0) shaped = sqrtf(fmaxf(0.0f, quality));
+  else if (mode == 2) shaped = quality * quality * quality;
+  if (ratio < (0.022f * gate) || coh < (0.11f * gate) || errHz > (320.0f * 1.10f)) return 0.0f;
+  if (detected) return d_clamp(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
+  return 0.0f;
+}
+
+__global__ __launch_bounds__(64) void k_pll(PllArgs a) {
+  __shared__ float sp[64][PLL_T + 1], sm[64][PLL_T + 1], sd[64][PLL_T + 1];
+  __shared__ float ol[64][PLL_T + 1], orr[64][PLL_T + 1];
+  const int lane = threadIdx.x;
+  const int c0 = blockIdx.x * 64;
+  const int c = c0 + lane;
+  const bool act = c < a.C;
+  const FmxDesign *__restrict__ D = a.des;
+  const int n = a.n;
+  const int Dly = D->delay_len;
+  FmxStereoState s;
+  FmxChanParam par;
+  if (act) {
+    s = a.st[c];
+    par = a.par[c];
+  } else {
+    s = FmxStereoState{};
+    par = FmxChanParam{};
+  }
+  const int mode = par.blend;
+  const float attack = D->blend_attack[mode], release = D->blend_release[mode], gate = D->gate[mode];
+  const bool fmono = par.force_mono != 0, fstereo = par.force_stereo != 0;
+  const float nominal = D->nominal, pmin = D->pll_min, pmax = D->pll_max;
+  const float alpha = D->pll_alpha, beta = D->pll_beta;
+  const float fsf = (float)D->fs;
+  constexpr float kS = 0.9995f;
+  constexpr float kI = 1.0f - 0.9995f;
+  float phaseNow = d_nco_phase(s.theta);
+  float vcoQ, vcoI;
+  sincosf(phaseNow, &vcoQ, &vcoI);
+  bool detected = s.detected != 0;
+
+  for (int n0 = 0; n0 < n; n0 += PLL_T) {
+    const int cnt = min(PLL_T, n - n0);
+    // cooperative coalesced tile loads: 64 rows x cnt columns
+    for (int idx = lane; idx < 64 * PLL_T; idx += 64) {
+      const int row = idx / PLL_T, col = idx % PLL_T;
+      const int ch = c0 + row;
+      if (ch < a.C && col < cnt) {
+        const size_t t = (size_t)(n0 + col);
+        sp[row][col] = a.pilot[(size_t)ch * a.pilot_stride + t];
+        sm[row][col] = a.mpx[(size_t)ch * a.mpx_stride + t];
+        const int di = n0 + col - Dly;
+        sd[row][col] = (di >= 0) ? a.mpx[(size_t)ch * a.mpx_stride + di]
+                                 : a.st_hist[((size_t)a.st_parity * a.C + ch) * FMX_HIST + FMX_HIST + di];
+      }
+    }
+    __syncthreads();
+    if (act) {
+      for (int k = 0; k < cnt; ++k) {
+        const float pilot = sp[lane][k];
+        const float mpx = sm[lane][k];
+        const float delayed = sd[lane][k];
+        s.pilot_band_mag = (s.pilot_band_mag * kS) + (fabsf(pilot) * kI);
+        s.mpx_mag = (s.mpx_mag * kS) + (fabsf(mpx) * kI);
+        const float err = pilot * vcoQ;
+        s.dtheta += d_nco_constrain(err * alpha);
+        s.theta += d_nco_constrain(err * beta);
+        s.theta += s.dtheta;
+        const float phaseNext = d_nco_phase(s.theta);
+        float dphi = phaseNext - phaseNow;
+        if (dphi > kPiF) dphi -= 2.0f * kPiF;
+        else if (dphi < -kPiF) dphi += 2.0f * kPiF;
+        s.pll_phase = phaseNext;
+        s.pll_freq = d_clamp(dphi, pmin, pmax);
+        s.pilot_i = (s.pilot_i * kS) + ((pilot * vcoI) * kI);
+        s.pilot_q = (s.pilot_q * kS) + ((pilot * vcoQ) * kI);
+        const float magNow = sqrtf((s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q));
+        const float ratioNow = s.pilot_band_mag / fmaxf(s.mpx_mag, 1e-3f);
+        const float cohNow = magNow / fmaxf(s.pilot_band_mag, 1e-4f);
+        const float errHzNow = fabsf(s.pll_freq - nominal) * fsf / (2.0f * kPiF);
+        const float tgt = blend_target(ratioNow, cohNow, errHzNow, mode, fmono, fstereo, detected, gate);
+        float sN, cN;
+        sincosf(phaseNext, &sN, &cN);
+        const float monoNorm = delayed * 0.5f;
+        const float cos2 = (cN * cN) - (sN * sN);
+        const float lr = 2.0f * delayed * cos2;
+        const float sl = (delayed + lr) * 0.5f;
+        const float sr = (delayed - lr) * 0.5f;
+        const float ba = (tgt > s.blend) ? attack : release;
+        s.blend += (tgt - s.blend) * ba;
+        ol[lane][k] = monoNorm + ((sl - monoNorm) * s.blend);
+        orr[lane][k] = monoNorm + ((sr - monoNorm) * s.blend);
+        phaseNow = phaseNext;
+        vcoI = cN;
+        vcoQ = sN;
+      }
+    }
+    __syncthreads();
+    for (int idx = lane; idx < 64 * PLL_T; idx += 64) {
+      const int row = idx / PLL_T, col = idx % PLL_T;
+      const int ch = c0 + row;
+      if (ch < a.C && col < cnt) {
+        const size_t t = (size_t)ch * a.lr_stride + n0 + col;
+        a.lraw[t] = ol[row][col];
+        a.rraw[t] = orr[row][col];
+      }
+    }
+    __syncthreads();
+  }
+  if (!act) return;
+  // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
+  {
+    const float mag = sqrtf((s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q));
+    s.pilot_magnitude = (s.pilot_magnitude * 0.9f) + (mag * 0.1f);
+    const float mpxThr = detected ? 0.0028f : 0.005f;
+    const float ratio = s.pilot_band_mag / fmaxf(s.mpx_mag, 1e-3f);
+    const float coh = s.pilot_magnitude / fmaxf(s.pilot_band_mag, 1e-4f);
+    const float ratioThr = detected ? 0.022f : 0.040f;
+    const float cohThr = detected ? 0.11f : 0.18f;
+    const float errHz = fabsf(s.pll_freq - nominal) * fsf / (2.0f * kPiF);
+    const float pllThr = detected ? 320.0f : 180.0f;
+    const bool present = (s.mpx_mag > mpxThr) && (ratio > ratioThr) && (coh > cohThr) && (errHz < pllThr);
+    if (!fstereo) {
+      if (!detected) {
+        if (present) {
+          s.pilot_count++;
+          s.loss_count = 0;
+          if (s.pilot_count >= 6) detected = true;
+        } else {
+          s.pilot_count = 0;
+        }
+      } else if (present) {
+        s.loss_count = 0;
+      } else if (++s.loss_count >= 24) {
+        detected = false;
+        s.pilot_count = 0;
+        s.loss_count = 0;
+      }
+    }
+    const float calibrated = s.pilot_magnitude * 8.0f;
+    int lvl = (int)roundf(calibrated * 750.0f);
+    s.level = lvl < 0 ? 0 : (lvl > 750 ? 750 : lvl);
+    s.detected = detected ? 1 : 0;
+  }
+  a.st[c] = s;
+  if (a.stereo_out) a.stereo_out[c] = s.detected;
+  if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
+}
+
+/* ================================================================== */
+/* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
+/* ================================================================== */
+__global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
+  __shared__ float li[AU_HALO + AU_T], ri[AU_HALO + AU_T];
+  __shared__ float lf[AU_RHALO + AU_T], rf[AU_RHALO + AU_T];
+  __shared__ float ol[AU_MAXOUT], orr[AU_MAXOUT];
+  __shared__ int s_eb, s_ee, s_count;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const FmxDesign *__restrict__ D = a.des;
+  const FmxChanParam par = a.par[c];
+  const int n = a.n;
+  const bool mono = (a.mode == 2 || a.mode == 3);
+  const bool lrfir = (a.mode == 0 || a.mode == 4);
+  const bool af = (a.mode != 4);
+  const bool pipe_mono = (a.mode == 3);
+  const int deemph = par.deemph;
+  const float dalpha = (deemph == 0) ? D->deemph_alpha[0] : D->deemph_alpha[1];
+  const bool de_on = deemph != 2;
+  const float dc_alpha = mono ? 0.0008f : 0.005f;
+  const float de_a1 = -(1.0f - dalpha);
+  const float dc_a1 = -1.0f + dc_alpha;
+  // halos
+  float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
+  float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
+  if (lrfir)
+    for (int h = tid; h < AU_HALO; h += 256) {
+      li[h] = lrh[h];
+      ri[h] = lrh[(FMX_LR_LEN - 1) + h];
+    }
+  for (int h = tid; h < AU_RHALO; h += 256) {
+    lf[h] = win[h];
+    rf[h] = mono ? 0.0f : win[32 + h];
+  }
+  float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
+  // serial IIR state: [de_v, dc_v] per side
+  float de_v = 0.0f, dc_v = 0.0f;
+  if (af && (tid == 0 || tid == 64)) {
+    const int side = (tid == 0) ? 0 : 1;
+    if (mono) {
+      de_v = iir[0];
+      dc_v = iir[1];
+    } else {
+      de_v = iir[side];
+      dc_v = iir[2 + side];
+    }
+  }
+  const FmxSched *sched = nullptr;
+  int sched_n = 0;
+  if (af) {
+    const int g = a.group[c];
+    sched = a.sched + (size_t)g * a.sched_stride;
+    sched_n = a.sched_n[g];
+  }
+  if (tid == 0) {
+    s_eb = 0;
+    s_count = 0;
+  }
+  const float *inl = a.in_l + (size_t)c * a.in_stride;
+  const float *inr = mono ? nullptr : a.in_r + (size_t)c * a.in_stride;
+  __syncthreads();
+  for (int n0 = 0; n0 < n; n0 += AU_T) {
+    const int cnt = min(AU_T, n - n0);
+    for (int j = tid; j < cnt; j += 256) {
+      if (lrfir) {
+        li[AU_HALO + j] = inl[n0 + j];
+        ri[AU_HALO + j] = inr[n0 + j];
+      } else {
+        lf[AU_RHALO + j] = inl[n0 + j];
+        if (!mono) rf[AU_RHALO + j] = inr[n0 + j];
+      }
+    }
+    __syncthreads();
+    if (lrfir) {
+      float zl[3], zr[3];
+      fir_r3(li, AU_HALO + 3 * tid, D->lr_taps, FMX_LR_LEN, zl);
+      fir_r3(ri, AU_HALO + 3 * tid, D->lr_taps, FMX_LR_LEN, zr);
+      const float sc = D->lr_scale;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int j = 3 * tid + r;
+        if (j < cnt) {
+          lf[AU_RHALO + j] = zl[r] * sc;
+          rf[AU_RHALO + j] = zr[r] * sc;
+          if (a.lr_out_l) {
+            a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = zl[r] * sc;
+            a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = zr[r] * sc;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (af) {
+      if (tid == 0) s_ee = sched_lower_bound(sched, sched_n, n0 + cnt);
+      __syncthreads();
+      const int eb = s_eb, ee = s_ee;
+      for (int e = eb + tid; e < ee; e += 256) {
+        const FmxSched en = sched[e];
+        auto gl = [&](int ii) -> float { return lf[AU_RHALO + ii - n0]; };
+        ol[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en.packed, en.mu, gl);
+        if (!mono) {
+          auto gr = [&](int ii) -> float { return rf[AU_RHALO + ii - n0]; };
+          orr[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en.packed, en.mu, gr);
+        }
+      }
+      __syncthreads();
+      // serial de-emphasis + DC block (DF-II), one thread per side
+      if (tid == 0 || (tid == 64 && !mono)) {
+        const bool left = (tid == 0);
+        const float *src = left ? ol : orr;
+        float *dst = left ? a.out_l : a.out_r;
+        const int base = s_count;
+        for (int k = 0; k < ee - eb; ++k) {
+          float x = src[k];
+          if (de_on) {
+            const float t = de_a1 * de_v;
+            const float v0 = x - t;
+            de_v = v0;
+            x = dalpha * v0;
+          }
+          const float t2 = dc_a1 * dc_v;
+          const float v0 = x - t2;
+          x = v0 - dc_v;
+          dc_v = v0;
+          if (pipe_mono) x = x * 0.5f;
+          if (a.clamp) x = d_clamp(x, -1.0f, 1.0f);
+          const int o = base + k;
+          if (o < a.cap) {
+            dst[(size_t)c * a.out_stride + o] = x;
+            if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = x;
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        s_count += ee - eb;
+        s_eb = ee;
+      }
+    }
+    // carry halos
+    {
+      float cl = 0.0f, cr = 0.0f, fl = 0.0f, fr = 0.0f;
+      if (lrfir && tid < AU_HALO) {
+        cl = li[tid + cnt];
+        cr = ri[tid + cnt];
+      }
+      if (tid < AU_RHALO) {
+        fl = lf[tid + cnt];
+        fr = rf[tid + cnt];
+      }
+      __syncthreads();
+      if (lrfir && tid < AU_HALO) {
+        li[tid] = cl;
+        ri[tid] = cr;
+      }
+      if (tid < AU_RHALO) {
+        lf[tid] = fl;
+        rf[tid] = fr;
+      }
+      __syncthreads();
+    }
+  }
+  if (lrfir)
+    for (int h = tid; h < AU_HALO; h += 256) {
+      lrh[h] = li[h];
+      lrh[(FMX_LR_LEN - 1) + h] = ri[h];
+    }
+  if (af) {
+    for (int h = tid; h < AU_RHALO; h += 256) {
+      win[h] = lf[h];
+      if (!mono) win[32 + h] = rf[h];
+    }
+    if (tid == 0 || (tid == 64 && !mono)) {
+      const int side = (tid == 0) ? 0 : 1;
+      if (mono) {
+        iir[0] = de_v;
+        iir[1] = dc_v;
+      } else {
+        iir[side] = de_v;
+        iir[2 + side] = dc_v;
+      }
+    }
+    if (tid == 0 && a.out_count) a.out_count[c] = s_count < a.cap ? s_count : a.cap;
+  }
+}
+
+/* ================================================================== */
+/* k_rds: 57 kHz BPSK demodulator + block sync, one lane per channel   */
+/* ================================================================== */
+enum { OA = 0, OB = 1, OC = 2, OCP = 3, OD = 4, OINV = 5 };
+__device__ __forceinline__ int bs_block_number(int off) {
+  return (off == OA) ? 0 : (off == OB) ? 1 : (off == OC || off == OCP) ? 2 : (off == OD) ? 3 : 0;
+}
+__device__ __forceinline__ int bs_next(int off) {
+  return (off == OA) ? OB : (off == OB) ? OC : (off == OC || off == OCP) ? OD : OA;
+}
+__device__ __forceinline__ int bs_offset_for(uint32_t s) {
+  switch (s) {
+    case 0x3D8: return OA; // 0b1111011000
+    case 0x3D4: return OB; // 0b1111010100
+    case 0x25C: return OC; // 0b1001011100
+    case 0x3CC: return OCP; // 0b1111001100
+    case 0x258: return OD; // 0b1001011000
+    default: return OINV;
+  }
+}
+__constant__ uint32_t c_parity[26] = {0x200, 0x100, 0x080, 0x040, 0x020, 0x010, 0x008, 0x004, 0x002,
+                                      0x001, 0x2DC, 0x16E, 0x0B7, 0x287, 0x39F, 0x313, 0x355, 0x376,
+                                      0x1BB, 0x201, 0x3DC, 0x1EE, 0x0F7, 0x2A7, 0x38F, 0x31B};
+__device__ __forceinline__ uint32_t bs_syndrome(uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 26; ++k) r ^= ((v >> k) & 1u) ? c_parity[25 - k] : 0u;
+  return r;
+}
+__device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t opos, int ooff) {
+  const uint32_t d = pos - opos;
+  return d % 26 == 0 && d / 26 <= 6 && off != OINV && ooff != OINV &&
+         ((uint32_t)bs_block_number(ooff) + d / 26) % 4 == (uint32_t)bs_block_number(off);
+}
+
+struct RdsLds {
+  float taps[24][12];
+  float mf[FMX_NPFB * FMX_SS_SUB];
+  float dmf[FMX_NPFB * FMX_SS_SUB];
+  uint32_t esyn[5][52];
+  uint32_t eerr[5][52];
+  float tin[64][65];
+};
+
+__device__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
+  fmx_rds_group g;
+  uint8_t e[4];
+  uint16_t d[4];
+  for (int i = 0; i < 4; ++i) {
+    const bool rec = s.bs_blk_flags[i] & 1;
+    const bool had = (s.bs_blk_flags[i] >> 1) & 1;
+    e[i] = rec ? (had ? 1 : 0) : 3;
+    d[i] = rec ? s.bs_blk_data[i] : 0;
+  }
+  g.a = d[0];
+  g.b = d[1];
+  g.c = d[2];
+  g.d = d[3];
+  g.errors = (uint8_t)((e[0] << 6) | (e[1] << 4) | (e[2] << 2) | e[3]);
+  g.pad = 0;
+  g.block_index = a.block_index;
+  if (ng < a.groups_stride) a.groups[(size_t)c * a.groups_stride + ng] = g;
+  ng++;
+}
+
+__device__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
+  s.bs_reg = (s.bs_reg << 1u) + (uint32_t)bit;
+  s.bs_until_next--;
+  s.bs_bitcount++;
+  if (s.bs_until_next != 0) return;
+  // findBlockInInputRegister
+  const uint32_t raw = s.bs_reg & ((1u << 26) - 1u);
+  const uint32_t syn = bs_syndrome(raw);
+  int off = bs_offset_for(syn);
+  bool done = false;
+  if (!s.bs_in_sync) {
+    s.bs_bits_since_lost++;
+    if (off != OINV) {
+      for (int i = 0; i < 3; ++i) {
+        s.bs_pulse_off[i] = s.bs_pulse_off[i + 1];
+        s.bs_pulse_pos[i] = s.bs_pulse_pos[i + 1];
+      }
+      s.bs_pulse_off[3] = off;
+      s.bs_pulse_pos[3] = s.bs_bitcount;
+      bool found = false;
+      for (int i = 0; i < 2 && !found; ++i)
+        for (int j = i + 1; j < 3 && !found; ++j)
+          if (pulse_follows(s.bs_pulse_pos[3], s.bs_pulse_off[3], s.bs_pulse_pos[j], s.bs_pulse_off[j]) &&
+              pulse_follows(s.bs_pulse_pos[j], s.bs_pulse_off[j], s.bs_pulse_pos[i], s.bs_pulse_off[i]))
+            found = true;
+      if (found) {
+        s.bs_in_sync = 1;
+        s.bs_expected = off;
+        for (int i = 0; i < 4; ++i) {
+          s.bs_blk_flags[i] = 0;
+          s.bs_blk_data[i] = 0;
+          s.bs_blk_raw[i] = 0;
+        }
+        s.bs_bits_since_lost = 0;
+      }
+    }
+  }
+  if (s.bs_in_sync) {
+    if (s.bs_expected == OC && off == OCP) s.bs_expected = OCP;
+    const bool had = (off != s.bs_expected);
+    // RunningSum<int, 50>
+    const int p = s.bs_err_ptr;
+    if (p < 32) {
+      if (had) s.bs_err_mask_lo |= (1u << p);
+      else s.bs_err_mask_lo &= ~(1u << p);
+    } else {
+      if (had) s.bs_err_mask_hi |= (1u << (p - 32));
+      else s.bs_err_mask_hi &= ~(1u << (p - 32));
+    }
+    s.bs_err_ptr = (p + 1) % 50;
+    if (__popc(s.bs_err_mask_lo) + __popc(s.bs_err_mask_hi) > 42) {
+      s.bs_in_sync = 0;
+      s.bs_err_mask_lo = 0;
+      s.bs_err_mask_hi = 0;
+      done = true;
+    }
+    if (!done) {
+      uint16_t data = (uint16_t)(raw >> 10);
+      if (had) {
+        for (int i = 0; i < 52; ++i)
+          if (L.esyn[s.bs_expected][i] == syn) {
+            data = (uint16_t)((raw ^ L.eerr[s.bs_expected][i]) >> 10);
+            off = s.bs_expected;
+            break;
+          }
+      }
+      if (off == s.bs_expected) {
+        const int bn = bs_block_number(s.bs_expected);
+        s.bs_blk_raw[bn] = raw;
+        s.bs_blk_data[bn] = data;
+        s.bs_blk_flags[bn] = (uint8_t)(1 | (had ? 2 : 0));
+      }
+      const int next = bs_next(s.bs_expected);
+      if (next == OA) {
+        rds_emit_group(s, a, c, ng);
+        for (int i = 0; i < 4; ++i) {
+          s.bs_blk_flags[i] = 0;
+          s.bs_blk_data[i] = 0;
+          s.bs_blk_raw[i] = 0;
+        }
+      }
+      s.bs_expected = next;
+    }
+  }
+  s.bs_until_next = s.bs_in_sync ? 26u : 1u;
+}
+
+__global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
+  __shared__ RdsLds L;
+  const int lane = threadIdx.x;
+  const int c0 = blockIdx.x * 64;
+  const int c = c0 + lane;
+  const bool act = c < a.C;
+  const FmxDesign *__restrict__ D = a.des;
+  // ---- LDS tables ----
+  for (int idx = lane; idx < 24 * 12; idx += 64) {
+    const int jp = idx / 12, i = idx % 12;
+    const int k = jp + 24 * i;
+    L.taps[jp][i] = (i < FMX_RDS_NACC && k < FMX_RDS_FIR) ? D->rds_fir[k] : 0.0f;
+  }
+  for (int idx = lane; idx < FMX_NPFB * FMX_SS_SUB; idx += 64) {
+    L.mf[idx] = D->ss_mf[idx];
+    L.dmf[idx] = D->ss_dmf[idx];
+  }
+  if (lane < 5) {
+    const uint32_t words[5] = {0x0FC, 0x198, 0x168, 0x350, 0x1B4};
+    int idx = 0;
+    for (int bits = 1; bits <= 3; bits += 2)
+      for (uint32_t sh = 0; sh < 26; ++sh) {
+        const uint32_t e = ((uint32_t)bits << sh) & ((1u << 26) - 1u);
+        L.esyn[lane][idx] = bs_syndrome(e ^ words[lane]);
+        L.eerr[lane][idx] = e;
+        idx++;
+      }
+  }
+  FmxRdsState s;
+  int count = 0;
+  if (act) {
+    s = a.st[c];
+    count = a.in_count[c];
+  }
+  __syncthreads();
+  float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
+  if (act && s.rebuild) {
+    // decimation phase changed by a reset: rebuild the partial sums from the
+    // last mixed samples (the reference's FIR window survives the reset)
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC; ++i) {
+      float ar = 0.0f, ai = 0.0f;
+      for (int kp = FMX_RDS_FIR - 1 - 24 * i; kp >= 1; --kp) {
+        const uint32_t idx = (s.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
+        const float h = D->rds_fir[24 * i + kp];
+        const float pr = h * ring[2 * idx];
+        const float pi = h * ring[2 * idx + 1];
+        ar = ar + pr;
+        ai = ai + pi;
+      }
+      s.acc_re[i] = ar;
+      s.acc_im[i] = ai;
+    }
+    s.rebuild = 0;
+  }
+  int ng = 0;
+  // wave-wide max sample count
+  int nmax = count;
+  for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d));
+  const float fscale = D->rds_fir_scale;
+  const float agc_bw = D->agc_bw;
+  const float ss_b0 = D->ss_b0, ss_a1 = D->ss_a1, ss_adj = D->ss_rate_adj;
+  const float psk_xr1 = D->psk_xr1, psk_xi1 = D->psk_xi1;
+  const float alpha = D->rds_alpha, beta = D->rds_beta;
+  const float dphi_psk = (float)(3.14159265358979323846 * (1.0 - 1.0 / 2));
+  const uint32_t ring0 = s.ring_pos;
+
+  for (int n0 = 0; n0 < nmax; n0 += 64) {
+    for (int idx = lane; idx < 64 * 64; idx += 64) {
+      const int row = idx >> 6, col = idx & 63;
+      const int ch = c0 + row;
+      if (ch < a.C) {
+        const int cn = a.in_count[ch];
+        L.tin[row][col] = (n0 + col < cn) ? a.in[(size_t)ch * a.in_stride + n0 + col] : 0.0f;
+      }
+    }
+    __syncthreads();
+    const int kend = act ? min(64, count - n0) : 0;
+    for (int k = 0; k < kend; ++k) {
+      const float x = L.tin[lane][k];
+      float sn, cs;
+      sincosf(-s.phase0, &sn, &cs);
+      const float mr = x * cs, mi = x * sn;
+      const int j = (int)(s.sample_since_reset % FMX_RDS_DECIM);
+      const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
+#pragma unroll
+      for (int i = 0; i < FMX_RDS_NACC; ++i) {
+        const float h = L.taps[jp][i];
+        const float pr = h * mr, pi = h * mi;
+        s.acc_re[i] = s.acc_re[i] + pr;
+        s.acc_im[i] = s.acc_im[i] + pi;
+      }
+      const int t = n0 + k;
+      if (t >= count - FMX_RDS_RING) {
+        const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
+        ring[2 * idx] = mr;
+        ring[2 * idx + 1] = mi;
+      }
+      if (j == 0) {
+        // ---- FIR output, AGC ----
+        const float fr = s.acc_re[0] * fscale, fi = s.acc_im[0] * fscale;
+#pragma unroll
+        for (int i = 0; i < FMX_RDS_NACC - 1; ++i) {
+          s.acc_re[i] = s.acc_re[i + 1];
+          s.acc_im[i] = s.acc_im[i + 1];
+        }
+        s.acc_re[FMX_RDS_NACC - 1] = 0.0f;
+        s.acc_im[FMX_RDS_NACC - 1] = 0.0f;
+        const float yr = fr * s.agc_g, yi = fi * s.agc_g;
+        const float y2 = yr * yr + yi * yi;
+        s.agc_y2p = (float)((1.0 - (double)agc_bw) * (double)s.agc_y2p + (double)(agc_bw * y2));
+        if (s.agc_y2p > 1e-6f) s.agc_g *= expf(-0.5f * agc_bw * logf(s.agc_y2p));
+        if (s.agc_g > 1e6f) s.agc_g = 1e6f;
+        // ---- symsync ----
+#pragma unroll
+        for (int m = 0; m < FMX_SS_SUB - 1; ++m) {
+          s.ss_win_re[m] = s.ss_win_re[m + 1];
+          s.ss_win_im[m] = s.ss_win_im[m + 1];
+        }
+        s.ss_win_re[FMX_SS_SUB - 1] = yr;
+        s.ss_win_im[FMX_SS_SUB - 1] = yi;
+        if (s.ss_mf_valid < FMX_SS_SUB) s.ss_mf_valid++;
+        int ns = 0;
+        float symr = 0.0f, symi = 0.0f;
+        while (s.ss_b < FMX_NPFB && ns < 16) {
+          const float *hm = L.mf + s.ss_b * FMX_SS_SUB;
+          float ar = 0.0f, ai = 0.0f;
+          const int first = FMX_SS_SUB - s.ss_mf_valid;
+#pragma unroll
+          for (int m = 0; m < FMX_SS_SUB; ++m) {
+            const float h = hm[FMX_SS_SUB - 1 - m];
+            const float wr = (m >= first) ? s.ss_win_re[m] : 0.0f;
+            const float wi = (m >= first) ? s.ss_win_im[m] : 0.0f;
+            const float pr = h * wr, pi = h * wi;
+            ar = ar + pr;
+            ai = ai + pi;
+          }
+          if (ns == 0) {
+            symr = ar / 3.0f;
+            symi = ai / 3.0f;
+          }
+          if (s.ss_decim == 1) {
+            s.ss_decim = 0;
+            const float *hd = L.dmf + s.ss_b * FMX_SS_SUB;
+            float dr = 0.0f, di = 0.0f;
+#pragma unroll
+            for (int m = 0; m < FMX_SS_SUB; ++m) {
+              const float h = hd[FMX_SS_SUB - 1 - m];
+              const float pr = h * s.ss_win_re[m], pi = h * s.ss_win_im[m];
+              dr = dr + pr;
+              di = di + pi;
+            }
+            float q = ar * dr + ai * di;
+            if (q > 1.0f) q = 1.0f;
+            else if (q < -1.0f) q = -1.0f;
+            const float t1 = ss_a1 * s.ss_v1;
+            const float v0 = q - t1;
+            s.ss_q_hat = ss_b0 * v0;
+            s.ss_v1 = v0;
+            s.ss_rate += ss_adj * s.ss_q_hat;
+            s.ss_del = s.ss_rate + s.ss_q_hat;
+          }
+          s.ss_decim++;
+          s.ss_tau += s.ss_del;
+          s.ss_b = (int)roundf(s.ss_tau * (float)FMX_NPFB);
+          ns++;
+        }
+        s.ss_tau -= 1.0f;
+        s.ss_b -= FMX_NPFB;
+        if (ns == 1) {
+          // ---- PSK2 modem phase error -> NCO PLL ----
+          float th = atan2f(symi, symr) - dphi_psk;
+          if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
+          const bool s1 = th > 0.0f;
+          const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
+          float pe = symi * xr - symr * xi;
+          pe = d_clamp(pe, -kPiF, kPiF);
+          const float dphi = pe * 12.0f;
+          s.dtheta += d_nco_constrain(dphi * alpha);
+          s.theta += d_nco_constrain(dphi * beta);
+          // ---- biphase + delta ----
+          const float bir = (symr - s.bi_prev_re) * 0.5f;
+          const int val = bir >= 0.0f;
+          const bool has = (s.bi_clock % 2u) == s.bi_polarity;
+          s.bi_prev_re = symr;
+          s.bi_prev_im = symi;
+          if ((s.bi_clock & 1u) == 0) s.bi_even += fabsf(bir);
+          else s.bi_odd += fabsf(bir);
+          s.bi_clock++;
+          if (s.bi_clock == 128u) {
+            if (s.bi_even > s.bi_odd) s.bi_polarity = 0;
+            else if (s.bi_odd > s.bi_even) s.bi_polarity = 1;
+            s.bi_even = 0.0f;
+            s.bi_odd = 0.0f;
+            s.bi_clock = 0;
+          }
+          if (has) {
+            const int bit = (val != s.delta_prev) ? 1 : 0;
+            s.delta_prev = val;
+            rds_push_bit(s, bit, L, a, c, ng);
+          }
+        }
+      }
+      // ---- NCO step + quad-phase wrapper ----
+      s.theta += s.dtheta;
+      const float now = d_nco_phase(s.theta);
+      float delta = now - s.prev_f0;
+      if (delta > kPiF) delta = delta - 2.f * kPiF;
+      else if (delta < -kPiF) delta = delta + 2.f * kPiF;
+      s.prev_f0 = now;
+      const float scaled = delta * 57000.f / 57000.f;
+      float ph = s.phase0 + scaled;
+      if (ph > kPiF) ph = ph - 2.f * kPiF;
+      else if (ph < -kPiF) ph = ph + 2.f * kPiF;
+      s.phase0 = ph;
+      s.sample_since_reset++;
+    }
+    __syncthreads();
+  }
+  if (!act) return;
+  s.ring_pos = ring0 + (uint32_t)count;
+  a.st[c] = s;
+  if (a.group_count) a.group_count[c] = ng;
+}
+
+/* ================================================================== */
+/* state reset / construction                                          */
+/* ================================================================== */
+__global__ void k_reset(ResetArgs a) {
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int m = a.mask[c];
+  if (m == 0) return;
+  const FmxDesign *D = a.des;
+  const bool create = m & RS_CREATE;
+  if (create || (m & RS_DECIM)) {
+    if (tid == 0) a.dec_valid[c] = 0;
+  }
+  if (create || (m & (RS_DEMOD | RS_IQFIR))) {
+    for (int h = tid; h < FMX_IQ_MAXLEN - 1; h += blockDim.x)
+      a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{0.0f, 0.0f};
+  }
+  if (create || (m & RS_DEMOD)) {
+    if (tid == 0) {
+      a.dc_v[2 * c] = 0.0f;
+      a.dc_v[2 * c + 1] = 0.0f;
+      a.fd_prev[2 * c] = 0.0f;
+      a.fd_prev[2 * c + 1] = 0.0f;
+      a.mono_iir[2 * c] = 0.0f;
+      a.mono_iir[2 * c + 1] = 0.0f;
+    }
+    for (int h = tid; h < 32; h += blockDim.x) a.mono_win[(size_t)c * 32 + h] = 0.0f;
+  }
+  if (create || (m & RS_AGC)) {
+    if (tid == 0) {
+      a.agc[2 * c] = 1.0f;
+      a.agc[2 * c + 1] = 1.0f;
+    }
+  }
+  if (create || (m & RS_STEREO)) {
+    for (int h = tid; h < FMX_HIST; h += blockDim.x) {
+      a.st_hist[(size_t)c * FMX_HIST + h] = 0.0f;
+      a.st_hist[((size_t)a.C + c) * FMX_HIST + h] = 0.0f;
+    }
+    for (int h = tid; h < 2 * (FMX_LR_LEN - 1); h += blockDim.x)
+      a.lr_hist[(size_t)c * 2 * (FMX_LR_LEN - 1) + h] = 0.0f;
+    if (tid == 0) {
+      FmxStereoState s{};
+      s.theta = 0;
+      s.dtheta = D->pll_dtheta0;
+      s.pll_freq = D->nominal;
+      a.st[c] = s;
+    }
+  }
+  if (create || (m & RS_AF)) {
+    for (int h = tid; h < 64; h += blockDim.x) a.af_win[(size_t)c * 64 + h] = 0.0f;
+    if (tid < 4) a.af_iir[(size_t)c * 4 + tid] = 0.0f;
+  }
+  if (m & RS_DEEMPH) {
+    if (tid == 0) {
+      a.af_iir[(size_t)c * 4 + 0] = 0.0f;
+      a.af_iir[(size_t)c * 4 + 1] = 0.0f;
+      a.mono_iir[2 * c] = 0.0f;
+    }
+  }
+  if (create || (m & RS_RDS)) {
+    if (tid == 0) {
+      FmxRdsState s;
+      if (create) {
+        s = FmxRdsState{};
+        s.agc_g = D->agc_g0;
+        s.agc_y2p = 1.0f;
+        s.rebuild = 0;
+      } else {
+        s = a.rds[c];
+        s.rebuild = 1;
+      }
+      s.theta = 0;
+      s.dtheta = D->rds_dtheta0;
+      s.sample_since_reset = 0;
+      // symsync reset (matched filter bank only)
+      s.ss_mf_valid = 0;
+      s.ss_rate = 3.0f;
+      s.ss_del = 3.0f;
+      s.ss_tau = 0.0f;
+      s.ss_b = 0;
+      s.ss_q_hat = 0.0f;
+      s.ss_v1 = 0.0f;
+      s.ss_v2 = 0.0f;
+      s.ss_decim = 0;
+      // fresh BlockStream
+      s.bs_bitcount = 0;
+      s.bs_until_next = 1;
+      s.bs_reg = 0;
+      s.bs_err_mask_lo = 0;
+      s.bs_err_mask_hi = 0;
+      s.bs_expected = OA;
+      s.bs_in_sync = 0;
+      s.bs_err_ptr = 0;
+      for (int i = 0; i < 4; ++i) {
+        s.bs_pulse_pos[i] = 0;
+        s.bs_pulse_off[i] = OINV;
+        s.bs_blk_raw[i] = 0;
+        s.bs_blk_data[i] = 0;
+        s.bs_blk_flags[i] = 0;
+      }
+      s.bs_bits_since_lost = 0;
+      a.rds[c] = s;
+    }
+    if (create) {
+      for (int h = tid; h < 2 * FMX_RDS_RING; h += blockDim.x) a.ring[(size_t)c * 2 * FMX_RDS_RING + h] = 0.0f;
+      for (int h = tid; h < 32; h += blockDim.x) a.rds_hist[(size_t)c * 32 + h] = 0.0f;
+    }
+  }
+}
+
+/* ================================================================== */
+/* synthetic IQ generator                                              */
+/* ================================================================== */
+__global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
+                        const uint8_t *bits, uint8_t *out, size_t out_stride) {
+  const int ci = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= n_ch || i >= n_samples) return;
+  const uint32_t ch = ch0 + (uint32_t)ci;
+  const fmx_synth_chan cp = fmx_synth_channel(&cfg, ch);
+  const uint8_t *b = bits ? bits + (size_t)ci * cfg.n_bits : nullptr;
+  uint8_t iq[2];
+  fmx_synth_sample(&cfg, ch, &cp, sample0 + i, b, iq);
+  uint16_t w = (uint16_t)iq[0] | ((uint16_t)iq[1] << 8);
+  reinterpret_cast<uint16_t *>(out + (size_t)ci * out_stride)[i] = w;
+}
+
+/* ================================================================== */
+/* launchers                                                           */
+/* ================================================================== */
+template <int M, int TPP> static size_t fe_smem() {
+  constexpr int Q = FE_T + ((M > 1) ? TPP : 1);
+  constexpr int IN_BYTES = (M > 1) ? M * Q * 4 : 0;
+  constexpr int YB_BYTES = (FE_T + 1) * 8;
+  constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
+  return (size_t)R0 + (FE_HALO_IQ + FE_T) * 8 + (FMX_HIST + FE_T) * 4 + sizeof(FeShared);
+}
+
+template <int M, int TPP> static int fe_launch(const FeArgs &a, hipStream_t st) {
+  const size_t smem = fe_smem<M, TPP>();
+  static bool configured = false;
+  if (!configured) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_frontend<M, TPP>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+      return FMX_E_HIP;
+    configured = true;
+  }
+  hipLaunchKernelGGL((k_frontend<M, TPP>), dim3(a.C), dim3(256), smem, st, a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+
+} // namespace fmx
+
+// The decimation factor is a host-known constant of the handle; expose
+// explicit launchers so fmx_capi can pick the instantiation.
+namespace fmx {
+int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1>(a, st);
+  if (M == 10 && tpp == 28) return fe_launch<10, 28>(a, st);
+  if (M == 8 && tpp == 28) return fe_launch<8, 28>(a, st);
+  if (M == 4 && tpp == 20) return fe_launch<4, 20>(a, st);
+  if (M == 2 && tpp == 12) return fe_launch<2, 12>(a, st);
+  return FMX_E_INVALID;
+}
+
+int launch_pll(const PllArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_pll, dim3((a.C + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_audio(const AudioArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_rds(const RdsArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_reset(const ResetArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_reset, dim3(a.C), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
+                 const uint8_t *bits, uint8_t *out, size_t out_stride, void *stream) {
+  if (n_ch <= 0 || n_samples <= 0) return FMX_OK;
+  dim3 grid((n_samples + 255) / 256, n_ch);
+  hipLaunchKernelGGL(k_synth, grid, dim3(256), 0, static_cast<hipStream_t>(stream), cfg, ch0, n_ch, sample0,
+                     n_samples, bits, out, out_stride);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+} // namespace fmx

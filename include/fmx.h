@@ -1,0 +1,207 @@
+/*
+ * fmx.h -- C ABI of the MI355X many-channel FM demodulator (libfmx.so).
+ *
+ * This is the drop-in boundary for bkram/fmtuner-sdr's per-block DSP hot path
+ * (SURVEY.md 8b).  One handle holds N independent channels, each with the
+ * exact state of one set of reference objects:
+ *
+ *   ComplexDecimator   include/dsp/liquid_primitives.h:161-188
+ *   FMDemod            include/fm_demod.h:11-67
+ *   StereoDecoder      include/stereo_decoder.h:10-55
+ *   AFPostProcessor    include/af_post_processor.h:9-37
+ *   RDSDecoder         include/rds_decoder.h:17-29
+ *
+ * and one call of fmx_process_block() replaces one iteration of the
+ * reference's per-block body (src/main.cpp:1239-1308) for every channel.
+ * The C++ facades in include/fmx_blocks.hpp map one reference object onto one
+ * channel slot and keep the reference's method signatures.
+ *
+ * Conventions (reference-compatible):
+ *   - sizes are SAMPLES, not bytes; IQ buffers are 2*n bytes, I then Q;
+ *   - the caller owns every buffer; outputs are written from index 0;
+ *   - functions return 0 (FMX_OK) or a negative FMX_E* code; the message is
+ *     available from fmx_last_error(); nothing throws across the ABI;
+ *   - pointers named d_* are DEVICE pointers (hipMalloc'd memory on the
+ *     handle's device), pointers named h_* are host pointers;
+ *   - a handle is not thread-safe (like the reference objects); all work is
+ *     queued on the handle's own HIP stream, fmx_sync() waits for it.
+ *
+ * No HIP or torch types appear in this header.
+ */
+#ifndef FMX_H
+#define FMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMX_ABI_VERSION 1
+
+enum {
+  FMX_OK = 0,
+  FMX_E_INVALID = -1,   /* bad argument / unsupported configuration        */
+  FMX_E_HIP = -2,       /* HIP runtime failure                             */
+  FMX_E_NOMEM = -3,     /* device allocation failed                        */
+  FMX_E_CAPACITY = -4,  /* n exceeds the block size the handle was made for */
+  FMX_E_NODEVICE = -5   /* no HIP device / kernels not loadable            */
+};
+
+/* dsp_agc (config.h:51) */
+enum { FMX_AGC_OFF = 0, FMX_AGC_FAST = 1, FMX_AGC_SLOW = 2 };
+/* stereo_blend (config.h:52) */
+enum { FMX_BLEND_SOFT = 0, FMX_BLEND_NORMAL = 1, FMX_BLEND_AGGRESSIVE = 2 };
+/* tuner.deemphasis (main.cpp:699-708) */
+enum { FMX_DEEMPH_50US = 0, FMX_DEEMPH_75US = 1, FMX_DEEMPH_OFF = 2 };
+
+typedef struct {
+  int iq_rate;         /* SDR rate, integer multiple of dsp_rate             */
+  int dsp_rate;        /* 240000 (2.4 MS/s / 10) or 256000 (reference)       */
+  int out_rate;        /* 32000                                              */
+  int block;           /* max DSP samples per call (dsp_block_samples)       */
+  int w0_bandwidth_hz; /* processing.w0_bandwidth_hz                         */
+  int bandwidth_hz;    /* XDR W value (0 = W0)                               */
+  int dsp_agc;         /* FMX_AGC_*                                          */
+  int stereo;          /* processing.stereo                                  */
+  int blend;           /* FMX_BLEND_*                                        */
+  int deemphasis;      /* FMX_DEEMPH_*                                       */
+  int force_mono;
+  int force_stereo;
+  int rds;             /* decode RDS                                          */
+} fmx_config;
+
+/* One RDS group as the reference's RDSGroup (rds_decoder.h:9-15). */
+typedef struct {
+  uint16_t a, b, c, d;
+  uint8_t errors; /* (eA<<6)|(eB<<4)|(eC<<2)|eD, e: 0 ok, 1 corrected, 3 missing */
+  uint8_t pad;
+  uint32_t block_index; /* fmx_process_block call that emitted it */
+} fmx_rds_group;
+
+/* Device output buffers of fmx_process_block (all optional except where
+ * noted; pass NULL to skip).  Strides are in elements. */
+typedef struct {
+  float *d_mpx;            /* [C][mpx_stride] discriminator MPX at dsp_rate   */
+  int mpx_stride;
+  float *d_pcm_l;          /* [C][pcm_stride] clamped 32 kHz audio (required) */
+  float *d_pcm_r;          /* [C][pcm_stride]                                 */
+  int pcm_stride;
+  int *d_pcm_count;        /* [C] samples written per channel (required)      */
+  int *d_stereo;           /* [C] StereoDecoder::isStereo()                   */
+  int *d_pilot_tenths;     /* [C] getPilotLevelTenthsKHz()                    */
+  float *d_clip_ratio;     /* [C] FMDemod::getClippingRatio()                 */
+  fmx_rds_group *d_groups; /* [C][groups_stride]                              */
+  int groups_stride;
+  int *d_group_count;      /* [C]                                             */
+} fmx_block_out;
+
+/* ---- lifetime ---- */
+int fmx_device_count(void);
+int fmx_create(const fmx_config *cfg, int n_channels, int device, void **handle);
+int fmx_destroy(void *handle);
+const char *fmx_last_error(void *handle);
+int fmx_sync(void *handle);
+int fmx_num_channels(void *handle);
+
+/* Runtime::reset fan-out (main.cpp:686-691: demod, stereo, afPost,
+ * decimator) plus the RDS worker reset (main.cpp:909-916).  channel = -1
+ * resets every channel. */
+int fmx_reset(void *handle, int channel);
+
+/* Per-channel settings mirroring the reference setters; channel = -1 = all. */
+enum {
+  FMX_PARAM_BANDWIDTH_HZ = 1,  /* FMDemod::setBandwidthHz (fm_demod.cpp:168)   */
+  FMX_PARAM_W0_HZ = 2,         /* FMDemod::setW0BandwidthHz (:206)             */
+  FMX_PARAM_DEEMPHASIS = 3,    /* tuner.deemphasis 0/1/2 -> both demod + AF   */
+  FMX_PARAM_DSP_AGC = 4,       /* FMDemod::setDspAgcMode (:210)                */
+  FMX_PARAM_BLEND = 5,         /* StereoDecoder::setBlendMode                  */
+  FMX_PARAM_FORCE_MONO = 6,    /* StereoDecoder::setForceMono                  */
+  FMX_PARAM_FORCE_STEREO = 7,  /* StereoDecoder::setForceStereo                */
+  FMX_PARAM_BANDWIDTH_MODE = 8 /* FMDemod::setBandwidthMode (TEF table)        */
+};
+int fmx_set_param(void *handle, int channel, int key, int value);
+
+/* One reference block for every channel.  d_iq: [C][iq_stride] bytes, each
+ * row holding 2*n*M interleaved u8 I/Q (M = iq_rate / dsp_rate); n <= block.
+ * Queued on the handle's stream; results are valid after fmx_sync(). */
+int fmx_process_block(void *handle, const uint8_t *d_iq, size_t iq_stride, int n,
+                      const fmx_block_out *out);
+
+/* ---- per-object stages (same state as fmx_process_block) ----
+ * Each mirrors one reference method, batched over all C channels. */
+/* ComplexDecimator::executeComplex: d_out [C][out_stride] complex float */
+int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, float *d_out,
+                 int out_stride);
+/* FMDemod::processSplitComplex(iq, mpx, mono, n): d_iq_cf complex float
+ * [C][in_stride]; d_mono may be NULL (stereo mode: returns 0 samples). */
+int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride,
+              float *d_mono, int mono_stride, int *d_mono_count);
+/* StereoDecoder::processAudio */
+int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_left, float *d_right,
+               int lr_stride, int *d_stereo, int *d_pilot_tenths);
+/* AFPostProcessor::process (outCapacity = cap) */
+int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_stride, int n,
+               float *d_out_l, float *d_out_r, int out_stride, int cap, int *d_count);
+/* RDSDecoder::process: groups of this call per channel */
+int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_group *d_groups,
+            int groups_stride, int *d_group_count);
+
+/* ---- device memory helpers (so C/FFI callers need no HIP headers) ---- */
+int fmx_malloc(void *handle, void **d_ptr, size_t bytes);
+int fmx_free(void *handle, void *d_ptr);
+int fmx_memcpy_h2d(void *handle, void *d_dst, const void *h_src, size_t bytes);
+int fmx_memcpy_d2h(void *handle, void *h_dst, const void *d_src, size_t bytes);
+int fmx_memset(void *handle, void *d_ptr, int value, size_t bytes);
+
+/* ---- HIP-event timing of the hot kernels (bench roofline support) ----
+ * When enabled, every launch of each kernel is bracketed by events on the
+ * stream it runs on; fmx_kernel_times returns the summed milliseconds and
+ * launch counts per kernel id since the last reset. */
+enum {
+  FMX_K_FRONTEND = 0, /* decimate + DC + IQ FIR + AGC + discriminator + pilot BPF + RDS resample */
+  FMX_K_STEREO = 1,   /* pilot PLL + blend + L-R matrix (one lane per channel)                 */
+  FMX_K_AUDIO = 2,    /* L/R 15 kHz FIRs + 32 kHz resampler + de-emphasis + DC + clamp         */
+  FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync + biphase + block sync                     */
+  FMX_K_COUNT = 4
+};
+int fmx_timing_enable(void *handle, int enable);
+int fmx_kernel_times(void *handle, double *ms, int *launches, int n);
+
+/* ---- synthetic IQ (bench / tests input; see fmx_synth.h) ---- */
+typedef struct {
+  int iq_rate;
+  int kind;        /* 0 mono two-tone, 1 stereo, 2 stereo + RDS             */
+  float amplitude; /* 0.8                                                   */
+  float noise_std; /* AWGN per component (0 = none)                         */
+  uint32_t seed_base;
+  int max_offset_hz;
+  float rds_level; /* 0.05                                                  */
+  int n_bits;      /* RDS bit-table length per channel                      */
+} fmx_synth_config;
+/* RDS test pattern: encoded (differential) bits [n_ch][n_bits] and, if
+ * h_groups != NULL, the transmitted groups [n_ch][n_bits/104][4]. */
+int fmx_synth_rds_bits(const fmx_synth_config *cfg, uint32_t ch0, int n_ch, uint8_t *h_bits,
+                       uint16_t *h_groups);
+/* host generation: h_out [n_ch][2*n_samples]; h_bits [n_ch][n_bits] or NULL */
+int fmx_synth_host(const fmx_synth_config *cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
+                   const uint8_t *h_bits, uint8_t *h_out, size_t out_stride, int threads);
+/* device generation on the handle's stream: d_out [n_ch][out_stride] */
+int fmx_synth_device(void *handle, const fmx_synth_config *cfg, uint32_t ch0, int n_ch, int64_t sample0,
+                     int n_samples, const uint8_t *d_bits, uint8_t *d_out, size_t out_stride);
+
+/* ---- diagnostics (host only, no GPU needed) ---- */
+/* Filter taps the handle would use: which = 0 decimator, 1 IQ FIR,
+ * 2 pilot BPF, 3 L/R LPF, 4 audio resampler prototype, 5 RDS resampler
+ * prototype, 6 RDS 2.4 kHz LPF, 7 symsync RRC, 8 symsync derivative.
+ * Returns the tap count (negative on error). */
+int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap);
+/* liquid resamp_rrrf output schedule for rate 1/del over n_in inputs from
+ * the reset state: packed = i | (branch << 16) | (boundary << 24). */
+int fmx_resamp_schedule(float del, int n_in, int *packed, float *mu, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

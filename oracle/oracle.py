@@ -1,0 +1,199 @@
+"""oracle.py -- TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU
+restatement (oracle/libfmx_oracle.so) and of the reference's own compiled
+block sync / signal level (oracle/_ref/libfmx_ref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product (fmtuner-sdr_amd/) never does.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_LIB = os.path.join(_HERE, "libfmx_oracle.so")
+REF_LIB = os.path.join(_HERE, "_ref", "libfmx_ref.so")
+
+
+class OracleCfg(C.Structure):
+    _fields_ = [(n, C.c_int) for n in (
+        "iq_rate", "dsp_rate", "out_rate", "block", "w0_bandwidth_hz",
+        "bandwidth_hz", "dsp_agc", "stereo", "blend", "deemphasis",
+        "force_mono", "force_stereo", "rds")]
+
+
+class OracleGroup(C.Structure):
+    _fields_ = [("a", C.c_uint16), ("b", C.c_uint16), ("c", C.c_uint16),
+                ("d", C.c_uint16), ("errors", C.c_uint8), ("pad", C.c_uint8),
+                ("block_index", C.c_uint32)]
+
+
+class BlockInfo(C.Structure):
+    _fields_ = [("n_mpx", C.c_int), ("n_pcm", C.c_int), ("stereo_detected", C.c_int),
+                ("pilot_tenths_khz", C.c_int), ("clip_ratio", C.c_float),
+                ("n_groups", C.c_int)]
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = C.CDLL(ORACLE_LIB)
+        vp, i, sz = C.c_void_p, C.c_int, C.c_size_t
+        sigs = {
+            "oracle_pipeline_create": (vp, [C.POINTER(OracleCfg)]),
+            "oracle_pipeline_destroy": (None, [vp]),
+            "oracle_pipeline_reset": (None, [vp]),
+            "oracle_pipeline_block": (i, [vp, vp, i, vp, vp, vp, i, vp, i, C.POINTER(BlockInfo)]),
+            "oracle_pipeline_taps": (i, [vp, i, vp, i]),
+            "oracle_decim_create": (vp, [C.c_uint32, C.c_uint32, C.c_float]),
+            "oracle_decim_destroy": (None, [vp]),
+            "oracle_decim_reset": (None, [vp]),
+            "oracle_decim_execute_complex": (sz, [vp, vp, sz, vp, sz]),
+            "oracle_demod_create": (vp, [i, i]),
+            "oracle_demod_destroy": (None, [vp]),
+            "oracle_demod_reset": (None, [vp]),
+            "oracle_demod_set": (None, [vp, i, i]),
+            "oracle_demod_process_split_complex": (sz, [vp, vp, vp, vp, sz]),
+            "oracle_demod_process_split": (sz, [vp, vp, vp, vp, sz]),
+            "oracle_demod_clip_ratio": (C.c_float, [vp]),
+            "oracle_stereo_create": (vp, [i, i]),
+            "oracle_stereo_destroy": (None, [vp]),
+            "oracle_stereo_reset": (None, [vp]),
+            "oracle_stereo_set": (None, [vp, i, i]),
+            "oracle_stereo_process": (sz, [vp, vp, vp, vp, sz, C.POINTER(i), C.POINTER(i)]),
+            "oracle_stereo_process_trace": (sz, [vp, vp, vp, vp, sz, vp, vp]),
+            "oracle_afpost_create": (vp, [i, i]),
+            "oracle_afpost_destroy": (None, [vp]),
+            "oracle_afpost_reset": (None, [vp]),
+            "oracle_afpost_set_deemphasis": (None, [vp, i]),
+            "oracle_afpost_process": (sz, [vp, vp, vp, sz, vp, vp, sz]),
+            "oracle_rds_create": (vp, [i]),
+            "oracle_rds_destroy": (None, [vp]),
+            "oracle_rds_reset": (None, [vp]),
+            "oracle_rds_process": (i, [vp, vp, sz, vp, i, vp, i, C.POINTER(i)]),
+            "oracle_blocksync_create": (vp, []),
+            "oracle_blocksync_destroy": (None, [vp]),
+            "oracle_blocksync_push": (i, [vp, vp, i, vp, i]),
+            "oracle_run_many": (C.c_double, [C.POINTER(OracleCfg), i, vp, i, i, C.POINTER(C.c_double)]),
+        }
+        for k, (r, a) in sigs.items():
+            f = getattr(L, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def ref_available():
+    return os.path.exists(REF_LIB)
+
+
+def ref():
+    """The reference's own block_sync/group/util + signal_level, compiled by
+    oracle/Makefile from /root/reference (travels as a built .so)."""
+    global _ref
+    if _ref is None:
+        L = C.CDLL(REF_LIB)
+        vp, i = C.c_void_p, C.c_int
+        L.ref_blocksync_create.restype = vp
+        L.ref_blocksync_create.argtypes = []
+        L.ref_blocksync_destroy.restype = None
+        L.ref_blocksync_destroy.argtypes = [vp]
+        L.ref_blocksync_push.restype = i
+        L.ref_blocksync_push.argtypes = [vp, vp, i, vp, i]
+        L.ref_signal_level.restype = None
+        L.ref_signal_level.argtypes = [vp, C.c_size_t, i, C.c_double, C.c_double, C.c_double,
+                                       C.c_double, C.POINTER(C.c_double)]
+        L.ref_smooth_signal_level.restype = C.c_float
+        L.ref_smooth_signal_level.argtypes = [C.c_float, C.POINTER(i), C.POINTER(C.c_float)]
+        _ref = L
+    return _ref
+
+
+def make_cfg(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=4096,
+             w0_bandwidth_hz=194_000, bandwidth_hz=0, dsp_agc=0, stereo=1, blend=1,
+             deemphasis=0, force_mono=0, force_stereo=0, rds=1):
+    return OracleCfg(iq_rate, dsp_rate, out_rate, block, w0_bandwidth_hz, bandwidth_hz,
+                     dsp_agc, stereo, blend, deemphasis, force_mono, force_stereo, rds)
+
+
+def groups_to_tuples(arr, n):
+    return [(arr[k].a, arr[k].b, arr[k].c, arr[k].d, arr[k].errors) for k in range(n)]
+
+
+class Pipeline:
+    """One channel of the reference per-block body (main.cpp:1232-1308)."""
+
+    def __init__(self, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self.p = self.L.oracle_pipeline_create(C.byref(cfg))
+        if not self.p:
+            raise RuntimeError("oracle_pipeline_create failed")
+        self.M = cfg.iq_rate // cfg.dsp_rate
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.oracle_pipeline_destroy(self.p)
+            self.p = None
+
+    def reset(self):
+        self.L.oracle_pipeline_reset(self.p)
+
+    def block(self, iq):
+        """iq: uint8 array of 2*block*M bytes -> dict of outputs."""
+        iq = np.ascontiguousarray(iq, dtype=np.uint8)
+        B = self.cfg.block
+        mpx = np.zeros(B, np.float32)
+        pl = np.zeros(B, np.float32)
+        pr = np.zeros(B, np.float32)
+        g = (OracleGroup * 64)()
+        info = BlockInfo()
+        n = self.L.oracle_pipeline_block(self.p, iq.ctypes.data, iq.size // 2, mpx.ctypes.data,
+                                         pl.ctypes.data, pr.ctypes.data, B, g, 64, C.byref(info))
+        return dict(mpx=mpx[:info.n_mpx], pcm_l=pl[:n], pcm_r=pr[:n],
+                    stereo=info.stereo_detected, pilot=info.pilot_tenths_khz,
+                    clip=info.clip_ratio, groups=groups_to_tuples(g, min(info.n_groups, 64)))
+
+    def taps(self, which):
+        n = self.L.oracle_pipeline_taps(self.p, which, None, 0)
+        if n < 0:
+            return None
+        buf = np.zeros(n, np.float32)
+        self.L.oracle_pipeline_taps(self.p, which, buf.ctypes.data, n)
+        return buf
+
+
+def blocksync(bits):
+    L = lib()
+    p = L.oracle_blocksync_create()
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    cap = bits.size // 26 + 8
+    g = (OracleGroup * cap)()
+    n = L.oracle_blocksync_push(p, bits.ctypes.data, bits.size, g, cap)
+    L.oracle_blocksync_destroy(p)
+    return groups_to_tuples(g, min(n, cap))
+
+
+def ref_blocksync(bits):
+    R = ref()
+    p = R.ref_blocksync_create()
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    cap = bits.size // 26 + 8
+    g = (OracleGroup * cap)()
+    n = R.ref_blocksync_push(p, bits.ctypes.data, bits.size, g, cap)
+    R.ref_blocksync_destroy(p)
+    return groups_to_tuples(g, min(n, cap))
+
+
+def run_many(cfg, iq, n_blocks, threads):
+    """CPU baseline: iq [C][n_blocks][2*B*M] uint8, one channel per thread."""
+    iq = np.ascontiguousarray(iq, dtype=np.uint8)
+    chk = C.c_double()
+    secs = lib().oracle_run_many(C.byref(cfg), iq.shape[0], iq.ctypes.data, n_blocks,
+                                 threads, C.byref(chk))
+    return secs, chk.value

@@ -1,0 +1,99 @@
+"""Shared driver for the GPU parity tests and smoke(): runs the same
+synthetic IQ through libfmx (GPU) and through the oracle (CPU) block by
+block and returns both outputs."""
+import numpy as np
+
+
+def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None):
+    """iq: uint8 [C][nblk * 2*B*M]. Returns per-block lists of numpy outputs."""
+    C = iq.shape[0]
+    B = cfg.block
+    M = cfg.iq_rate // cfg.dsp_rate
+    n = n or B
+    h = fmx.Handle(cfg, C)
+    dev = torch.device("cuda")
+    d_iq = torch.from_numpy(np.ascontiguousarray(iq)).to(dev)
+    mpx = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    pl = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    pr = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    st = torch.zeros(C, dtype=torch.int32, device=dev)
+    pil = torch.zeros(C, dtype=torch.int32, device=dev)
+    clip = torch.zeros(C, dtype=torch.float32, device=dev)
+    GS = 8
+    grp = torch.zeros((C, GS, 4), dtype=torch.int32, device=dev)  # 16-byte fmx_rds_group
+    gcnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    out = fmx.BlockOut(mpx.data_ptr(), B, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(),
+                       st.data_ptr(), pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS,
+                       gcnt.data_ptr())
+    res = []
+    row = iq.shape[1]
+    for b in range(nblk):
+        if resets and b in resets:
+            h.reset(resets[b])
+        if params and b in params:
+            for (k, v, ch) in params[b]:
+                h.set_param(k, v, ch)
+        base = d_iq.data_ptr() + b * 2 * n * M
+        h.process_block(base, row, n, out)
+        h.sync()
+        g = grp.cpu().numpy().view(np.uint8).reshape(C, GS, 16)
+        gc = gcnt.cpu().numpy()
+        groups = []
+        for c in range(C):
+            lst = []
+            for k in range(min(int(gc[c]), GS)):
+                w = g[c, k]
+                a, bb, cc, d = np.frombuffer(w[:8].tobytes(), dtype=np.uint16)
+                lst.append((int(a), int(bb), int(cc), int(d), int(w[8])))
+            groups.append(lst)
+        res.append(dict(mpx=mpx[:, :n].cpu().numpy().copy(), pcm_l=pl.cpu().numpy().copy(),
+                        pcm_r=pr.cpu().numpy().copy(), count=cnt.cpu().numpy().copy(),
+                        stereo=st.cpu().numpy().copy(), pilot=pil.cpu().numpy().copy(),
+                        clip=clip.cpu().numpy().copy(), groups=groups))
+    h.close()
+    return res
+
+
+def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=None):
+    B = ocfg.block
+    M = ocfg.iq_rate // ocfg.dsp_rate
+    n = n or B
+    p = oracle.Pipeline(ocfg)
+    res = []
+    for b in range(nblk):
+        if resets and b in resets:
+            p.reset()
+        res.append(p.block(iq_row[b * 2 * n * M:(b + 1) * 2 * n * M]))
+    return res
+
+
+def compare(gres, ores, c, nblk):
+    """Per-channel comparison stats."""
+    mpx_err = 0.0
+    pcm_sq = 0.0
+    pcm_n = 0
+    pcm_max = 0.0
+    st_mismatch = 0
+    pil_mismatch = 0
+    cnt_mismatch = 0
+    g_gpu, g_ora = [], []
+    for b in range(nblk):
+        o, g = ores[b], gres[b]
+        mpx_err = max(mpx_err, float(np.max(np.abs(o["mpx"] - g["mpx"][c, :len(o["mpx"])]))))
+        k = len(o["pcm_l"])
+        if int(g["count"][c]) != k:
+            cnt_mismatch += 1
+        k = min(k, int(g["count"][c]))
+        dl = o["pcm_l"][:k] - g["pcm_l"][c, :k]
+        dr = o["pcm_r"][:k] - g["pcm_r"][c, :k]
+        pcm_sq += float(np.sum(dl * dl) + np.sum(dr * dr))
+        pcm_n += 2 * k
+        pcm_max = max(pcm_max, float(np.max(np.abs(dl))) if k else 0.0, float(np.max(np.abs(dr))) if k else 0.0)
+        st_mismatch += int(o["stereo"] != int(g["stereo"][c]))
+        pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
+        g_gpu += g["groups"][c]
+        g_ora += o["groups"]
+    return dict(mpx_max=mpx_err, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
+                stereo_mismatch=st_mismatch, pilot_mismatch=pil_mismatch, count_mismatch=cnt_mismatch,
+                groups_gpu=g_gpu, groups_oracle=g_ora)
