@@ -37,19 +37,28 @@ struct TimingSet {
   std::vector<int> chan_group;
   std::vector<FmxSched> hsched;
   std::vector<int> hcount;
-  FmxSched *d_sched = nullptr;
-  int *d_count = nullptr;
-  int *d_group = nullptr;
+  // device copies, double-buffered by step parity: step k+1 uploads while
+  // the consumers of step k may still run on another stream
+  FmxSched *d_sched[2] = {nullptr, nullptr};
+  int *d_count[2] = {nullptr, nullptr};
+  int *d_group[2] = {nullptr, nullptr};
   int stride = 0, cap_groups = 0;
-  bool group_dirty = true;
+  int cur = 0; // buffer holding the latest upload
 };
 
 struct Handle {
   fmx_config cfg{};
   int C = 0, device = 0, M = 1;
   std::string err;
-  hipStream_t stream = nullptr, stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // sA: frontend, resets, uploads; sB: stereo + audio; sC: RDS.  Step k's
+  // frontend runs while step k-1's stereo/RDS kernels (latency-bound, one
+  // lane per channel) still occupy a few SIMDs.
+  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr;
+  hipEvent_t evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr}, evC[2] = {nullptr, nullptr};
+  hipEvent_t evTmpB = nullptr, evTmpC = nullptr;
+  bool evB_set[2] = {false, false}, evC_set[2] = {false, false};
+  uint64_t step = 0;
+  int st_idx = 0;
   FmxDesign *hdes = nullptr;
   FmxDesign *ddes = nullptr;
   DesignExtras ex;
@@ -69,11 +78,11 @@ struct Handle {
   FmxRdsState *rds = nullptr;
   int *reset_mask = nullptr;
   std::vector<int> hmask;
-  // intermediates
-  float *mpx = nullptr, *pilot = nullptr, *lraw = nullptr, *rraw = nullptr, *rds_in = nullptr;
-  int *rds_count = nullptr, *tmp_count = nullptr, *tmp_int = nullptr;
+  // intermediates (double-buffered by step parity)
+  float *mpx[2] = {nullptr, nullptr}, *pilot[2] = {nullptr, nullptr}, *rds_in[2] = {nullptr, nullptr};
+  int *rds_count[2] = {nullptr, nullptr};
+  float *lraw = nullptr, *rraw = nullptr;
   int rds_stride = 0;
-  int st_parity = 0;
   uint32_t block_index = 0;
   TimingSet t_af, t_mono, t_rds;
   // kernel timing
@@ -161,10 +170,11 @@ static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
   t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
   int rc;
-  if ((rc = dalloc(h, &t.d_sched, static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &t.d_count, static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &t.d_group, static_cast<size_t>(h->C))) != FMX_OK) return rc;
-  t.group_dirty = true;
+  for (int b = 0; b < 2; ++b) {
+    if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &t.d_group[b], static_cast<size_t>(h->C))) != FMX_OK) return rc;
+  }
   return FMX_OK;
 }
 
@@ -185,7 +195,6 @@ static void tset_reset_channel(TimingSet &t, int c) {
     g = static_cast<int>(t.groups.size()) - 1;
   }
   t.chan_group[static_cast<size_t>(c)] = g;
-  t.group_dirty = true;
 }
 
 static void tset_compact(TimingSet &t) {
@@ -205,7 +214,6 @@ static void tset_compact(TimingSet &t) {
       }
       remap[i] = found;
     }
-  if (ng.size() != t.groups.size() || ng.empty()) t.group_dirty = true;
   for (int &g : t.chan_group) g = remap[static_cast<size_t>(g)];
   if (ng.empty()) {
     ResampTiming r;
@@ -216,22 +224,27 @@ static void tset_compact(TimingSet &t) {
   t.groups = ng;
 }
 
-// Simulate n inputs for every group, upload schedules; returns max count.
-static int tset_advance(Handle *h, TimingSet &t, int n, int *max_count) {
+// Simulate n inputs for every group and upload the schedules into buffer
+// `buf` (step parity) on stream sA; returns the largest output count.
+static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
   tset_compact(t);
   const int G = static_cast<int>(t.groups.size());
   if (G > t.cap_groups) {
-    h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_sched)), h->allocs.end());
-    h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_count)), h->allocs.end());
-    hipFree(t.d_sched);
-    hipFree(t.d_count);
+    HIP_TRY(hipDeviceSynchronize());
+    for (int b = 0; b < 2; ++b) {
+      for (void *p : {static_cast<void *>(t.d_sched[b]), static_cast<void *>(t.d_count[b])}) {
+        h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), p), h->allocs.end());
+        HIP_TRY(hipFree(p));
+      }
+    }
     t.cap_groups = G * 2;
     t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
     t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
-    HIP_TRY(hipMalloc(&t.d_sched, sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.cap_groups));
-    HIP_TRY(hipMalloc(&t.d_count, sizeof(int) * static_cast<size_t>(t.cap_groups)));
-    h->allocs.push_back(t.d_sched);
-    h->allocs.push_back(t.d_count);
+    int rc;
+    for (int b = 0; b < 2; ++b) {
+      if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
+      if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
+    }
   }
   int mx = 0;
   for (int g = 0; g < G; ++g) {
@@ -244,17 +257,24 @@ static int tset_advance(Handle *h, TimingSet &t, int n, int *max_count) {
     t.hcount[static_cast<size_t>(g)] = k;
     mx = std::max(mx, k);
   }
-  HIP_TRY(hipMemcpyAsync(t.d_sched, t.hsched.data(), sizeof(FmxSched) * static_cast<size_t>(t.stride) * G,
-                         hipMemcpyHostToDevice, h->stream));
-  HIP_TRY(hipMemcpyAsync(t.d_count, t.hcount.data(), sizeof(int) * G, hipMemcpyHostToDevice, h->stream));
-  if (t.group_dirty) {
-    HIP_TRY(hipMemcpyAsync(t.d_group, t.chan_group.data(), sizeof(int) * h->C, hipMemcpyHostToDevice,
-                           h->stream));
-    t.group_dirty = false;
-  }
-  // hipMemcpyAsync from pageable memory is staged synchronously, so the host
-  // vectors may be reused immediately.
+  // pageable-memory copies are staged before hipMemcpyAsync returns, so the
+  // host vectors can be reused by the next call immediately
+  HIP_TRY(hipMemcpyAsync(t.d_sched[buf], t.hsched.data(), sizeof(FmxSched) * static_cast<size_t>(t.stride) * G,
+                         hipMemcpyHostToDevice, h->sA));
+  HIP_TRY(hipMemcpyAsync(t.d_count[buf], t.hcount.data(), sizeof(int) * G, hipMemcpyHostToDevice, h->sA));
+  HIP_TRY(hipMemcpyAsync(t.d_group[buf], t.chan_group.data(), sizeof(int) * h->C, hipMemcpyHostToDevice, h->sA));
+  t.cur = buf;
   if (max_count) *max_count = mx;
+  return FMX_OK;
+}
+
+// Make sA wait for everything queued on sB and sC (used before resets,
+// parameter uploads and the single-stream stage entry points).
+static int join_into_A(Handle *h) {
+  HIP_TRY(hipEventRecord(h->evTmpB, h->sB));
+  HIP_TRY(hipEventRecord(h->evTmpC, h->sC));
+  HIP_TRY(hipStreamWaitEvent(h->sA, h->evTmpB, 0));
+  HIP_TRY(hipStreamWaitEvent(h->sA, h->evTmpC, 0));
   return FMX_OK;
 }
 
@@ -286,8 +306,10 @@ static int apply_resets(Handle *h) {
   bool any = false;
   for (int v : h->hmask) any |= (v != 0);
   if (!any) return FMX_OK;
-  HIP_TRY(hipMemcpyAsync(h->reset_mask, h->hmask.data(), sizeof(int) * h->C, hipMemcpyHostToDevice, h->stream));
-  int rc = launch_reset(reset_args(h), h->stream);
+  int rc = join_into_A(h);
+  if (rc != FMX_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(h->reset_mask, h->hmask.data(), sizeof(int) * h->C, hipMemcpyHostToDevice, h->sA));
+  rc = launch_reset(reset_args(h), h->sA);
   if (rc != FMX_OK) {
     h->err = "reset kernel launch failed";
     return rc;
@@ -298,7 +320,9 @@ static int apply_resets(Handle *h) {
 
 static int sync_params(Handle *h) {
   if (!h->par_dirty) return FMX_OK;
-  HIP_TRY(hipMemcpyAsync(h->dpar, h->hpar.data(), sizeof(FmxChanParam) * h->C, hipMemcpyHostToDevice, h->stream));
+  int rc = join_into_A(h);
+  if (rc != FMX_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(h->dpar, h->hpar.data(), sizeof(FmxChanParam) * h->C, hipMemcpyHostToDevice, h->sA));
   h->par_dirty = false;
   return FMX_OK;
 }
@@ -334,18 +358,22 @@ static void set_agc(Handle *h, int c, int mode) { // fm_demod.cpp:210-217
 
 static void destroy(Handle *h) {
   if (!h) return;
-  if (h->stream) hipStreamSynchronize(h->stream);
-  if (h->stream2) hipStreamSynchronize(h->stream2);
+  if (h->sA) hipStreamSynchronize(h->sA);
+  if (h->sB) hipStreamSynchronize(h->sB);
+  if (h->sC) hipStreamSynchronize(h->sC);
   for (auto &p : h->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
   }
   for (auto e : h->pool) hipEventDestroy(e);
   for (void *p : h->allocs) hipFree(p);
-  if (h->ev_fork) hipEventDestroy(h->ev_fork);
-  if (h->ev_join) hipEventDestroy(h->ev_join);
-  if (h->stream) hipStreamDestroy(h->stream);
-  if (h->stream2) hipStreamDestroy(h->stream2);
+  for (int b = 0; b < 2; ++b)
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b]})
+      if (e) hipEventDestroy(e);
+  if (h->evTmpB) hipEventDestroy(h->evTmpB);
+  if (h->evTmpC) hipEventDestroy(h->evTmpC);
+  for (hipStream_t st : {h->sA, h->sB, h->sC})
+    if (st) hipStreamDestroy(st);
   delete h->hdes;
   delete h;
 }
@@ -384,10 +412,16 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     h->err = "dsp_rate / out_rate must be >= 3";
     return FMX_E_INVALID;
   }
-  HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&h->sA, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+  for (int b = 0; b < 2; ++b) {
+    HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->evB[b], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->evC[b], hipEventDisableTiming));
+  }
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, hipEventDisableTiming));
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
@@ -416,7 +450,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->fd_prev, C * 2)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->iq_hist, C * (FMX_IQ_MAXLEN - 1))) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->st_hist, 2 * C * FMX_HIST)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->st_hist, FMX_ST_BUFS * C * FMX_HIST)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->lr_hist, C * 2 * (FMX_LR_LEN - 1))) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->af_win, C * 64)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->af_iir, C * 4)) != FMX_OK) return rc;
@@ -428,18 +462,20 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->rds, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->reset_mask, C)) != FMX_OK) return rc;
   // intermediates
-  if ((rc = dalloc(h, &h->mpx, C * B)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->pilot, C * B)) != FMX_OK) return rc;
+  for (int b = 0; b < 2; ++b) {
+    if ((rc = dalloc(h, &h->mpx[b], C * B)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->pilot[b], C * B)) != FMX_OK) return rc;
+  }
   if ((rc = dalloc(h, &h->lraw, C * B)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->rraw, C * B)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
   h->rds_stride = h->t_rds.stride;
-  if ((rc = dalloc(h, &h->rds_in, C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->rds_count, C)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->tmp_count, C)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->tmp_int, C * 2)) != FMX_OK) return rc;
+  for (int b = 0; b < 2; ++b) {
+    if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
+  }
   // construct every object (RS_CREATE) then apply main.cpp's configuration
   std::fill(h->hmask.begin(), h->hmask.end(), static_cast<int>(RS_CREATE));
   for (int c = 0; c < n; ++c) {
@@ -450,31 +486,31 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   }
   rc = prepare(h);
   if (rc != FMX_OK) return rc;
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipStreamSynchronize(h->sA));
   return FMX_OK;
 }
 
-static FeArgs fe_args(Handle *h, int n, int mode) {
+static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   FeArgs a{};
   a.des = h->ddes;
   a.par = h->dpar;
   a.C = h->C;
   a.n = n;
   a.in_mode = mode;
-  a.st_parity = h->st_parity;
+  a.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
+  a.st_hist_wr = h->st_hist + static_cast<size_t>((h->st_idx + 1) % FMX_ST_BUFS) * h->C * FMX_HIST;
   a.dec_hist = h->dec_hist;
   a.dec_valid = h->dec_valid;
   a.dc_v = h->dc_v;
   a.iq_hist = h->iq_hist;
   a.agc = h->agc;
   a.fd_prev = h->fd_prev;
-  a.st_hist = h->st_hist;
   a.rds_hist = h->rds_hist;
   a.clip_out = h->clip;
-  a.rds_count = h->rds_count;
-  a.rds_sched = h->t_rds.d_sched;
-  a.rds_sched_n = h->t_rds.d_count;
-  a.rds_group = h->t_rds.d_group;
+  a.rds_count = h->rds_count[buf];
+  a.rds_sched = h->t_rds.d_sched[h->t_rds.cur];
+  a.rds_sched_n = h->t_rds.d_count[h->t_rds.cur];
+  a.rds_group = h->t_rds.d_group[h->t_rds.cur];
   a.rds_sched_stride = h->t_rds.stride;
   return a;
 }
@@ -492,26 +528,25 @@ static AudioArgs audio_args(Handle *h, int n, int mode, TimingSet *t) {
   a.mono_win = h->mono_win;
   a.mono_iir = h->mono_iir;
   if (t) {
-    a.sched = t->d_sched;
-    a.sched_n = t->d_count;
-    a.group = t->d_group;
+    a.sched = t->d_sched[t->cur];
+    a.sched_n = t->d_count[t->cur];
+    a.group = t->d_group[t->cur];
     a.sched_stride = t->stride;
   }
   return a;
 }
 
-static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride) {
+static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
   PllArgs a{};
   a.des = h->ddes;
   a.par = h->dpar;
   a.C = h->C;
   a.n = n;
-  a.st_parity = h->st_parity;
-  a.pilot = h->pilot;
+  a.pilot = h->pilot[buf];
   a.pilot_stride = h->cfg.block;
   a.mpx = mpx;
   a.mpx_stride = mpx_stride;
-  a.st_hist = h->st_hist;
+  a.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
   a.lraw = h->lraw;
   a.rraw = h->rraw;
   a.lr_stride = h->cfg.block;
@@ -519,13 +554,13 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride) {
   return a;
 }
 
-static RdsArgs rds_args(Handle *h) {
+static RdsArgs rds_args(Handle *h, int buf) {
   RdsArgs a{};
   a.des = h->ddes;
   a.C = h->C;
-  a.in = h->rds_in;
+  a.in = h->rds_in[buf];
   a.in_stride = h->rds_stride;
-  a.in_count = h->rds_count;
+  a.in_count = h->rds_count[buf];
   a.st = h->rds;
   a.ring = h->ring;
   a.block_index = h->block_index;
@@ -540,6 +575,12 @@ static int check_n(Handle *h, int n) {
   return FMX_OK;
 }
 
+// end of a step: advance the stereo-history rotation and the step counter
+static void step_done(Handle *h, bool stereo_hist_written) {
+  if (stereo_hist_written) h->st_idx = (h->st_idx + 1) % FMX_ST_BUFS;
+  h->step++;
+}
+
 static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *o) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
@@ -547,82 +588,92 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     h->err = "process_block: d_iq, d_pcm_l, d_pcm_r and d_pcm_count are required";
     return FMX_E_INVALID;
   }
+  if (n == 0) return FMX_OK;
   if ((rc = prepare(h)) != FMX_OK) return rc;
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
-  if (n == 0) return FMX_OK;
-  if (rds && (rc = tset_advance(h, h->t_rds, n, nullptr)) != FMX_OK) return rc;
+  const int buf = static_cast<int>(h->step & 1);
+  // buffers of parity `buf` were last read by step k-2 on sB / sC
+  if (h->evB_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf], 0));
+  if (h->evC_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf], 0));
+  if (o->d_mpx) { // a caller-owned MPX buffer is read by step k-1's stereo/RDS kernels
+    if (h->evB_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf ^ 1], 0));
+    if (h->evC_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf ^ 1], 0));
+  }
+  if (rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
-  int max_out = 0;
-  if ((rc = tset_advance(h, *tau, n, &max_out)) != FMX_OK) return rc;
-  float *mpx = o->d_mpx ? o->d_mpx : h->mpx;
+  if ((rc = tset_advance(h, *tau, n, buf, nullptr)) != FMX_OK) return rc;
+  float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
-  // ---- front end ----
+  // ---- front end (sA) ----
   {
-    FeArgs a = fe_args(h, n, h->M > 1 ? FE_IN_U8_DECIM : FE_IN_U8_DIRECT);
+    FeArgs a = fe_args(h, n, h->M > 1 ? FE_IN_U8_DECIM : FE_IN_U8_DIRECT, buf);
     a.iq = d_iq;
     a.iq_stride = iq_stride;
     a.mpx_out = mpx;
     a.mpx_stride = mpx_stride;
     a.do_demod = 1;
     if (stereo) {
-      a.pilot_out = h->pilot;
+      a.pilot_out = h->pilot[buf];
       a.pilot_stride = h->cfg.block;
     }
     if (rds) {
-      a.rds_out = h->rds_in;
+      a.rds_out = h->rds_in[buf];
       a.rds_stride = h->rds_stride;
     }
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
-    KTimer t(h, FMX_K_FRONTEND, h->stream);
-    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->stream)) != FMX_OK) {
+    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA)) != FMX_OK) {
       h->err = "frontend launch failed";
       return rc;
     }
   }
-  // ---- RDS on the second stream, concurrent with stereo/audio ----
+  HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
+  // ---- RDS (sC) ----
+  HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   if (rds) {
-    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-    RdsArgs a = rds_args(h);
+    RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
-    KTimer t(h, FMX_K_RDS, h->stream2);
-    if ((rc = launch_rds(a, h->stream2)) != FMX_OK) {
+    KTimer t(h, FMX_K_RDS, h->sC);
+    if ((rc = launch_rds(a, h->sC)) != FMX_OK) {
       h->err = "rds launch failed";
       return rc;
     }
+  } else if (o->d_group_count) {
+    HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
   }
+  HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
+  h->evC_set[buf] = true;
+  // ---- stereo + audio (sB) ----
+  HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   if (stereo) {
     {
-      PllArgs a = pll_args(h, n, mpx, mpx_stride);
+      PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
       a.stereo_out = o->d_stereo;
       a.pilot_tenths_out = o->d_pilot_tenths;
-      KTimer t(h, FMX_K_STEREO, h->stream);
-      if ((rc = launch_pll(a, h->stream)) != FMX_OK) {
+      KTimer t(h, FMX_K_STEREO, h->sB);
+      if ((rc = launch_pll(a, h->sB)) != FMX_OK) {
         h->err = "pll launch failed";
         return rc;
       }
     }
-    {
-      AudioArgs a = audio_args(h, n, 0, &h->t_af);
-      a.in_l = h->lraw;
-      a.in_r = h->rraw;
-      a.in_stride = h->cfg.block;
-      a.out_l = o->d_pcm_l;
-      a.out_r = o->d_pcm_r;
-      a.out_stride = o->pcm_stride;
-      a.out_count = o->d_pcm_count;
-      a.cap = h->cfg.block;
-      a.clamp = 1;
-      KTimer t(h, FMX_K_AUDIO, h->stream);
-      if ((rc = launch_audio(a, h->stream)) != FMX_OK) {
-        h->err = "audio launch failed";
-        return rc;
-      }
+    AudioArgs a = audio_args(h, n, 0, &h->t_af);
+    a.in_l = h->lraw;
+    a.in_r = h->rraw;
+    a.in_stride = h->cfg.block;
+    a.out_l = o->d_pcm_l;
+    a.out_r = o->d_pcm_r;
+    a.out_stride = o->pcm_stride;
+    a.out_count = o->d_pcm_count;
+    a.cap = h->cfg.block;
+    a.clamp = 1;
+    KTimer t(h, FMX_K_AUDIO, h->sB);
+    if ((rc = launch_audio(a, h->sB)) != FMX_OK) {
+      h->err = "audio launch failed";
+      return rc;
     }
-    h->st_parity ^= 1;
   } else {
     AudioArgs a = audio_args(h, n, 3, &h->t_mono);
     a.in_l = mpx;
@@ -634,30 +685,44 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.out_count = o->d_pcm_count;
     a.cap = 1 << 30;
     a.clamp = 1;
-    KTimer t(h, FMX_K_AUDIO, h->stream);
-    if ((rc = launch_audio(a, h->stream)) != FMX_OK) {
-      h->err = "audio launch failed";
-      return rc;
+    {
+      KTimer t(h, FMX_K_AUDIO, h->sB);
+      if ((rc = launch_audio(a, h->sB)) != FMX_OK) {
+        h->err = "audio launch failed";
+        return rc;
+      }
     }
+    if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->sB));
+    if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->sB));
   }
-  if (rds) {
-    HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-  } else if (o->d_group_count) {
-    HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->stream));
-  }
-  if (!stereo) {
-    if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->stream));
-    if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->stream));
-  }
+  HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
+  h->evB_set[buf] = true;
   h->block_index++;
-  (void)max_out;
+  step_done(h, stereo);
+  return FMX_OK;
+}
+
+// Stage entry points run every kernel on sA after the pipelined streams
+// have drained into it.
+static int stage_begin(Handle *h, int n) {
+  int rc;
+  if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  if ((rc = prepare(h)) != FMX_OK) return rc;
+  return join_into_A(h);
+}
+// later pipelined work on sB / sC must see the stage's results
+static int stage_end(Handle *h) {
+  const int buf = static_cast<int>(h->step & 1);
+  HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
+  HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   return FMX_OK;
 }
 
 } // namespace fmx
 
 using namespace fmx;
+
 
 static Handle *H(void *p) { return static_cast<Handle *>(p); }
 
@@ -687,8 +752,9 @@ const char *fmx_last_error(void *handle) { return handle ? H(handle)->err.c_str(
 int fmx_sync(void *handle) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  HIP_TRY(hipStreamSynchronize(h->stream2));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipStreamSynchronize(h->sC));
+  HIP_TRY(hipStreamSynchronize(h->sB));
+  HIP_TRY(hipStreamSynchronize(h->sA));
   return FMX_OK;
 }
 
@@ -756,46 +822,52 @@ int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out,
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   int rc;
-  if ((rc = check_n(h, n_out)) != FMX_OK) return rc;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = stage_begin(h, n_out)) != FMX_OK) return rc;
   if (n_out == 0) return FMX_OK;
   if (h->M == 1) {
     h->err = "fmx_decimate needs iq_rate > dsp_rate";
     return FMX_E_INVALID;
   }
-  FeArgs a = fe_args(h, n_out, FE_IN_U8_DECIM);
+  FeArgs a = fe_args(h, n_out, FE_IN_U8_DECIM, 0);
   a.iq = d_iq;
   a.iq_stride = iq_stride;
   a.bb_out = d_out;
   a.bb_stride = out_stride;
   a.do_demod = 0;
   a.clip_out = nullptr;
-  KTimer t(h, FMX_K_FRONTEND, h->stream);
-  return launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->stream);
+  {
+    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA)) != FMX_OK) return rc;
+  }
+  return stage_end(h);
 }
 
-int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride, float *d_mono,
-              int mono_stride, int *d_mono_count) {
-  Handle *h = H(handle);
-  if (!h) return FMX_E_INVALID;
+static int demod_common(Handle *h, int mode, const void *d_in, size_t in_stride, int n, float *d_mpx,
+                        int mpx_stride, float *d_mono, int mono_stride, int *d_mono_count, float *d_clip) {
   int rc;
-  if ((rc = check_n(h, n)) != FMX_OK) return rc;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
-  float *mpx = d_mpx ? d_mpx : h->mpx;
+  const int buf = static_cast<int>(h->step & 1);
+  float *mpx = d_mpx ? d_mpx : h->mpx[buf];
   const int ms = d_mpx ? mpx_stride : h->cfg.block;
   {
-    FeArgs a = fe_args(h, n, FE_IN_CF);
-    a.in_f = d_iq_cf;
-    a.in_stride = in_stride;
+    FeArgs a = fe_args(h, n, mode, buf);
+    if (mode == FE_IN_CF) {
+      a.in_f = static_cast<const float *>(d_in);
+      a.in_stride = static_cast<int>(in_stride);
+    } else {
+      a.iq = static_cast<const uint8_t *>(d_in);
+      a.iq_stride = in_stride;
+    }
     a.mpx_out = mpx;
     a.mpx_stride = ms;
     a.do_demod = 1;
-    KTimer t(h, FMX_K_FRONTEND, h->stream);
-    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+    if (d_clip) a.clip_out = d_clip;
+    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    if ((rc = launch_frontend_m(a, 1, 1, h->sA)) != FMX_OK) return rc;
   }
   if (d_mono) {
-    if ((rc = tset_advance(h, h->t_mono, n, nullptr)) != FMX_OK) return rc;
+    if ((rc = tset_advance(h, h->t_mono, n, buf, nullptr)) != FMX_OK) return rc;
     AudioArgs a = audio_args(h, n, 2, &h->t_mono);
     a.in_l = mpx;
     a.in_stride = ms;
@@ -805,12 +877,53 @@ int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d
     a.out_count = d_mono_count;
     a.cap = 1 << 30;
     a.clamp = 0;
-    KTimer t(h, FMX_K_AUDIO, h->stream);
-    if ((rc = launch_audio(a, h->stream)) != FMX_OK) return rc;
+    KTimer t(h, FMX_K_AUDIO, h->sA);
+    if ((rc = launch_audio(a, h->sA)) != FMX_OK) return rc;
   } else if (d_mono_count) {
-    HIP_TRY(hipMemsetAsync(d_mono_count, 0, sizeof(int) * h->C, h->stream));
+    HIP_TRY(hipMemsetAsync(d_mono_count, 0, sizeof(int) * h->C, h->sA));
   }
-  return FMX_OK;
+  return stage_end(h);
+}
+
+int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride, float *d_mono,
+              int mono_stride, int *d_mono_count) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  return demod_common(h, FE_IN_CF, d_iq_cf, static_cast<size_t>(in_stride), n, d_mpx, mpx_stride, d_mono,
+                      mono_stride, d_mono_count, nullptr);
+}
+
+int fmx_demod_u8(void *handle, const uint8_t *d_iq, size_t iq_stride, int n, float *d_mpx, int mpx_stride,
+                 float *d_mono, int mono_stride, int *d_mono_count, float *d_clip_ratio) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  return demod_common(h, FE_IN_U8_DIRECT, d_iq, iq_stride, n, d_mpx, mpx_stride, d_mono, mono_stride,
+                      d_mono_count, d_clip_ratio);
+}
+
+int fmx_downsample(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_out, int out_stride,
+                   int *d_count) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  int rc;
+  if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
+  if (n == 0) return FMX_OK;
+  const int buf = static_cast<int>(h->step & 1);
+  if ((rc = tset_advance(h, h->t_mono, n, buf, nullptr)) != FMX_OK) return rc;
+  AudioArgs a = audio_args(h, n, 2, &h->t_mono);
+  a.in_l = d_mpx;
+  a.in_stride = mpx_stride;
+  a.out_l = d_out;
+  a.out_r = d_out;
+  a.out_stride = out_stride;
+  a.out_count = d_count;
+  a.cap = 1 << 30;
+  a.clamp = 0;
+  {
+    KTimer t(h, FMX_K_AUDIO, h->sA);
+    if ((rc = launch_audio(a, h->sA)) != FMX_OK) return rc;
+  }
+  return stage_end(h);
 }
 
 int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_left, float *d_right, int lr_stride,
@@ -818,25 +931,26 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   int rc;
-  if ((rc = check_n(h, n)) != FMX_OK) return rc;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
+  const int buf = static_cast<int>(h->step & 1);
   {
-    FeArgs a = fe_args(h, n, FE_IN_MPX);
+    FeArgs a = fe_args(h, n, FE_IN_MPX, buf);
     a.in_f = d_mpx;
     a.in_stride = mpx_stride;
-    a.pilot_out = h->pilot;
+    a.pilot_out = h->pilot[buf];
     a.pilot_stride = h->cfg.block;
     a.do_demod = 0;
-    KTimer t(h, FMX_K_FRONTEND, h->stream);
-    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+    a.clip_out = nullptr;
+    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    if ((rc = launch_frontend_m(a, 1, 1, h->sA)) != FMX_OK) return rc;
   }
   {
-    PllArgs a = pll_args(h, n, d_mpx, mpx_stride);
+    PllArgs a = pll_args(h, n, d_mpx, mpx_stride, buf);
     a.stereo_out = d_stereo;
     a.pilot_tenths_out = d_pilot_tenths;
-    KTimer t(h, FMX_K_STEREO, h->stream);
-    if ((rc = launch_pll(a, h->stream)) != FMX_OK) return rc;
+    KTimer t(h, FMX_K_STEREO, h->sA);
+    if ((rc = launch_pll(a, h->sA)) != FMX_OK) return rc;
   }
   {
     AudioArgs a = audio_args(h, n, 4, nullptr);
@@ -846,11 +960,12 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
     a.lr_out_l = d_left;
     a.lr_out_r = d_right;
     a.lr_out_stride = lr_stride;
-    KTimer t(h, FMX_K_AUDIO, h->stream);
-    if ((rc = launch_audio(a, h->stream)) != FMX_OK) return rc;
+    KTimer t(h, FMX_K_AUDIO, h->sA);
+    if ((rc = launch_audio(a, h->sA)) != FMX_OK) return rc;
   }
-  h->st_parity ^= 1;
-  return FMX_OK;
+  rc = stage_end(h);
+  step_done(h, true);
+  return rc;
 }
 
 int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_stride, int n, float *d_out_l,
@@ -858,16 +973,18 @@ int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_s
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   int rc;
-  if ((rc = check_n(h, n)) != FMX_OK) return rc;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0 || cap <= 0) return FMX_OK;
   // AFPostProcessor::process stops consuming input once outCapacity outputs
   // are written; only the no-truncation case is supported here.
   std::vector<ResampTiming> saved = h->t_af.groups;
+  std::vector<int> saved_map = h->t_af.chan_group;
   int mx = 0;
-  if ((rc = tset_advance(h, h->t_af, n, &mx)) != FMX_OK) return rc;
+  const int buf = static_cast<int>(h->step & 1);
+  if ((rc = tset_advance(h, h->t_af, n, buf, &mx)) != FMX_OK) return rc;
   if (mx > cap) {
     h->t_af.groups = saved;
+    h->t_af.chan_group = saved_map;
     h->err = "fmx_afpost: outCapacity smaller than the produced sample count is not supported";
     return FMX_E_CAPACITY;
   }
@@ -881,8 +998,11 @@ int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_s
   a.out_count = d_count;
   a.cap = cap;
   a.clamp = 0;
-  KTimer t(h, FMX_K_AUDIO, h->stream);
-  return launch_audio(a, h->stream);
+  {
+    KTimer t(h, FMX_K_AUDIO, h->sA);
+    if ((rc = launch_audio(a, h->sA)) != FMX_OK) return rc;
+  }
+  return stage_end(h);
 }
 
 int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_group *d_groups, int groups_stride,
@@ -890,31 +1010,34 @@ int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_gro
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   int rc;
-  if ((rc = check_n(h, n)) != FMX_OK) return rc;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) {
-    if (d_group_count) HIP_TRY(hipMemsetAsync(d_group_count, 0, sizeof(int) * h->C, h->stream));
+    if (d_group_count) HIP_TRY(hipMemsetAsync(d_group_count, 0, sizeof(int) * h->C, h->sA));
     return FMX_OK;
   }
-  if ((rc = tset_advance(h, h->t_rds, n, nullptr)) != FMX_OK) return rc;
+  const int buf = static_cast<int>(h->step & 1);
+  if ((rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   {
-    FeArgs a = fe_args(h, n, FE_IN_MPX);
+    FeArgs a = fe_args(h, n, FE_IN_MPX, buf);
     a.in_f = d_mpx;
     a.in_stride = mpx_stride;
-    a.rds_out = h->rds_in;
+    a.rds_out = h->rds_in[buf];
     a.rds_stride = h->rds_stride;
     a.do_demod = 0;
-    KTimer t(h, FMX_K_FRONTEND, h->stream);
-    if ((rc = launch_frontend_m(a, 1, 1, h->stream)) != FMX_OK) return rc;
+    a.clip_out = nullptr;
+    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    if ((rc = launch_frontend_m(a, 1, 1, h->sA)) != FMX_OK) return rc;
   }
-  RdsArgs a = rds_args(h);
+  RdsArgs a = rds_args(h, buf);
   a.groups = d_groups;
   a.groups_stride = d_groups ? groups_stride : 0;
   a.group_count = d_group_count;
-  KTimer t(h, FMX_K_RDS, h->stream);
-  rc = launch_rds(a, h->stream);
+  {
+    KTimer t(h, FMX_K_RDS, h->sA);
+    if ((rc = launch_rds(a, h->sA)) != FMX_OK) return rc;
+  }
   h->block_index++;
-  return rc;
+  return stage_end(h);
 }
 
 int fmx_malloc(void *handle, void **d_ptr, size_t bytes) {
@@ -937,22 +1060,22 @@ int fmx_free(void *handle, void *d_ptr) {
 int fmx_memcpy_h2d(void *handle, void *d_dst, const void *h_src, size_t bytes) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice));
   return FMX_OK;
 }
 int fmx_memcpy_d2h(void *handle, void *h_dst, const void *d_src, size_t bytes) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  HIP_TRY(hipStreamSynchronize(h->stream2));
-  HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost));
   return FMX_OK;
 }
 int fmx_memset(void *handle, void *d_ptr, int value, size_t bytes) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  HIP_TRY(hipMemsetAsync(d_ptr, value, bytes, h->stream));
+  HIP_TRY(hipMemsetAsync(d_ptr, value, bytes, h->sA));
+  HIP_TRY(hipStreamSynchronize(h->sA));
   return FMX_OK;
 }
 
@@ -960,8 +1083,7 @@ int fmx_timing_enable(void *handle, int enable) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   if (h->timing && !enable) {
-    hipStreamSynchronize(h->stream);
-    hipStreamSynchronize(h->stream2);
+    (void)hipDeviceSynchronize();
     collect_timing(h);
   }
   h->timing = enable != 0;
@@ -975,8 +1097,7 @@ int fmx_timing_enable(void *handle, int enable) {
 int fmx_kernel_times(void *handle, double *ms, int *launches, int n) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  hipStreamSynchronize(h->stream);
-  hipStreamSynchronize(h->stream2);
+  (void)hipDeviceSynchronize();
   collect_timing(h);
   for (int k = 0; k < n && k < FMX_K_COUNT; ++k) {
     if (ms) ms[k] = h->kms[k];
@@ -1073,7 +1194,7 @@ int fmx_synth_device(void *handle, const fmx_synth_config *cfg, uint32_t ch0, in
                      int n_samples, const uint8_t *d_bits, uint8_t *d_out, size_t out_stride) {
   Handle *h = H(handle);
   if (!h || !cfg) return FMX_E_INVALID;
-  return launch_synth(*cfg, ch0, n_ch, sample0, n_samples, d_bits, d_out, out_stride, h->stream);
+  return launch_synth(*cfg, ch0, n_ch, sample0, n_samples, d_bits, d_out, out_stride, h->sA);
 }
 
 /* ---------------- diagnostics (no GPU needed) ---------------- */

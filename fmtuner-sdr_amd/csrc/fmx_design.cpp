@@ -186,6 +186,8 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     d->dec_scale = 2.0f * cutoff;
     constexpr float kScale = 1.0f / 127.5f;
     for (int i = 0; i < d->dec_len; ++i) d->dec_taps[i] = d->dec_taps_raw[i] * kScale;
+    for (int p = 0; p < M; ++p)
+      for (int q = 0; q < d->dec_tpp; ++q) d->dec_poly[p * d->dec_tpp + q] = d->dec_taps[q * M + p];
   } else {
     d->dec_scale = 1.0f;
   }
@@ -310,6 +312,10 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
       ex->rrc_d = dh;
     }
   }
+  for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
+    for (int k = 0; k < d->iq_len[i]; ++k) d->iq_pad[i][k + 5] = d->iq_taps[i][k];
+  for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
+  for (int k = 0; k < FMX_LR_LEN; ++k) d->lr_pad[k + 5] = d->lr_taps[k];
   if (ex) {
     ex->proto_af = proto_af;
     ex->proto_rds = proto_rds;

@@ -24,6 +24,7 @@
 #define FMX_SS_SUB 18        // (2*32*3*3+1 - 1) / 32
 #define FMX_HIST 512         // stereo MPX history (>= pilot taps - 1 and delay line)
 #define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
+#define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
 
 typedef struct {
   float x, y;
@@ -38,17 +39,21 @@ typedef struct {
   float dec_scale;
   float dec_taps[FMX_MAX_DEC];
   float dec_taps_raw[FMX_MAX_DEC];
+  float dec_poly[FMX_MAX_DEC]; // [p][q] = dec_taps[q*M + p]  (phase-major)
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
   int iq_len[FMX_IQ_DESIGNS];
   float iq_scale[FMX_IQ_DESIGNS];
   float iq_taps[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN];
+  float iq_pad[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN + FMX_PAD]; // [k + 5] = taps[k], zeros around
   float fd_ref;          // 1 / (2 pi kf), kf = 75 kHz / Fs
   float deemph_alpha[2]; // 50 us, 75 us at out_rate (fm_demod.cpp:119-131)
   // StereoDecoder (stereo_decoder.cpp:25-63)
   int pilot_len, delay_len; // delay_len = delaySamples + 1 (ring size)
   float pilot_taps[FMX_PILOT_MAX];
+  float pilot_pad[FMX_PILOT_MAX + FMX_PAD];
   float lr_scale;
   float lr_taps[FMX_LR_LEN];
+  float lr_pad[FMX_LR_LEN + FMX_PAD];
   float nominal, pll_min, pll_max, pll_alpha, pll_beta;
   uint32_t pll_dtheta0;
   float blend_attack[3], blend_release[3], gate[3];

@@ -57,7 +57,6 @@ struct FeArgs {
   float *clip_out;   // [C]
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
-  int st_parity;     // stereo history ping-pong index (read), writes 1 - parity
   // state
   uint8_t *dec_hist;
   int *dec_valid;
@@ -65,7 +64,8 @@ struct FeArgs {
   float2_t *iq_hist; // [C][FMX_IQ_MAXLEN-1]
   float *agc;        // [C][2]
   float *fd_prev;    // [C][2]
-  float *st_hist;    // [2][C][FMX_HIST]
+  const float *st_hist_rd; // [C][FMX_HIST] stereo MPX history before this call
+  float *st_hist_wr;       // [C][FMX_HIST] history after this call (another buffer)
   float *rds_hist;   // [C][32]
   // schedules
   const FmxSched *rds_sched; // [groups][rds_sched_stride]
@@ -77,12 +77,12 @@ struct FeArgs {
 struct PllArgs {
   const FmxDesign *des;
   const FmxChanParam *par;
-  int C, n, st_parity;
+  int C, n;
   const float *pilot;
   int pilot_stride;
   const float *mpx;
   int mpx_stride;
-  const float *st_hist; // [2][C][FMX_HIST]
+  const float *st_hist_rd; // [C][FMX_HIST] history the frontend of this call read
   float *lraw, *rraw;
   int lr_stride;
   FmxStereoState *st;
@@ -147,10 +147,11 @@ struct ResetArgs {
   float2_t *iq_hist;
   float *agc;
   float *fd_prev;
-  float *st_hist;
+  float *st_hist; // [FMX_ST_BUFS][C][FMX_HIST]
   float *lr_hist, *af_win, *af_iir, *mono_win, *mono_iir;
   float *rds_hist;
 };
+#define FMX_ST_BUFS 3 // rotating stereo-history buffers (frontend k+1 overlaps stereo k)
 enum ResetParts {
   RS_DECIM = 1,    // ComplexDecimator::reset
   RS_DEMOD = 2,    // FMDemod::reset (DC, IQ FIR, discriminator, mono chain)

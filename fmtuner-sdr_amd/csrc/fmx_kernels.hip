@@ -70,18 +70,20 @@ struct FeShared {
 };
 
 // Decimator: outputs j = 3*tid + r of the chunk.  inq is phase-major:
-// inq[ph * Q + q] holds input li = q*M + ph.
+// inq[ph * Q + q] holds input li = q*M + ph; poly[p][qq] = taps[qq*M + p].
+// One phase at a time (not unrolled) keeps the live set to ~30 half2 loads.
 template <int M, int TPP>
-__device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const float *__restrict__ taps, int tid,
+__device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const float *__restrict__ poly, int tid,
                                             float (&ai)[3], float (&aq)[3]) {
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     ai[r] = 0.0f;
     aq[r] = 0.0f;
   }
-#pragma unroll
+#pragma unroll 1
   for (int p = 0; p < M; ++p) {
     const __half2 *row = inq + (M - 1 - p) * Q + 3 * tid + (TPP - 1);
+    const float *h = poly + p * TPP;
 #pragma unroll
     for (int s = -(TPP - 1); s <= 2; ++s) {
       const __half2 hv = row[s];
@@ -91,67 +93,57 @@ __device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const flo
       for (int r = 0; r < 3; ++r) {
         const int qq = r - s;
         if (qq >= 0 && qq < TPP) {
-          const float h = taps[qq * M + p];
-          ai[r] = fmaf(h, xi, ai[r]);
-          aq[r] = fmaf(h, xq, aq[r]);
+          ai[r] = fmaf(h[qq], xi, ai[r]);
+          aq[r] = fmaf(h[qq], xq, aq[r]);
         }
       }
     }
   }
 }
 
-// Real-tap FIR on a complex LDS signal: outputs at x[base + 3*tid + r].
-template <int L>
-__device__ __forceinline__ void fir_c3(const float2 *x, int base, const float *__restrict__ h, float (&zr)[3],
-                                       float (&zi)[3]) {
+// Real-tap FIR of runtime length L on a complex LDS signal, 3 outputs per
+// thread at x[base + r]; hp = taps padded with 5 zeros on each side
+// (hp[k + 5] = h[k]), x needs 3 samples of slack past base + 2.
+__device__ __forceinline__ void fir_c3(const float2 *x, int base, const float *__restrict__ hp, int L,
+                                       float (&zr)[3], float (&zi)[3]) {
+  float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, i0 = 0.0f, i1 = 0.0f, i2 = 0.0f;
+#pragma unroll 1
+  for (int s = -(L - 1); s <= 2; s += 4) {
+    const float *h = hp + 5 - s; // h[r - u] = taps[r - (s + u)]
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    zr[r] = 0.0f;
-    zi[r] = 0.0f;
-  }
-#pragma unroll
-  for (int s = -(L - 1); s <= 2; ++s) {
-    const float2 v = x[base + s];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int k = r - s;
-      if (k >= 0 && k < L) {
-        zr[r] = fmaf(h[k], v.x, zr[r]);
-        zi[r] = fmaf(h[k], v.y, zi[r]);
-      }
+    for (int u = 0; u < 4; ++u) {
+      const float2 v = x[base + s + u];
+      r0 = fmaf(h[0 - u], v.x, r0);
+      i0 = fmaf(h[0 - u], v.y, i0);
+      r1 = fmaf(h[1 - u], v.x, r1);
+      i1 = fmaf(h[1 - u], v.y, i1);
+      r2 = fmaf(h[2 - u], v.x, r2);
+      i2 = fmaf(h[2 - u], v.y, i2);
     }
   }
+  zr[0] = r0;
+  zr[1] = r1;
+  zr[2] = r2;
+  zi[0] = i0;
+  zi[1] = i1;
+  zi[2] = i2;
 }
 
-// Real FIR of runtime length P on a real LDS signal, 3 outputs per thread.
-__device__ __forceinline__ void fir_r3(const float *x, int base, const float *__restrict__ h, int P,
+// Real FIR of runtime length P on a real LDS signal, 3 outputs per thread;
+// hp padded as above; x needs 3 samples of slack past base + 2.
+__device__ __forceinline__ void fir_r3(const float *x, int base, const float *__restrict__ hp, int P,
                                        float (&z)[3]) {
   float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-  // s = -(P-1), -(P-2): only r = 2 / r >= 1 valid
-  {
-    const float v = x[base - (P - 1)];
-    a2 = fmaf(h[P - 1], v, a2);
-  }
-  {
-    const float v = x[base - (P - 2)];
-    a1 = fmaf(h[P - 1], v, a1);
-    a2 = fmaf(h[P - 2], v, a2);
-  }
-#pragma unroll 8
-  for (int s = -(P - 3); s <= 0; ++s) {
-    const float v = x[base + s];
-    a0 = fmaf(h[-s], v, a0);
-    a1 = fmaf(h[1 - s], v, a1);
-    a2 = fmaf(h[2 - s], v, a2);
-  }
-  {
-    const float v = x[base + 1];
-    a1 = fmaf(h[0], v, a1);
-    a2 = fmaf(h[1], v, a2);
-  }
-  {
-    const float v = x[base + 2];
-    a2 = fmaf(h[0], v, a2);
+#pragma unroll 1
+  for (int s = -(P - 1); s <= 2; s += 4) {
+    const float *h = hp + 5 - s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = x[base + s + u];
+      a0 = fmaf(h[0 - u], v, a0);
+      a1 = fmaf(h[1 - u], v, a1);
+      a2 = fmaf(h[2 - u], v, a2);
+    }
   }
   z[0] = a0;
   z[1] = a1;
@@ -215,8 +207,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   __half2 *inq = reinterpret_cast<__half2 *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem);
   float2 *xin = reinterpret_cast<float2 *>(smem + R0);
-  float *mx = reinterpret_cast<float *>(smem + R0 + (FE_HALO_IQ + FE_T) * 8);
-  FeShared *sh = reinterpret_cast<FeShared *>(smem + R0 + (FE_HALO_IQ + FE_T) * 8 + (FMX_HIST + FE_T) * 4);
+  float *mx = reinterpret_cast<float *>(smem + R0 + (FE_HALO_IQ + FE_T + 8) * 8);
+  FeShared *sh = reinterpret_cast<FeShared *>(smem + R0 + (FE_HALO_IQ + FE_T + 8) * 8 + (FMX_HIST + FE_T + 8) * 4);
 
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -226,7 +218,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   const int n = a.n;
   const FmxChanParam par = a.par[c];
   const int iqL = D->iq_len[par.iqsel];
-  const float *__restrict__ iqh = D->iq_taps[par.iqsel];
+  const float *__restrict__ iqh = D->iq_pad[par.iqsel];
   const float iqscale = D->iq_scale[par.iqsel];
   const bool demod = a.do_demod != 0;
   const bool pilot = a.pilot_out != nullptr;
@@ -234,6 +226,10 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
   const float dc_c = -dc_a1;
 
+  // zero the FIR slack past the chunk (read against zero-padded taps)
+  for (int h = tid; h < FE_HALO_IQ + FE_T + 8; h += 256) xin[h] = make_float2(0.0f, 0.0f);
+  for (int h = tid; h < FMX_HIST + FE_T + 8; h += 256) mx[h] = 0.0f;
+  __syncthreads();
   // ---- load carried state ----
   if (demod) {
     for (int h = tid; h < FE_HALO_IQ; h += 256) {
@@ -248,7 +244,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     }
   }
   if (pilot || rds || demod) {
-    const float *hist = a.st_hist + ((size_t)a.st_parity * a.C + c) * FMX_HIST;
+    const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
     for (int h = tid; h < FMX_HIST; h += 256) mx[h] = pilot ? hist[h] : 0.0f;
   }
   if (tid == 0) sh->clip = 0;
@@ -299,7 +295,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         }
         __syncthreads();
         float ai[3], aq[3];
-        fe_decimate<M, TPP>(inq, Q, D->dec_taps, tid, ai, aq);
+        fe_decimate<M, TPP>(inq, Q, D->dec_poly, tid, ai, aq);
         int myclip = 0;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -410,8 +406,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       // ================= IQ FIR =================
       {
         float zr[3], zi[3];
-        if (iqL == 121) fir_c3<121>(xin, FE_HALO_IQ + 3 * tid, iqh, zr, zi);
-        else fir_c3<81>(xin, FE_HALO_IQ + 3 * tid, iqh, zr, zi);
+        fir_c3(xin, FE_HALO_IQ + 3 * tid, iqh, iqL, zr, zi);
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const int j = 3 * tid + r;
@@ -453,7 +448,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     // ================= 19 kHz pilot band-pass =================
     if (pilot) {
       float z[3];
-      fir_r3(mx, FMX_HIST + 3 * tid, D->pilot_taps, D->pilot_len, z);
+      fir_r3(mx, FMX_HIST + 3 * tid, D->pilot_pad, D->pilot_len, z);
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int j = 3 * tid + r;
@@ -545,7 +540,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     }
   }
   if (pilot) {
-    float *hist = a.st_hist + ((size_t)(1 - a.st_parity) * a.C + c) * FMX_HIST;
+    float *hist = a.st_hist_wr + (size_t)c * FMX_HIST;
     for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[h];
   }
   if (rds) {
@@ -626,7 +621,7 @@ __global__ __launch_bounds__(64) void k_pll(PllArgs a) {
         sm[row][col] = a.mpx[(size_t)ch * a.mpx_stride + t];
         const int di = n0 + col - Dly;
         sd[row][col] = (di >= 0) ? a.mpx[(size_t)ch * a.mpx_stride + di]
-                                 : a.st_hist[((size_t)a.st_parity * a.C + ch) * FMX_HIST + FMX_HIST + di];
+                                 : a.st_hist_rd[(size_t)ch * FMX_HIST + FMX_HIST + di];
       }
     }
     __syncthreads();
@@ -726,7 +721,7 @@ __global__ __launch_bounds__(64) void k_pll(PllArgs a) {
 /* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
 /* ================================================================== */
 __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
-  __shared__ float li[AU_HALO + AU_T], ri[AU_HALO + AU_T];
+  __shared__ float li[AU_HALO + AU_T + 8], ri[AU_HALO + AU_T + 8];
   __shared__ float lf[AU_RHALO + AU_T], rf[AU_RHALO + AU_T];
   __shared__ float ol[AU_MAXOUT], orr[AU_MAXOUT];
   __shared__ int s_eb, s_ee, s_count;
@@ -745,6 +740,11 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const float dc_alpha = mono ? 0.0008f : 0.005f;
   const float de_a1 = -(1.0f - dalpha);
   const float dc_a1 = -1.0f + dc_alpha;
+  for (int h = tid; h < AU_HALO + AU_T + 8; h += 256) {
+    li[h] = 0.0f;
+    ri[h] = 0.0f;
+  }
+  __syncthreads();
   // halos
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
@@ -798,8 +798,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     __syncthreads();
     if (lrfir) {
       float zl[3], zr[3];
-      fir_r3(li, AU_HALO + 3 * tid, D->lr_taps, FMX_LR_LEN, zl);
-      fir_r3(ri, AU_HALO + 3 * tid, D->lr_taps, FMX_LR_LEN, zr);
+      fir_r3(li, AU_HALO + 3 * tid, D->lr_pad, FMX_LR_LEN, zl);
+      fir_r3(ri, AU_HALO + 3 * tid, D->lr_pad, FMX_LR_LEN, zr);
       const float sc = D->lr_scale;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -953,7 +953,7 @@ struct RdsLds {
   float tin[64][65];
 };
 
-__device__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
+__device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
   fmx_rds_group g;
   uint8_t e[4];
   uint16_t d[4];
@@ -974,7 +974,7 @@ __device__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng)
   ng++;
 }
 
-__device__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
+__device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
   s.bs_reg = (s.bs_reg << 1u) + (uint32_t)bit;
   s.bs_until_next--;
   s.bs_bitcount++;
@@ -994,11 +994,13 @@ __device__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const Rds
       s.bs_pulse_off[3] = off;
       s.bs_pulse_pos[3] = s.bs_bitcount;
       bool found = false;
-      for (int i = 0; i < 2 && !found; ++i)
-        for (int j = i + 1; j < 3 && !found; ++j)
-          if (pulse_follows(s.bs_pulse_pos[3], s.bs_pulse_off[3], s.bs_pulse_pos[j], s.bs_pulse_off[j]) &&
-              pulse_follows(s.bs_pulse_pos[j], s.bs_pulse_off[j], s.bs_pulse_pos[i], s.bs_pulse_off[i]))
-            found = true;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j)
+          found = found ||
+                  (pulse_follows(s.bs_pulse_pos[3], s.bs_pulse_off[3], s.bs_pulse_pos[j], s.bs_pulse_off[j]) &&
+                   pulse_follows(s.bs_pulse_pos[j], s.bs_pulse_off[j], s.bs_pulse_pos[i], s.bs_pulse_off[i]));
       if (found) {
         s.bs_in_sync = 1;
         s.bs_expected = off;
@@ -1033,18 +1035,24 @@ __device__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const Rds
     if (!done) {
       uint16_t data = (uint16_t)(raw >> 10);
       if (had) {
+        const uint32_t *es = L.esyn[s.bs_expected];
+        const uint32_t *ee = L.eerr[s.bs_expected];
         for (int i = 0; i < 52; ++i)
-          if (L.esyn[s.bs_expected][i] == syn) {
-            data = (uint16_t)((raw ^ L.eerr[s.bs_expected][i]) >> 10);
+          if (es[i] == syn) {
+            data = (uint16_t)((raw ^ ee[i]) >> 10);
             off = s.bs_expected;
             break;
           }
       }
       if (off == s.bs_expected) {
         const int bn = bs_block_number(s.bs_expected);
-        s.bs_blk_raw[bn] = raw;
-        s.bs_blk_data[bn] = data;
-        s.bs_blk_flags[bn] = (uint8_t)(1 | (had ? 2 : 0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i == bn) {
+            s.bs_blk_raw[i] = raw;
+            s.bs_blk_data[i] = data;
+            s.bs_blk_flags[i] = (uint8_t)(1 | (had ? 2 : 0));
+          }
       }
       const int next = bs_next(s.bs_expected);
       if (next == OA) {
@@ -1321,10 +1329,8 @@ __global__ void k_reset(ResetArgs a) {
     }
   }
   if (create || (m & RS_STEREO)) {
-    for (int h = tid; h < FMX_HIST; h += blockDim.x) {
-      a.st_hist[(size_t)c * FMX_HIST + h] = 0.0f;
-      a.st_hist[((size_t)a.C + c) * FMX_HIST + h] = 0.0f;
-    }
+    for (int h = tid; h < FMX_HIST; h += blockDim.x)
+      for (int k = 0; k < FMX_ST_BUFS; ++k) a.st_hist[((size_t)k * a.C + c) * FMX_HIST + h] = 0.0f;
     for (int h = tid; h < 2 * (FMX_LR_LEN - 1); h += blockDim.x)
       a.lr_hist[(size_t)c * 2 * (FMX_LR_LEN - 1) + h] = 0.0f;
     if (tid == 0) {
@@ -1422,7 +1428,7 @@ template <int M, int TPP> static size_t fe_smem() {
   constexpr int IN_BYTES = (M > 1) ? M * Q * 4 : 0;
   constexpr int YB_BYTES = (FE_T + 1) * 8;
   constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
-  return (size_t)R0 + (FE_HALO_IQ + FE_T) * 8 + (FMX_HIST + FE_T) * 4 + sizeof(FeShared);
+  return (size_t)R0 + (FE_HALO_IQ + FE_T + 8) * 8 + (FMX_HIST + FE_T + 8) * 4 + sizeof(FeShared);
 }
 
 template <int M, int TPP> static int fe_launch(const FeArgs &a, hipStream_t st) {

@@ -42,6 +42,7 @@ typedef struct {
   int f_l, f_r; /* L/R tone frequencies, Hz (mono: f1, f2) */
   float a_l, a_r;
   float ph_l, ph_r; /* initial tone phases, rad */
+  int64_t rds_off;  /* RDS bit-clock offset in samples (stations are not synchronised) */
 } fmx_synth_chan;
 
 #ifdef __cplusplus
@@ -80,6 +81,7 @@ FMX_HD fmx_synth_chan fmx_synth_channel(const fmx_synth_cfg *cfg, uint32_t ch) {
     c.ph_l = 6.2831853f * fmx_u01(h2 >> 7);
     c.ph_r = 6.2831853f * fmx_u01(h3 >> 29);
   }
+  c.rds_off = (int64_t)(fmx_splitmix64(s ^ 4) % (uint64_t)(2 * cfg->iq_rate));
   return c;
 }
 
@@ -127,12 +129,14 @@ FMX_HD float fmx_synth_fm_phase(const fmx_synth_cfg *cfg, const fmx_synth_chan *
   /* pilot 0.09 sin(th_p) */
   ph += fmx_int_sin(0.09f, 19000, n, fs, 0.0f);
   if (cfg->kind == FMX_SYNTH_STEREO_RDS && bits && cfg->n_bits > 0) {
-    /* half-bit index and symbol sign */
-    int64_t h = (n * 2375) / fs;
+    /* half-bit index and symbol sign; the RDS waveform is shifted by the
+     * channel's bit-clock offset (a constant phase term is dropped) */
+    const int64_t nr = n + c->rds_off;
+    int64_t h = (nr * 2375) / fs;
     int64_t k = h >> 1;
     int bit = bits[k % cfg->n_bits];
     float s = (bit ? 1.0f : -1.0f) * ((h & 1) ? -1.0f : 1.0f);
-    float a57 = fmx_angle(57000, n, fs);
+    float a57 = fmx_angle(57000, nr, fs);
     ph += s * (75000.0f * cfg->rds_level / 57000.0f) * (1.0f - cosf(a57));
   }
   return ph;

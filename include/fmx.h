@@ -138,6 +138,14 @@ int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out,
  * [C][in_stride]; d_mono may be NULL (stereo mode: returns 0 samples). */
 int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride,
               float *d_mono, int mono_stride, int *d_mono_count);
+/* FMDemod::processSplit(iq, mpx, mono, n) on u8 IQ at dsp_rate (iq_rate ==
+ * dsp_rate; byte LUT (v-127)/127.5, clip = byte 0/255, fm_demod.cpp:219-249) */
+int fmx_demod_u8(void *handle, const uint8_t *d_iq, size_t iq_stride, int n, float *d_mpx, int mpx_stride,
+                 float *d_mono, int mono_stride, int *d_mono_count, float *d_clip_ratio);
+/* FMDemod::downsampleAudio(demod, audio, n): mono resampler + de-emphasis +
+ * DC block on MPX (fm_demod.cpp:279-295) */
+int fmx_downsample(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_out, int out_stride,
+                   int *d_count);
 /* StereoDecoder::processAudio */
 int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d_left, float *d_right,
                int lr_stride, int *d_stereo, int *d_pilot_tenths);
