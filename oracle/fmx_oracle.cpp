@@ -1553,6 +1553,36 @@ int oracle_pipeline_block(void *p, const uint8_t *iq, int iq_samples, float *mpx
   return static_cast<ref::Pipeline *>(p)->block(iq, iq_samples, mpx_out, pcm_l, pcm_r, pcm_cap, groups,
                                                 groups_cap, info);
 }
+/* main.cpp's runtime setter paths (XDR callbacks applied between blocks):
+ * keys as include/fmx.h FMX_PARAM_*: 1 bandwidth Hz (main.cpp:1052-1062),
+ * 2 W0, 3 deemphasis 0/1/2 (main.cpp:1123-1136), 4 dsp_agc, 5 blend,
+ * 6 force mono, 7 force stereo, 8 bandwidth mode. */
+void oracle_pipeline_set(void *pp, int key, int v) {
+  auto *p = static_cast<ref::Pipeline *>(pp);
+  switch (key) {
+    case 1: p->demod.setBandwidthHz(v); break;
+    case 2: p->demod.setW0(v); break;
+    case 3:
+      if (v == 0) {
+        p->af.setDeemphasis(50);
+        p->demod.setDeemphasis(50);
+      } else if (v == 1) {
+        p->af.setDeemphasis(75);
+        p->demod.setDeemphasis(75);
+      } else {
+        p->af.setDeemphasis(0);
+        p->demod.setDeemphasis(0);
+      }
+      break;
+    case 4: p->demod.setDspAgcMode(v); break;
+    case 5: p->stereo.blendMode = v; break;
+    case 6: p->stereo.forceMono = v != 0; break;
+    case 7: p->stereo.forceStereo = v != 0; break;
+    case 8: p->demod.setBandwidthMode(v); break;
+    default: break;
+  }
+}
+
 int oracle_pipeline_taps(void *pp, int which, float *out, int cap) {
   auto *p = static_cast<ref::Pipeline *>(pp);
   std::vector<float> v;

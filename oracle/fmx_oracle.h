@@ -68,6 +68,8 @@ int oracle_pipeline_block(void *p, const uint8_t *iq, int iq_samples,
                           float *mpx_out, float *pcm_l, float *pcm_r,
                           int pcm_cap, oracle_group *groups, int groups_cap,
                           oracle_blockinfo *info);
+/* runtime setters as main.cpp applies them (keys = FMX_PARAM_* of fmx.h) */
+void oracle_pipeline_set(void *p, int key, int value);
 /* debug taps: which = 0 decim, 1 iqfir, 2 pilot, 3 lr, 4 af_resamp proto,
  * 5 rds_resamp proto, 6 rds_fir, 7 symsync mf, 8 symsync dmf */
 int oracle_pipeline_taps(void *p, int which, float *out, int cap);

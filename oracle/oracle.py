@@ -49,6 +49,7 @@ def lib():
             "oracle_pipeline_reset": (None, [vp]),
             "oracle_pipeline_block": (i, [vp, vp, i, vp, vp, vp, i, vp, i, C.POINTER(BlockInfo)]),
             "oracle_pipeline_taps": (i, [vp, i, vp, i]),
+            "oracle_pipeline_set": (None, [vp, i, i]),
             "oracle_decim_create": (vp, [C.c_uint32, C.c_uint32, C.c_float]),
             "oracle_decim_destroy": (None, [vp]),
             "oracle_decim_reset": (None, [vp]),
@@ -144,8 +145,15 @@ class Pipeline:
     def reset(self):
         self.L.oracle_pipeline_reset(self.p)
 
+    PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
+                 force_mono=6, force_stereo=7, bandwidth_mode=8)
+
+    def set_param(self, key, value):
+        k = self.PARAM[key] if isinstance(key, str) else key
+        self.L.oracle_pipeline_set(self.p, k, value)
+
     def block(self, iq):
-        """iq: uint8 array of 2*block*M bytes -> dict of outputs."""
+        """iq: uint8 array of 2*n*M bytes (n <= block) -> dict of outputs."""
         iq = np.ascontiguousarray(iq, dtype=np.uint8)
         B = self.cfg.block
         mpx = np.zeros(B, np.float32)

@@ -64,6 +64,9 @@ def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=
     for b in range(nblk):
         if resets and b in resets:
             p.reset()
+        if params and b in params:
+            for (k, v) in params[b]:
+                p.set_param(k, v)
         res.append(p.block(iq_row[b * 2 * n * M:(b + 1) * 2 * n * M]))
     return res
 

@@ -1,0 +1,285 @@
+"""GPU parity: the HIP path (libfmx.so through its C ABI) against the oracle
+on identical seeded IQ.  Bars (BASELINE.json north_star): RDS groups
+bit-exact, PCM within 1e-4 RMS; stereo flag, pilot level and sample counts
+exact; MPX within 1e-4 (max abs).  Every test here runs on the GPU."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import gpu_harness as H
+
+pytestmark = pytest.mark.gpu
+
+PCM_RMS_TOL = 1e-4   # north_star: audio PCM within 1e-4 RMS
+PCM_MAX_TOL = 2e-3
+MPX_MAX_TOL = 1e-4
+
+
+def make_iq(fmx, kind, C, nblk, iq_rate=2_400_000, M=10, B=4096, noise=0.0, ch0=0, n=None):
+    n = n or B
+    scfg = fmx.make_synth(iq_rate=iq_rate, kind=kind, noise_std=noise, n_bits=8192)
+    bits, groups = fmx.synth_rds_bits(scfg, ch0, C)
+    iq = fmx.synth_host(scfg, ch0, C, 0, n * M * nblk, bits)
+    return iq, groups
+
+
+def check(g, o, c, nblk, tag=""):
+    st = H.compare(g, o, c, nblk)
+    assert st["count_mismatch"] == 0, (tag, c, st)
+    assert st["stereo_mismatch"] == 0 and st["pilot_mismatch"] == 0, (tag, c, st)
+    assert st["mpx_max"] < MPX_MAX_TOL, (tag, c, st)
+    assert st["pcm_rms"] < PCM_RMS_TOL, (tag, c, st)
+    assert st["pcm_max"] < PCM_MAX_TOL, (tag, c, st)
+    assert st["groups_gpu"] == st["groups_oracle"], (tag, c, st["groups_gpu"], st["groups_oracle"])
+    return st
+
+
+def run_both(fmx, oracle, torch, cfgkw, iq, nblk, n=None, resets=None, params=None, per_channel_resets=None):
+    C = iq.shape[0]
+    g = H.run_gpu_pipeline(fmx, torch, fmx.make_config(**cfgkw), iq, nblk, n=n, resets=resets, params=params)
+    outs = []
+    for c in range(C):
+        rs = None
+        if resets:
+            rs = {b: ch for b, ch in resets.items() if ch in (-1, c)}
+        op = None
+        if params:
+            op = {b: [(k, v) for (k, v, ch) in lst if ch in (-1, c)] for b, lst in params.items()}
+        outs.append(H.run_oracle_pipeline(oracle, oracle.make_cfg(**cfgkw), iq[c], nblk, n=n, resets=rs, params=op))
+    return g, outs
+
+
+def test_stereo_rds_parity_2m4(fmx, oracle, torch_cuda):
+    """Cfg2/3 channel: 2.4 MS/s stereo FM + RDS, M=10 -> 240 kHz, 50 us."""
+    C, nblk = 8, 40
+    iq, _ = make_iq(fmx, 2, C, nblk)
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk)
+    ngroups = 0
+    for c in range(C):
+        st = check(g, outs[c], c, nblk, "2m4")
+        ngroups += len(st["groups_oracle"])
+    assert ngroups >= 3 * C
+
+
+def test_reference_native_rate_2m048(fmx, oracle, torch_cuda):
+    """The reference's own configuration: 2.048 MS/s, M=8 -> 256 kHz."""
+    C, nblk = 4, 30
+    kw = dict(iq_rate=2_048_000, dsp_rate=256_000)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=2_048_000, M=8)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "2m048")
+
+
+def test_decimation_factor_4(fmx, oracle, torch_cuda):
+    C, nblk = 2, 12
+    kw = dict(iq_rate=1_024_000, dsp_rate=256_000)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=1_024_000, M=4)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "m4")
+
+
+def test_direct_u8_no_decimation(fmx, oracle, torch_cuda):
+    """iq_rate == dsp_rate: FMDemod::processSplit on bytes (fm_demod.cpp:219-249)."""
+    C, nblk = 2, 10
+    kw = dict(iq_rate=256_000, dsp_rate=256_000)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=256_000, M=1)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "m1")
+
+
+def test_mono_config1(fmx, oracle, torch_cuda):
+    """Config 1: mono FM (1 kHz + 3 kHz, no pilot), stereo=false path."""
+    C, nblk = 2, 16
+    kw = dict(stereo=0, rds=0)
+    iq, _ = make_iq(fmx, 0, C, nblk)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "mono")
+        assert np.array_equal(g[-1]["pcm_l"][c], g[-1]["pcm_r"][c])
+
+
+def test_weak_signal_agc_fast_soft_blend(fmx, oracle, torch_cuda):
+    """Config 5 subset: AWGN, dsp_agc=fast, stereo_blend=soft."""
+    C, nblk = 4, 24
+    kw = dict(dsp_agc=1, blend=0)
+    iq, _ = make_iq(fmx, 2, C, nblk, noise=0.25)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "weak")
+
+
+@pytest.mark.parametrize("w0", [309_000, 114_000, 42_000, 9_000])
+def test_w0_bandwidth_sweep(fmx, oracle, torch_cuda, w0):
+    C, nblk = 2, 10
+    kw = dict(w0_bandwidth_hz=w0)
+    iq, _ = make_iq(fmx, 2, C, nblk, ch0=20)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, f"w0={w0}")
+
+
+def test_resets_and_runtime_setters(fmx, oracle, torch_cuda):
+    """Runtime::reset of one channel / all channels, XDR bandwidth change
+    (re-created IQ FIR), de-emphasis change, force mono, AGC switch."""
+    C, nblk = 3, 30
+    iq, _ = make_iq(fmx, 2, C, nblk, ch0=40)
+    resets = {8: 1, 16: -1}
+    params = {10: [("bandwidth_hz", 63_000, -1)], 12: [("deemphasis", 1, -1)],
+              14: [("force_mono", 1, 2)], 18: [("force_mono", 0, 2), ("bandwidth_hz", 0, -1)],
+              20: [("dsp_agc", 2, 0), ("blend", 2, -1)], 24: [("deemphasis", 2, 1)]}
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, resets=resets, params=params)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "setters")
+
+
+@pytest.mark.parametrize("n", [1500, 333])
+def test_ragged_call_sizes(fmx, oracle, torch_cuda, n):
+    """Calls of n < dsp_block samples that do not divide the kernel chunks."""
+    C, nblk = 3, 60 if n == 1500 else 40
+    iq, _ = make_iq(fmx, 2, C, nblk, n=n, ch0=60)
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, n=n)
+    for c in range(C):
+        check(g, outs[c], c, nblk, f"n={n}")
+
+
+def test_stage_entry_points(fmx, oracle, torch_cuda):
+    """fmx_decimate / fmx_demod / fmx_stereo / fmx_afpost / fmx_rds against the
+    individual oracle objects (ComplexDecimator, FMDemod, StereoDecoder,
+    AFPostProcessor, RDSDecoder)."""
+    import ctypes as Ct
+    torch = torch_cuda
+    L = oracle.lib()
+    C, B, M, nblk = 2, 4096, 10, 14
+    iq, _ = make_iq(fmx, 2, C, nblk, ch0=80)
+    cfg = fmx.make_config(bandwidth_hz=-1, deemphasis=1)  # objects as constructed (75 us, ctor IQ filter)
+    h = fmx.Handle(cfg, C)
+    dev = torch.device("cuda")
+    d_iq = torch.from_numpy(iq).to(dev)
+    bb = torch.zeros((C, 2 * B), dtype=torch.float32, device=dev)
+    mpx = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    mono = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    lf = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    rf = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    st = torch.zeros(C, dtype=torch.int32, device=dev)
+    pil = torch.zeros(C, dtype=torch.int32, device=dev)
+    ol = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    orr = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    acnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    grp = torch.zeros((C, 8, 4), dtype=torch.int32, device=dev)
+    gcnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    od = [L.oracle_decim_create(M, 28, 80.0) for _ in range(C)]
+    odm = [L.oracle_demod_create(240_000, 32_000) for _ in range(C)]
+    ost = [L.oracle_stereo_create(240_000, 32_000) for _ in range(C)]
+    oaf = [L.oracle_afpost_create(240_000, 32_000) for _ in range(C)]
+    ords = [L.oracle_rds_create(240_000) for _ in range(C)]
+    groups_g = [[] for _ in range(C)]
+    groups_o = [[] for _ in range(C)]
+    for b in range(nblk):
+        h.decimate(d_iq.data_ptr() + b * 2 * B * M, iq.shape[1], B, bb.data_ptr(), 2 * B)
+        h.demod(bb.data_ptr(), 2 * B, B, mpx.data_ptr(), B, mono.data_ptr(), B, cnt.data_ptr())
+        h.stereo(mpx.data_ptr(), B, B, lf.data_ptr(), rf.data_ptr(), B, st.data_ptr(), pil.data_ptr())
+        h.afpost(lf.data_ptr(), rf.data_ptr(), B, B, ol.data_ptr(), orr.data_ptr(), B, B, acnt.data_ptr())
+        h.rds(mpx.data_ptr(), B, B, grp.data_ptr(), 8, gcnt.data_ptr())
+        h.sync()
+        G = {k: v.cpu().numpy() for k, v in dict(bb=bb, mpx=mpx, mono=mono, cnt=cnt, lf=lf, rf=rf, st=st, pil=pil,
+                                                  ol=ol, orr=orr, acnt=acnt, gcnt=gcnt).items()}
+        graw = grp.cpu().numpy().view(np.uint8).reshape(C, 8, 16)
+        for c in range(C):
+            x = np.ascontiguousarray(iq[c, b * 2 * B * M:(b + 1) * 2 * B * M])
+            obb = np.zeros(2 * B, np.float32)
+            L.oracle_decim_execute_complex(od[c], x.ctypes.data, B * M, obb.ctypes.data, B)
+            assert np.max(np.abs(obb - G["bb"][c])) < 1e-5
+            om = np.zeros(B, np.float32)
+            omono = np.zeros(B, np.float32)
+            k = L.oracle_demod_process_split_complex(odm[c], G["bb"][c].ctypes.data, om.ctypes.data,
+                                                     omono.ctypes.data, B)
+            assert k == G["cnt"][c]
+            assert np.max(np.abs(om - G["mpx"][c])) < MPX_MAX_TOL
+            assert np.sqrt(np.mean((omono[:k] - G["mono"][c][:k]) ** 2)) < PCM_RMS_TOL
+            ol_, or_ = np.zeros(B, np.float32), np.zeros(B, np.float32)
+            s_, p_ = Ct.c_int(), Ct.c_int()
+            mpx_c = np.ascontiguousarray(G["mpx"][c])
+            L.oracle_stereo_process(ost[c], mpx_c.ctypes.data, ol_.ctypes.data, or_.ctypes.data, B,
+                                    Ct.byref(s_), Ct.byref(p_))
+            assert s_.value == G["st"][c] and p_.value == G["pil"][c]
+            assert np.sqrt(np.mean((ol_ - G["lf"][c]) ** 2)) < PCM_RMS_TOL
+            assert np.sqrt(np.mean((or_ - G["rf"][c]) ** 2)) < PCM_RMS_TOL
+            al, ar = np.zeros(B, np.float32), np.zeros(B, np.float32)
+            lfc, rfc = np.ascontiguousarray(G["lf"][c]), np.ascontiguousarray(G["rf"][c])
+            k = L.oracle_afpost_process(oaf[c], lfc.ctypes.data, rfc.ctypes.data, B, al.ctypes.data,
+                                        ar.ctypes.data, B)
+            assert k == G["acnt"][c]
+            assert np.max(np.abs(al[:k] - G["ol"][c][:k])) < 1e-5
+            gg = (oracle.OracleGroup * 16)()
+            ng = L.oracle_rds_process(ords[c], mpx_c.ctypes.data, B, gg, 16, None, 0, None)
+            groups_o[c] += oracle.groups_to_tuples(gg, ng)
+            for q in range(int(G["gcnt"][c])):
+                w = graw[c, q]
+                a, bb_, cc, d = np.frombuffer(w[:8].tobytes(), dtype=np.uint16)
+                groups_g[c].append((int(a), int(bb_), int(cc), int(d), int(w[8])))
+    for c in range(C):
+        assert groups_g[c] == groups_o[c]
+    assert sum(len(x) for x in groups_o) >= 2
+    h.close()
+
+
+def test_full_size_properties(fmx, torch_cuda):
+    """Bench size (4096 channels): no NaN, exact sample counts, stereo on
+    every channel after acquisition, and every error-free RDS group equals
+    the transmitted group sequence (ground truth, size-independent)."""
+    torch = torch_cuda
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_oracle_pinning import groups_align
+    C, B, M, nblk = 4096, 4096, 10, 40
+    cfg = fmx.make_config()
+    h = fmx.Handle(cfg, C)
+    dev = torch.device("cuda")
+    n_iq = B * M
+    scfg = fmx.make_synth(kind=2, n_bits=int((nblk * n_iq + 4_800_000) * 1187.5 / 2.4e6) + 208)
+    bits, tx = fmx.synth_rds_bits(scfg, 0, C)
+    d_bits = torch.from_numpy(bits).to(dev)
+    row = 2 * n_iq * nblk
+    d_iq = torch.empty((C, row), dtype=torch.uint8, device=dev)
+    h.synth_device(scfg, 0, C, 0, n_iq * nblk, d_bits.data_ptr(), d_iq.data_ptr(), row)
+    pl = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    pr = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    st = torch.zeros(C, dtype=torch.int32, device=dev)
+    grp = torch.zeros((C, 8, 4), dtype=torch.int32, device=dev)
+    gcnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    out = fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(), st.data_ptr(), None, None,
+                       grp.data_ptr(), 8, gcnt.data_ptr())
+    got = [[] for _ in range(C)]
+    total = 0
+    for b in range(nblk):
+        h.process_block(d_iq.data_ptr() + b * 2 * n_iq, row, B, out)
+        h.sync()
+        c_ = cnt.cpu().numpy()
+        assert set(np.unique(c_)) <= {546, 547}
+        assert torch.isfinite(pl).all() and torch.isfinite(pr).all()
+        gc = gcnt.cpu().numpy()
+        graw = grp.cpu().numpy().view(np.uint8).reshape(C, 8, 16)
+        for c in np.nonzero(gc)[0]:
+            for q in range(int(gc[c])):
+                w = graw[c, q]
+                a, bb_, cc, d = np.frombuffer(w[:8].tobytes(), dtype=np.uint16)
+                got[c].append((int(a), int(bb_), int(cc), int(d), int(w[8])))
+                total += 1
+    assert st.float().mean().item() > 0.99
+    assert total > 3 * C
+    bad = [c for c in range(C) if got[c] and not groups_align(got[c], tx[c])]
+    assert not bad, bad[:10]
+    assert sum(1 for c in range(C) if any(g[4] == 0 for g in got[c])) > 0.99 * C
+    h.close()
+
+
+def test_graft_smoke(torch_cuda):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
+    __graft_entry__.smoke()

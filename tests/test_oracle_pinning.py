@@ -1,0 +1,203 @@
+"""Pins the oracle (oracle/fmx_oracle.cpp) before it is trusted as the GPU
+checker:
+  * RDS block sync vs the REFERENCE's own BlockStream (golden fixtures made
+    by tools/gen_golden.py from oracle/_ref, and live when _ref is built);
+  * filter design of the product == filter design of the oracle, bit for bit;
+  * resampler timing vs an independent float32 restatement of liquid's
+    resamp_rrrf timing loop;
+  * known answers: discriminator gain (fm_demod.cpp:64-71), transmitted RDS
+    groups recovered from synthetic IQ, stereo pilot acquisition, mono tones;
+  * a regression pin of the oracle pipeline on seeded IQ.
+MPX / PCM parity against a real liquid-dsp build is unpinned."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def bits_of(s):
+    return np.frombuffer(s.encode(), dtype=np.uint8) - ord("0")
+
+
+@pytest.mark.parametrize("stream", [s["name"] for s in load("blocksync.json")["streams"]])
+def test_blocksync_matches_reference_fixture(oracle, stream):
+    fx = {s["name"]: s for s in load("blocksync.json")["streams"]}[stream]
+    got = [list(g) for g in oracle.blocksync(bits_of(fx["bits"]))]
+    assert got == fx["groups"]
+
+
+def test_blocksync_matches_reference_live(oracle):
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(7)
+    fx = load("blocksync.json")["streams"][0]
+    clean = bits_of(fx["bits"])
+    for trial in range(20):
+        b = clean.copy()
+        b ^= (rng.random(b.size) < rng.choice([0.0, 1e-3, 5e-3, 2e-2, 8e-2])).astype(np.uint8)
+        if trial % 3 == 0:
+            b = np.delete(b, rng.integers(100, b.size - 100))
+        assert oracle.blocksync(b) == oracle.ref_blocksync(b)
+
+
+CONFIGS = [dict(iq_rate=2_400_000, dsp_rate=240_000), dict(iq_rate=2_048_000, dsp_rate=256_000),
+           dict(iq_rate=1_024_000, dsp_rate=256_000), dict(iq_rate=256_000, dsp_rate=256_000)]
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
+@pytest.mark.parametrize("w0", [309_000, 194_000, 114_000, 42_000, 9_000])
+def test_product_design_equals_oracle_design(fmx, oracle, rates, w0):
+    cfg = fmx.make_config(w0_bandwidth_hz=w0, **rates)
+    p = oracle.Pipeline(oracle.make_cfg(w0_bandwidth_hz=w0, **rates))
+    for which in range(9):
+        if which == 0 and rates["iq_rate"] == rates["dsp_rate"]:
+            continue
+        a, b = fmx.design_taps(cfg, which), p.taps(which)
+        assert a.shape == b.shape, which
+        assert np.array_equal(a, b), which
+
+
+def test_bandwidth_table_quirks(fmx):
+    # 309 kHz maps to index 0 == m_bandwidthMode's initial value: the ctor
+    # filter (81 taps @ 110 kHz) stays (fm_demod.cpp:114-117 via :183-185)
+    ctor = fmx.design_taps(fmx.make_config(w0_bandwidth_hz=309_000), 1)
+    assert ctor.size == 81
+    assert fmx.design_taps(fmx.make_config(w0_bandwidth_hz=114_000), 1).size == 81
+    assert fmx.design_taps(fmx.make_config(w0_bandwidth_hz=73_000), 1).size == 121
+    assert fmx.design_taps(fmx.make_config(w0_bandwidth_hz=42_000), 1).size == 121
+
+
+def py_schedule(del_, n, npfb=32):
+    """Independent float32 restatement of liquid resamp_rrrf timing."""
+    f = np.float32
+    tau, bf, mu, b, state, out = f(0), f(0), f(0), 0, 0, []
+    d = f(del_)
+
+    def upd(tau):
+        tau = f(tau + d)
+        bf = f(tau * f(npfb))
+        b = int(np.floor(bf))
+        return tau, bf, b, f(bf - f(b))
+
+    for i in range(n):
+        while b < npfb:
+            if state == 1:
+                out.append((i, npfb - 1, 1, mu))
+                tau, bf, b, mu = upd(tau)
+                state = 0
+            elif b == npfb - 1:
+                state, b = 1, npfb
+            else:
+                out.append((i, b, 0, mu))
+                tau, bf, b, mu = upd(tau)
+        tau, bf, b = f(tau - f(1)), f(bf - f(npfb)), b - npfb
+    return out
+
+
+@pytest.mark.parametrize("ratio", [32000 / 240000, 32000 / 256000, 171000 / 240000, 171000 / 256000])
+def test_resampler_schedule_matches_independent_restatement(fmx, ratio):
+    del_ = np.float32(1.0) / np.float32(ratio)
+    packed, mu = fmx.resamp_schedule(float(del_), 3000)
+    ref = py_schedule(del_, 3000)
+    assert len(packed) == len(ref)
+    for k, (i, b, bd, m) in enumerate(ref):
+        assert packed[k] & 0xFFFF == i and (packed[k] >> 16) & 0xFF == b and (packed[k] >> 24) & 1 == bd
+        assert mu[k] == m
+
+
+def test_discriminator_gain_known_answer(oracle):
+    """+-75 kHz deviation -> +-1.0 (fm_demod.cpp:64-71): a tone at f Hz off
+    the carrier demodulates to f / 75000."""
+    import ctypes as C
+    L = oracle.lib()
+    fs = 240_000
+    for f in (37_500.0, -18_750.0, 60_000.0):
+        d = L.oracle_demod_create(fs, 32_000)
+        L.oracle_demod_set(d, 3, 0)  # setBandwidthHz(0) -> W0 194 kHz filter
+        n = 30_000
+        t = np.arange(n)
+        x = (0.5 * np.exp(2j * np.pi * f * t / fs)).astype(np.complex64)
+        mpx = np.zeros(n, np.float32)
+        L.oracle_demod_process_split_complex(d, x.ctypes.data, mpx.ctypes.data, None, n)
+        L.oracle_demod_destroy(d)
+        assert abs(float(np.mean(mpx[20_000:])) - f / 75_000) < 2e-4, f
+
+
+def synth_channel(fmx, kind, ch, nblk, B=4096, M=10, noise=0.0):
+    scfg = fmx.make_synth(kind=kind, n_bits=8192, noise_std=noise)
+    bits, groups = fmx.synth_rds_bits(scfg, ch, 1)
+    iq = fmx.synth_host(scfg, ch, 1, 0, B * M * nblk, bits)
+    return iq[0], groups[0], scfg
+
+
+def test_oracle_recovers_transmitted_groups_and_stereo(fmx, oracle):
+    nblk, B, M = 60, 4096, 10
+    iq, tx, _ = synth_channel(fmx, 2, 11, nblk)
+    p = oracle.Pipeline(oracle.make_cfg())
+    got, stereo = [], []
+    for b in range(nblk):
+        o = p.block(iq[b * 2 * B * M:(b + 1) * 2 * B * M])
+        got += o["groups"]
+        stereo.append(o["stereo"])
+    assert stereo[7] == 1 and all(stereo[7:])  # 6 consecutive present blocks (stereo_decoder.cpp:320-327)
+    assert sum(1 for g in got if g[4] == 0) >= 8
+    assert groups_align(got, tx)
+
+
+def groups_align(got, tx):
+    """True if some offset k0 maps every error-free decoded group i onto the
+    transmitted group k0 + i (groups arrive once per 104 bits)."""
+    txl = [tuple(int(v) for v in g) for g in tx]
+    clean = [(i, tuple(int(v) for v in g[:4])) for i, g in enumerate(got) if g[4] == 0]
+    if not clean:
+        return False
+    for k0 in range(len(txl)):
+        if all(0 <= k0 + i < len(txl) and txl[k0 + i] == g for i, g in clean):
+            return True
+    return False
+
+
+def test_oracle_mono_config1_tones(fmx, oracle):
+    """Config 1: mono FM, 1 kHz + 3 kHz, stereo=false path (main.cpp:1267-1279)."""
+    nblk, B, M = 16, 4096, 10
+    iq, _, _ = synth_channel(fmx, 0, 0, nblk)
+    p = oracle.Pipeline(oracle.make_cfg(stereo=0, rds=0))
+    pcm = []
+    for b in range(nblk):
+        o = p.block(iq[b * 2 * B * M:(b + 1) * 2 * B * M])
+        assert np.array_equal(o["pcm_l"], o["pcm_r"])
+        assert len(o["pcm_l"]) in (546, 547)
+        pcm.append(o["pcm_l"])
+    x = np.concatenate(pcm)[4000:]
+    spec = np.abs(np.fft.rfft(x * np.hanning(x.size)))
+    freqs = np.fft.rfftfreq(x.size, 1 / 32000)
+    top = freqs[np.argsort(spec)[-2:]]
+    assert sorted(np.round(top / 100) * 100) == [1000.0, 3000.0]
+
+
+def test_oracle_regression_fixture(fmx, oracle):
+    reg = load("oracle_regress.json")
+    for tag, kind, stereo in (("stereo_rds", 2, 1), ("mono", 0, 0)):
+        B, M, nblk = 4096, 10, 12
+        scfg = fmx.make_synth(kind=kind, n_bits=6000)
+        bits, _ = fmx.synth_rds_bits(scfg, 3, 1)
+        iq = fmx.synth_host(scfg, 3, 1, 0, B * M * nblk, bits)
+        assert hashlib.sha256(iq.tobytes()).hexdigest() == reg[tag]["iq_sha256"]
+        p = oracle.Pipeline(oracle.make_cfg(stereo=stereo, rds=1))
+        for b, want in enumerate(reg[tag]["blocks"]):
+            o = p.block(iq[0, b * 2 * B * M:(b + 1) * 2 * B * M])
+            assert o["stereo"] == want["stereo"] and o["pilot"] == want["pilot"]
+            assert len(o["pcm_l"]) == want["n_pcm"]
+            assert [list(g) for g in o["groups"]] == want["groups"]
+            np.testing.assert_allclose(o["pcm_l"][:4], want["pcm_l_head"], rtol=0, atol=1e-6)
+            np.testing.assert_allclose(o["mpx"][:4], want["mpx_head"], rtol=0, atol=1e-6)
