@@ -79,6 +79,7 @@ def compare(gres, ores, c, nblk):
     pcm_max = 0.0
     st_mismatch = 0
     pil_mismatch = 0
+    pil_maxdiff = 0
     cnt_mismatch = 0
     g_gpu, g_ora = [], []
     for b in range(nblk):
@@ -95,8 +96,9 @@ def compare(gres, ores, c, nblk):
         pcm_max = max(pcm_max, float(np.max(np.abs(dl))) if k else 0.0, float(np.max(np.abs(dr))) if k else 0.0)
         st_mismatch += int(o["stereo"] != int(g["stereo"][c]))
         pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
+        pil_maxdiff = max(pil_maxdiff, abs(int(o["pilot"]) - int(g["pilot"][c])))
         g_gpu += g["groups"][c]
         g_ora += o["groups"]
     return dict(mpx_max=mpx_err, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
-                stereo_mismatch=st_mismatch, pilot_mismatch=pil_mismatch, count_mismatch=cnt_mismatch,
+                stereo_mismatch=st_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
                 groups_gpu=g_gpu, groups_oracle=g_ora)

@@ -1,7 +1,17 @@
 """GPU parity: the HIP path (libfmx.so through its C ABI) against the oracle
 on identical seeded IQ.  Bars (BASELINE.json north_star): RDS groups
 bit-exact, PCM within 1e-4 RMS; stereo flag, pilot level and sample counts
-exact; MPX within 1e-4 (max abs).  Every test here runs on the GPU."""
+exact; MPX within 1e-4 (max abs).
+
+The XDR pilot level (stereo_decoder.cpp pilotLevelTenthsKHz, 0.1 kHz steps)
+is exact wherever the pilot PLL is locked.  With a narrow IQ filter
+(W0 / XDR bandwidth < 100 kHz) the 19 kHz pilot is attenuated, the PLL free-
+runs, and the level becomes chaotic: the oracle against ITSELF moves by up to
+4 tenths when 1e-5 of noise is added to the MPX
+(tests/test_oracle_pinning.py::test_unlocked_pilot_level_is_chaotic), so
+those cases hold the level to PILOT_UNLOCKED_TOL instead.  Every test here
+runs on the GPU.
+"""
 import os
 import sys
 
@@ -25,14 +35,19 @@ def make_iq(fmx, kind, C, nblk, iq_rate=2_400_000, M=10, B=4096, noise=0.0, ch0=
     return iq, groups
 
 
-def check(g, o, c, nblk, tag=""):
+PILOT_UNLOCKED_TOL = 16   # tenths of kHz, free-running PLL only (see module doc)
+
+
+def check(g, o, c, nblk, tag="", pilot_tol=0):
     st = H.compare(g, o, c, nblk)
-    assert st["count_mismatch"] == 0, (tag, c, st)
-    assert st["stereo_mismatch"] == 0 and st["pilot_mismatch"] == 0, (tag, c, st)
-    assert st["mpx_max"] < MPX_MAX_TOL, (tag, c, st)
-    assert st["pcm_rms"] < PCM_RMS_TOL, (tag, c, st)
-    assert st["pcm_max"] < PCM_MAX_TOL, (tag, c, st)
+    info = (tag, c, {k: v for k, v in st.items() if not k.startswith("groups")})
+    assert st["count_mismatch"] == 0, info
+    assert st["stereo_mismatch"] == 0, info
+    assert st["mpx_max"] < MPX_MAX_TOL, info
+    assert st["pcm_rms"] < PCM_RMS_TOL, info
+    assert st["pcm_max"] < PCM_MAX_TOL, info
     assert st["groups_gpu"] == st["groups_oracle"], (tag, c, st["groups_gpu"], st["groups_oracle"])
+    assert st["pilot_maxdiff"] <= pilot_tol, info
     return st
 
 
@@ -120,21 +135,22 @@ def test_w0_bandwidth_sweep(fmx, oracle, torch_cuda, w0):
     iq, _ = make_iq(fmx, 2, C, nblk, ch0=20)
     g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
     for c in range(C):
-        check(g, outs[c], c, nblk, f"w0={w0}")
+        check(g, outs[c], c, nblk, f"w0={w0}", pilot_tol=0 if w0 >= 100_000 else PILOT_UNLOCKED_TOL)
 
 
-def test_resets_and_runtime_setters(fmx, oracle, torch_cuda):
+@pytest.mark.parametrize("bw", [114_000, 63_000])
+def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
     """Runtime::reset of one channel / all channels, XDR bandwidth change
     (re-created IQ FIR), de-emphasis change, force mono, AGC switch."""
     C, nblk = 3, 30
     iq, _ = make_iq(fmx, 2, C, nblk, ch0=40)
     resets = {8: 1, 16: -1}
-    params = {10: [("bandwidth_hz", 63_000, -1)], 12: [("deemphasis", 1, -1)],
+    params = {10: [("bandwidth_hz", bw, -1)], 12: [("deemphasis", 1, -1)],
               14: [("force_mono", 1, 2)], 18: [("force_mono", 0, 2), ("bandwidth_hz", 0, -1)],
               20: [("dsp_agc", 2, 0), ("blend", 2, -1)], 24: [("deemphasis", 2, 1)]}
     g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, resets=resets, params=params)
     for c in range(C):
-        check(g, outs[c], c, nblk, "setters")
+        check(g, outs[c], c, nblk, f"setters bw={bw}", pilot_tol=0 if bw >= 100_000 else PILOT_UNLOCKED_TOL)
 
 
 @pytest.mark.parametrize("n", [1500, 333])
@@ -273,7 +289,9 @@ def test_full_size_properties(fmx, torch_cuda):
                 total += 1
     assert st.float().mean().item() > 0.99
     assert total > 3 * C
-    bad = [c for c in range(C) if got[c] and not groups_align(got[c], tx[c])]
+    # some channels need > 40 blocks to acquire (oracle identical, see
+    # DESIGN.md); every channel that produced an error-free group must align
+    bad = [c for c in range(C) if any(g[4] == 0 for g in got[c]) and not groups_align(got[c], tx[c])]
     assert not bad, bad[:10]
     assert sum(1 for c in range(C) if any(g[4] == 0 for g in got[c])) > 0.99 * C
     h.close()

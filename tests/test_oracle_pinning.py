@@ -201,3 +201,41 @@ def test_oracle_regression_fixture(fmx, oracle):
             assert [list(g) for g in o["groups"]] == want["groups"]
             np.testing.assert_allclose(o["pcm_l"][:4], want["pcm_l_head"], rtol=0, atol=1e-6)
             np.testing.assert_allclose(o["mpx"][:4], want["mpx_head"], rtol=0, atol=1e-6)
+
+
+def _pilot_levels_with_perturbation(fmx, oracle, w0, nblk=10, ch=21):
+    import ctypes as Ct
+    B, M = 4096, 10
+    L = oracle.lib()
+    scfg = fmx.make_synth(kind=2, n_bits=8192)
+    bits, _ = fmx.synth_rds_bits(scfg, ch, 1)
+    iq = fmx.synth_host(scfg, ch, 1, 0, B * M * nblk, bits)[0]
+    p = oracle.Pipeline(oracle.make_cfg(w0_bandwidth_hz=w0))
+    s1 = L.oracle_stereo_create(240_000, 32_000)
+    s2 = L.oracle_stereo_create(240_000, 32_000)
+    rng = np.random.default_rng(1)
+    l, r = np.zeros(B, np.float32), np.zeros(B, np.float32)
+    a, b1, c, b2 = Ct.c_int(), Ct.c_int(), Ct.c_int(), Ct.c_int()
+    out = []
+    for b in range(nblk):
+        o = p.block(iq[b * 2 * B * M:(b + 1) * 2 * B * M])
+        mpx = np.ascontiguousarray(o["mpx"])
+        mp2 = np.ascontiguousarray((mpx + rng.normal(0, 1e-5, mpx.size)).astype(np.float32))
+        L.oracle_stereo_process(s1, mpx.ctypes.data, l.ctypes.data, r.ctypes.data, B, Ct.byref(a), Ct.byref(b1))
+        L.oracle_stereo_process(s2, mp2.ctypes.data, l.ctypes.data, r.ctypes.data, B, Ct.byref(c), Ct.byref(b2))
+        assert b1.value == o["pilot"]
+        out.append((b1.value, b2.value))
+    L.oracle_stereo_destroy(s1)
+    L.oracle_stereo_destroy(s2)
+    return out
+
+
+def test_unlocked_pilot_level_is_chaotic(fmx, oracle):
+    """Justifies the GPU tests' pilot-level tolerance for narrow IQ filters:
+    with W0 = 42 kHz the pilot PLL free-runs and 1e-5 of MPX noise moves the
+    oracle's OWN pilot level by several tenths; at W0 = 194 kHz (locked) it
+    does not move at all."""
+    wide = _pilot_levels_with_perturbation(fmx, oracle, 194_000)
+    assert all(x == y for x, y in wide)
+    narrow = _pilot_levels_with_perturbation(fmx, oracle, 42_000)
+    assert max(abs(x - y) for x, y in narrow) >= 2
