@@ -38,7 +38,7 @@ namespace fmx {
 #define AU_HALO 120
 #define AU_RHALO 32
 #define AU_MAXOUT 256
-#define PLL_T 64
+#define PLL_T 16
 
 static constexpr float kPiF = 3.14159265358979323846f;
 
@@ -577,109 +577,194 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
   return 0.0f;
 }
 
-__global__ __launch_bounds__(64) void k_pll(PllArgs a) {
-  __shared__ float sp[64][PLL_T + 1], sm[64][PLL_T + 1], sd[64][PLL_T + 1];
-  __shared__ float ol[64][PLL_T + 1], orr[64][PLL_T + 1];
-  const int lane = threadIdx.x;
-  const int c0 = blockIdx.x * 64;
-  const int c = c0 + lane;
-  const bool act = c < a.C;
+/* k_pll is a three-stage software pipeline over tiles of PLL_T samples for
+ * PLL_CH channels, one stage per wave of the workgroup:
+ *   wave 0  (lane = channel, serial)   PLL phase recursion, pilot/MPX
+ *           envelopes, pilot I/Q integrators: only what feeds back.
+ *   waves 2-3 (lane = (channel, t))    everything that is parallel in time:
+ *           sqrt, the five divisions of the blend target, the L-R matrix.
+ *   wave 1  (lane = channel, serial)   the blend recursion and the outputs,
+ *           then the loads of the next input tiles.
+ * Tile k is in stage 1 while tile k-1 is in stage 2 and tile k-2 in stage 3;
+ * three LDS slots rotate.  The arithmetic of every value is the reference's
+ * (stereo_decoder.cpp:226-288) in the same order; only WHERE it runs moved. */
+#define PLL_CH 64
+#define PLL_TS (PLL_T + 4)                 // padded row (16-B aligned)
+#define PLL_NF 5                           // fields per (channel, t) in a slot
+struct PllShared {
+  float slot[3][PLL_NF][PLL_CH][PLL_TS];   // S1 -> S2 (in place) -> S3
+  float in[2][2][PLL_CH][PLL_TS];          // pilot, mpx tiles for S1
+  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles for S2
+  int s2_flags[PLL_CH];                    // bit0 fmono, bit1 fstereo, bit2 detected, bits 8.. blend mode
+  float s2_gate[PLL_CH];
+  float blend_out[PLL_CH];                 // stage 3 -> stage 1 at block end
+};
+enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2, F_FREQ = 3, F_COS2 = 4 };  // S1 output
+enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };                 // S2 output
+
+// pilot + MPX of tile (t0, cnt) into in[buf]; lanes of one wave, 16-B loads
+// when rows are aligned.
+__device__ __forceinline__ void pll_load_in(const PllArgs &a, PllShared *sh, int buf, int c0, int t0, int cnt,
+                                            int lane, bool vec) {
+  if (vec && cnt == PLL_T) {
+    constexpr int Q = PLL_T / 4;  // float4 per row
+    float4 v[2][PLL_CH * Q / 64];
+#pragma unroll
+    for (int j = 0; j < PLL_CH * Q / 64; ++j) {
+      const int idx = lane + 64 * j;
+      const int row = idx / Q, q = idx % Q;
+      const int ch = min(c0 + row, a.C - 1);
+      v[0][j] = *reinterpret_cast<const float4 *>(a.pilot + (size_t)ch * a.pilot_stride + t0 + 4 * q);
+      v[1][j] = *reinterpret_cast<const float4 *>(a.mpx + (size_t)ch * a.mpx_stride + t0 + 4 * q);
+    }
+#pragma unroll
+    for (int j = 0; j < PLL_CH * Q / 64; ++j) {
+      const int idx = lane + 64 * j;
+      const int row = idx / Q, q = idx % Q;
+      *reinterpret_cast<float4 *>(&sh->in[buf][0][row][4 * q]) = v[0][j];
+      *reinterpret_cast<float4 *>(&sh->in[buf][1][row][4 * q]) = v[1][j];
+    }
+    return;
+  }
+  for (int idx = lane; idx < PLL_CH * PLL_T; idx += 64) {
+    const int row = idx / PLL_T, col = idx % PLL_T;
+    const int ch = c0 + row;
+    float p = 0.0f, m = 0.0f;
+    if (ch < a.C && col < cnt) {
+      p = a.pilot[(size_t)ch * a.pilot_stride + t0 + col];
+      m = a.mpx[(size_t)ch * a.mpx_stride + t0 + col];
+    }
+    sh->in[buf][0][row][col] = p;
+    sh->in[buf][1][row][col] = m;
+  }
+}
+
+// delay-line outputs of tile (t0, cnt): mpx[t - Dly] or the previous call's
+// history (stereo_decoder.cpp delayLine).
+__device__ __forceinline__ void pll_load_dly(const PllArgs &a, PllShared *sh, int buf, int c0, int t0, int cnt,
+                                             int lane, int Dly) {
+  constexpr int J = PLL_CH * PLL_T / 64;
+  float v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int idx = lane + 64 * j;
+    const int row = idx / PLL_T, col = idx % PLL_T;
+    const int ch = c0 + row;
+    float x = 0.0f;
+    if (ch < a.C && col < cnt) {
+      const int di = t0 + col - Dly;
+      x = (di >= 0) ? a.mpx[(size_t)ch * a.mpx_stride + di] : a.st_hist_rd[(size_t)ch * FMX_HIST + FMX_HIST + di];
+    }
+    v[j] = x;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int idx = lane + 64 * j;
+    sh->dly[buf][idx / PLL_T][idx % PLL_T] = v[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pll(PllArgs a) {
+  __shared__ PllShared shm;
+  PllShared *sh = &shm;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int c0 = blockIdx.x * PLL_CH;
   const FmxDesign *__restrict__ D = a.des;
   const int n = a.n;
+  const int NT = (n + PLL_T - 1) / PLL_T;
   const int Dly = D->delay_len;
-  FmxStereoState s;
-  FmxChanParam par;
-  if (act) {
-    s = a.st[c];
-    par = a.par[c];
-  } else {
-    s = FmxStereoState{};
-    par = FmxChanParam{};
-  }
-  const int mode = par.blend;
-  const float attack = D->blend_attack[mode], release = D->blend_release[mode], gate = D->gate[mode];
-  const bool fmono = par.force_mono != 0, fstereo = par.force_stereo != 0;
-  const float nominal = D->nominal, pmin = D->pll_min, pmax = D->pll_max;
-  const float alpha = D->pll_alpha, beta = D->pll_beta;
-  const float fsf = (float)D->fs;
   constexpr float kS = 0.9995f;
   constexpr float kI = 1.0f - 0.9995f;
-  float phaseNow = d_nco_phase(s.theta);
-  float vcoQ, vcoI;
-  sincosf(phaseNow, &vcoQ, &vcoI);
-  bool detected = s.detected != 0;
-
-  for (int n0 = 0; n0 < n; n0 += PLL_T) {
-    const int cnt = min(PLL_T, n - n0);
-    // cooperative coalesced tile loads: 64 rows x cnt columns
-    for (int idx = lane; idx < 64 * PLL_T; idx += 64) {
-      const int row = idx / PLL_T, col = idx % PLL_T;
-      const int ch = c0 + row;
-      if (ch < a.C && col < cnt) {
-        const size_t t = (size_t)(n0 + col);
-        sp[row][col] = a.pilot[(size_t)ch * a.pilot_stride + t];
-        sm[row][col] = a.mpx[(size_t)ch * a.mpx_stride + t];
-        const int di = n0 + col - Dly;
-        sd[row][col] = (di >= 0) ? a.mpx[(size_t)ch * a.mpx_stride + di]
-                                 : a.st_hist_rd[(size_t)ch * FMX_HIST + FMX_HIST + di];
-      }
+  if (n <= 0) {  // processAudio(n == 0) returns before touching state
+    const int ch = c0 + tid;
+    if (tid < PLL_CH && ch < a.C) {
+      if (a.stereo_out) a.stereo_out[ch] = a.st[ch].detected;
+      if (a.pilot_tenths_out) a.pilot_tenths_out[ch] = a.st[ch].level;
     }
-    __syncthreads();
-    if (act) {
-      for (int k = 0; k < cnt; ++k) {
-        const float pilot = sp[lane][k];
-        const float mpx = sm[lane][k];
-        const float delayed = sd[lane][k];
-        s.pilot_band_mag = (s.pilot_band_mag * kS) + (fabsf(pilot) * kI);
-        s.mpx_mag = (s.mpx_mag * kS) + (fabsf(mpx) * kI);
-        const float err = pilot * vcoQ;
-        s.dtheta += d_nco_constrain(err * alpha);
-        s.theta += d_nco_constrain(err * beta);
-        s.theta += s.dtheta;
-        const float phaseNext = d_nco_phase(s.theta);
-        float dphi = phaseNext - phaseNow;
-        if (dphi > kPiF) dphi -= 2.0f * kPiF;
-        else if (dphi < -kPiF) dphi += 2.0f * kPiF;
-        s.pll_phase = phaseNext;
-        s.pll_freq = d_clamp(dphi, pmin, pmax);
-        s.pilot_i = (s.pilot_i * kS) + ((pilot * vcoI) * kI);
-        s.pilot_q = (s.pilot_q * kS) + ((pilot * vcoQ) * kI);
-        const float magNow = sqrtf((s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q));
-        const float ratioNow = s.pilot_band_mag / fmaxf(s.mpx_mag, 1e-3f);
-        const float cohNow = magNow / fmaxf(s.pilot_band_mag, 1e-4f);
-        const float errHzNow = fabsf(s.pll_freq - nominal) * fsf / (2.0f * kPiF);
-        const float tgt = blend_target(ratioNow, cohNow, errHzNow, mode, fmono, fstereo, detected, gate);
-        float sN, cN;
-        sincosf(phaseNext, &sN, &cN);
-        const float monoNorm = delayed * 0.5f;
-        const float cos2 = (cN * cN) - (sN * sN);
-        const float lr = 2.0f * delayed * cos2;
-        const float sl = (delayed + lr) * 0.5f;
-        const float sr = (delayed - lr) * 0.5f;
-        const float ba = (tgt > s.blend) ? attack : release;
-        s.blend += (tgt - s.blend) * ba;
-        ol[lane][k] = monoNorm + ((sl - monoNorm) * s.blend);
-        orr[lane][k] = monoNorm + ((sr - monoNorm) * s.blend);
-        phaseNow = phaseNext;
-        vcoI = cN;
-        vcoQ = sN;
-      }
-    }
-    __syncthreads();
-    for (int idx = lane; idx < 64 * PLL_T; idx += 64) {
-      const int row = idx / PLL_T, col = idx % PLL_T;
-      const int ch = c0 + row;
-      if (ch < a.C && col < cnt) {
-        const size_t t = (size_t)ch * a.lr_stride + n0 + col;
-        a.lraw[t] = ol[row][col];
-        a.rraw[t] = orr[row][col];
-      }
-    }
-    __syncthreads();
+    return;
   }
-  if (!act) return;
-  // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
-  {
+  const bool vec = ((((uintptr_t)a.pilot) | ((uintptr_t)a.mpx)) & 15) == 0 && (a.pilot_stride & 3) == 0 &&
+                   (a.mpx_stride & 3) == 0;
+
+  if (tid < PLL_CH) {
+    const int ch = c0 + tid;
+    int f = 0;
+    float g = 1.0f;
+    if (ch < a.C) {
+      const FmxChanParam par = a.par[ch];
+      f = (par.force_mono ? 1 : 0) | (par.force_stereo ? 2 : 0) | (a.st[ch].detected ? 4 : 0) | (par.blend << 8);
+      g = D->gate[par.blend];
+    }
+    sh->s2_flags[tid] = f;
+    sh->s2_gate[tid] = g;
+  }
+  if (wave == 1) pll_load_in(a, sh, 0, c0, 0, min(PLL_T, n), lane, vec);
+  __syncthreads();
+
+  const int c = c0 + lane;
+  const bool act = c < a.C;
+  if (wave == 0) {
+    // ---------------- stage 1: the feedback recursions ----------------
+    FmxStereoState s = act ? a.st[c] : FmxStereoState{};
+    const float nominal = D->nominal, pmin = D->pll_min, pmax = D->pll_max;
+    const float alpha = D->pll_alpha, beta = D->pll_beta;
+    float phaseNow = d_nco_phase(s.theta);
+    float vcoQ, vcoI;
+    sincosf(phaseNow, &vcoQ, &vcoI);
+    for (int k = 0; k < NT + 2; ++k) {
+      if (k < NT) {
+        const int cnt = min(PLL_T, n - k * PLL_T);
+        const int ib = k & 1, sb = k % 3;
+        float pv[PLL_T], mv[PLL_T];
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const float4 x = *reinterpret_cast<const float4 *>(&sh->in[ib][0][lane][4 * q]);
+          const float4 y = *reinterpret_cast<const float4 *>(&sh->in[ib][1][lane][4 * q]);
+          pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
+          mv[4 * q] = y.x; mv[4 * q + 1] = y.y; mv[4 * q + 2] = y.z; mv[4 * q + 3] = y.w;
+        }
+#pragma unroll
+        for (int t = 0; t < PLL_T; ++t) {
+          if (t < cnt) {
+            const float pilot = pv[t];
+            const float mpx = mv[t];
+            s.pilot_band_mag = (s.pilot_band_mag * kS) + (fabsf(pilot) * kI);
+            s.mpx_mag = (s.mpx_mag * kS) + (fabsf(mpx) * kI);
+            const float err = pilot * vcoQ;
+            s.dtheta += d_nco_constrain(err * alpha);
+            s.theta += d_nco_constrain(err * beta);
+            s.theta += s.dtheta;
+            const float phaseNext = d_nco_phase(s.theta);
+            float dphi = phaseNext - phaseNow;
+            if (dphi > kPiF) dphi -= 2.0f * kPiF;
+            else if (dphi < -kPiF) dphi += 2.0f * kPiF;
+            s.pll_freq = d_clamp(dphi, pmin, pmax);
+            s.pilot_i = (s.pilot_i * kS) + ((pilot * vcoI) * kI);
+            s.pilot_q = (s.pilot_q * kS) + ((pilot * vcoQ) * kI);
+            float sN, cN;
+            sincosf(phaseNext, &sN, &cN);
+            sh->slot[sb][F_PBM][lane][t] = s.pilot_band_mag;
+            sh->slot[sb][F_MM][lane][t] = s.mpx_mag;
+            sh->slot[sb][F_MAG2][lane][t] = (s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q);
+            sh->slot[sb][F_FREQ][lane][t] = s.pll_freq;
+            sh->slot[sb][F_COS2][lane][t] = (cN * cN) - (sN * sN);
+            phaseNow = phaseNext;
+            vcoI = cN;
+            vcoQ = sN;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (!act) return;
+    s.pll_phase = phaseNow;
+    // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
+    const FmxChanParam par = a.par[c];
+    const bool fstereo = par.force_stereo != 0;
+    const float fsf = (float)D->fs;
+    bool detected = s.detected != 0;
     const float mag = sqrtf((s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q));
     s.pilot_magnitude = (s.pilot_magnitude * 0.9f) + (mag * 0.1f);
     const float mpxThr = detected ? 0.0028f : 0.005f;
@@ -711,10 +796,106 @@ __global__ __launch_bounds__(64) void k_pll(PllArgs a) {
     int lvl = (int)roundf(calibrated * 750.0f);
     s.level = lvl < 0 ? 0 : (lvl > 750 ? 750 : lvl);
     s.detected = detected ? 1 : 0;
+    s.blend = sh->blend_out[lane];  // stage 3 owns blend (stored before the last barrier)
+    a.st[c] = s;
+    if (a.stereo_out) a.stereo_out[c] = s.detected;
+    if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
+  } else if (wave == 1) {
+    // ---------------- stage 3: blend recursion + outputs; loader ----------------
+    float blend = act ? a.st[c].blend : 0.0f;
+    const int mode = sh->s2_flags[lane] >> 8;
+    const float attack = D->blend_attack[mode], release = D->blend_release[mode];
+    for (int k = 0; k < NT + 2; ++k) {
+      const int kt = k - 2;
+      if (kt >= 0 && kt < NT) {
+        const int cnt = min(PLL_T, n - kt * PLL_T);
+        const int sb = kt % 3;
+        float ov[2][PLL_T];
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const float4 tg = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_TGT][lane][4 * q]);
+          const float4 mo = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_MONO][lane][4 * q]);
+          const float4 dl = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_DL][lane][4 * q]);
+          const float4 dr = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_DR][lane][4 * q]);
+          const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
+          const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = 4 * q + u;
+            if (t < cnt) {
+              const float tgt = tga[u];
+              const float ba = (tgt > blend) ? attack : release;
+              blend += (tgt - blend) * ba;
+              ov[0][t] = moa[u] + (dla[u] * blend);
+              ov[1][t] = moa[u] + (dra[u] * blend);
+            }
+          }
+        }
+        if (act) {
+          float *ol = a.lraw + (size_t)c * a.lr_stride + kt * PLL_T;
+          float *orr = a.rraw + (size_t)c * a.lr_stride + kt * PLL_T;
+#pragma unroll
+          for (int t = 0; t < PLL_T; ++t) {
+            if (t < cnt) {
+              ol[t] = ov[0][t];
+              orr[t] = ov[1][t];
+            }
+          }
+        }
+      }
+      if (k == NT + 1) sh->blend_out[lane] = blend;
+      // loader: S1 input of tile k+1, delay-line tile k for S2
+      if (k + 1 < NT) pll_load_in(a, sh, (k + 1) & 1, c0, (k + 1) * PLL_T, min(PLL_T, n - (k + 1) * PLL_T), lane, vec);
+      if (k < NT) pll_load_dly(a, sh, k & 1, c0, k * PLL_T, min(PLL_T, n - k * PLL_T), lane, Dly);
+      __syncthreads();
+    }
+  } else {
+    // ---------------- stage 2: time-parallel work ----------------
+    const int t2 = tid - 128;  // 0..127
+    const float nominal = D->nominal;
+    const float fsf = (float)D->fs;
+    for (int k = 0; k < NT + 2; ++k) {
+      const int kt = k - 1;
+      if (kt >= 0 && kt < NT) {
+        const int cnt = min(PLL_T, n - kt * PLL_T);
+        const int sb = kt % 3, db = kt & 1;
+#pragma unroll 2
+        for (int j = 0; j < PLL_CH * PLL_T / 128; ++j) {
+          const int idx = t2 + 128 * j;
+          const int row = idx / PLL_T, t = idx % PLL_T;
+          const int fl = sh->s2_flags[row];
+          const float pbm = sh->slot[sb][F_PBM][row][t];
+          const float mm = sh->slot[sb][F_MM][row][t];
+          const float mag2 = sh->slot[sb][F_MAG2][row][t];
+          const float pf = sh->slot[sb][F_FREQ][row][t];
+          const float cos2 = sh->slot[sb][F_COS2][row][t];
+          const float delayed = sh->dly[db][row][t];
+          float tgt;
+          if (fl & 1) tgt = 0.0f;
+          else if (fl & 2) tgt = 1.0f;
+          else if (!(fl & 4)) tgt = 0.0f;  // blend_target() returns 0 on every path
+          else {
+            const float magNow = sqrtf(mag2);
+            const float ratioNow = pbm / fmaxf(mm, 1e-3f);
+            const float cohNow = magNow / fmaxf(pbm, 1e-4f);
+            const float errHzNow = fabsf(pf - nominal) * fsf / (2.0f * kPiF);
+            tgt = blend_target(ratioNow, cohNow, errHzNow, fl >> 8, false, false, true, sh->s2_gate[row]);
+          }
+          const float monoNorm = delayed * 0.5f;
+          const float lr = 2.0f * delayed * cos2;
+          const float sl = (delayed + lr) * 0.5f;
+          const float sr = (delayed - lr) * 0.5f;
+          if (t < cnt) {
+            sh->slot[sb][F_TGT][row][t] = tgt;
+            sh->slot[sb][F_MONO][row][t] = monoNorm;
+            sh->slot[sb][F_DL][row][t] = sl - monoNorm;
+            sh->slot[sb][F_DR][row][t] = sr - monoNorm;
+          }
+        }
+      }
+      __syncthreads();
+    }
   }
-  a.st[c] = s;
-  if (a.stereo_out) a.stereo_out[c] = s.detected;
-  if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
 }
 
 /* ================================================================== */
@@ -1460,7 +1641,7 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_pll, dim3((a.C + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(256), 0, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {

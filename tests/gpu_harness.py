@@ -71,8 +71,9 @@ def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=
     return res
 
 
-def compare(gres, ores, c, nblk):
-    """Per-channel comparison stats."""
+def compare(gres, ores, c, nblk, pcm_blocks=None):
+    """Per-channel comparison stats.  pcm_blocks (optional) restricts the PCM
+    and pilot-level statistics to those blocks."""
     mpx_err = 0.0
     pcm_sq = 0.0
     pcm_n = 0
@@ -88,17 +89,19 @@ def compare(gres, ores, c, nblk):
         k = len(o["pcm_l"])
         if int(g["count"][c]) != k:
             cnt_mismatch += 1
+        st_mismatch += int(o["stereo"] != int(g["stereo"][c]))
+        g_gpu += g["groups"][c]
+        g_ora += o["groups"]
+        if pcm_blocks is not None and b not in pcm_blocks:
+            continue
         k = min(k, int(g["count"][c]))
         dl = o["pcm_l"][:k] - g["pcm_l"][c, :k]
         dr = o["pcm_r"][:k] - g["pcm_r"][c, :k]
         pcm_sq += float(np.sum(dl * dl) + np.sum(dr * dr))
         pcm_n += 2 * k
         pcm_max = max(pcm_max, float(np.max(np.abs(dl))) if k else 0.0, float(np.max(np.abs(dr))) if k else 0.0)
-        st_mismatch += int(o["stereo"] != int(g["stereo"][c]))
         pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
         pil_maxdiff = max(pil_maxdiff, abs(int(o["pilot"]) - int(g["pilot"][c])))
-        g_gpu += g["groups"][c]
-        g_ora += o["groups"]
     return dict(mpx_max=mpx_err, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
                 stereo_mismatch=st_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
                 groups_gpu=g_gpu, groups_oracle=g_ora)

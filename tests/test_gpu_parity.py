@@ -38,8 +38,8 @@ def make_iq(fmx, kind, C, nblk, iq_rate=2_400_000, M=10, B=4096, noise=0.0, ch0=
 PILOT_UNLOCKED_TOL = 16   # tenths of kHz, free-running PLL only (see module doc)
 
 
-def check(g, o, c, nblk, tag="", pilot_tol=0):
-    st = H.compare(g, o, c, nblk)
+def check(g, o, c, nblk, tag="", pilot_tol=0, pcm_blocks=None):
+    st = H.compare(g, o, c, nblk, pcm_blocks=pcm_blocks)
     info = (tag, c, {k: v for k, v in st.items() if not k.startswith("groups")})
     assert st["count_mismatch"] == 0, info
     assert st["stereo_mismatch"] == 0, info
@@ -141,7 +141,11 @@ def test_w0_bandwidth_sweep(fmx, oracle, torch_cuda, w0):
 @pytest.mark.parametrize("bw", [114_000, 63_000])
 def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
     """Runtime::reset of one channel / all channels, XDR bandwidth change
-    (re-created IQ FIR), de-emphasis change, force mono, AGC switch."""
+    (re-created IQ FIR), de-emphasis change, force mono, AGC switch.
+    At 63 kHz the pilot PLL free-runs while the blend is still open (stereo was
+    acquired at the wide setting): the oracle's own L/R then moves by 1e-2 RMS
+    under 1e-5 of MPX noise, so PCM and pilot level are compared outside the
+    narrow-bandwidth blocks 10..15 (MPX, flags, counts, RDS everywhere)."""
     C, nblk = 3, 30
     iq, _ = make_iq(fmx, 2, C, nblk, ch0=40)
     resets = {8: 1, 16: -1}
@@ -150,7 +154,10 @@ def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
               20: [("dsp_agc", 2, 0), ("blend", 2, -1)], 24: [("deemphasis", 2, 1)]}
     g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, resets=resets, params=params)
     for c in range(C):
-        check(g, outs[c], c, nblk, f"setters bw={bw}", pilot_tol=0 if bw >= 100_000 else PILOT_UNLOCKED_TOL)
+        narrow = bw < 100_000
+        blocks = [b for b in range(nblk) if not (10 <= b < 16)] if narrow else None
+        check(g, outs[c], c, nblk, f"setters bw={bw}", pcm_blocks=blocks,
+              pilot_tol=PILOT_UNLOCKED_TOL if narrow else 0)
 
 
 @pytest.mark.parametrize("n", [1500, 333])
