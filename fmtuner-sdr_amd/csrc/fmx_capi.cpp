@@ -49,6 +49,9 @@ struct TimingSet {
 struct Handle {
   fmx_config cfg{};
   int C = 0, device = 0, M = 1;
+  // decimator input samples every channel has seen since its last reset
+  // (capped at L-1): a full history lets the frontend take its VEC path
+  long dec_fill = 0;
   std::string err;
   // sA: frontend, resets, uploads; sB: stereo + audio; sC: RDS.  Step k's
   // frontend runs while step k-1's stereo/RDS kernels (latency-bound, one
@@ -278,6 +281,11 @@ static int join_into_A(Handle *h) {
   return FMX_OK;
 }
 
+static bool dec_warm(const Handle *h) { return h->M > 1 && h->dec_fill >= h->hdes->dec_len - 1; }
+static void dec_advance(Handle *h, int n_out) {
+  h->dec_fill = std::min<long>(h->hdes->dec_len - 1, h->dec_fill + (long)n_out * h->M);
+}
+
 static ResetArgs reset_args(Handle *h) {
   ResetArgs r{};
   r.des = h->ddes;
@@ -304,7 +312,10 @@ static ResetArgs reset_args(Handle *h) {
 
 static int apply_resets(Handle *h) {
   bool any = false;
-  for (int v : h->hmask) any |= (v != 0);
+  for (int v : h->hmask) {
+    any |= (v != 0);
+    if (v & (RS_DECIM | RS_CREATE)) h->dec_fill = 0;
+  }
   if (!any) return FMX_OK;
   int rc = join_into_A(h);
   if (rc != FMX_OK) return rc;
@@ -623,10 +634,11 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
     KTimer t(h, FMX_K_FRONTEND, h->sA);
-    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA)) != FMX_OK) {
+    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
       return rc;
     }
+    dec_advance(h, n);
   }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC) ----
@@ -837,7 +849,8 @@ int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out,
   a.clip_out = nullptr;
   {
     KTimer t(h, FMX_K_FRONTEND, h->sA);
-    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA)) != FMX_OK) return rc;
+    if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) return rc;
+    dec_advance(h, n_out);
   }
   return stage_end(h);
 }

@@ -188,6 +188,7 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     for (int i = 0; i < d->dec_len; ++i) d->dec_taps[i] = d->dec_taps_raw[i] * kScale;
     for (int p = 0; p < M; ++p)
       for (int q = 0; q < d->dec_tpp; ++q) d->dec_poly[p * d->dec_tpp + q] = d->dec_taps[q * M + p];
+    for (int i = 0; i < d->dec_len; ++i) d->dec_pad[FMX_DEC_PAD + i] = d->dec_taps[i];
   } else {
     d->dec_scale = 1.0f;
   }

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #define FMX_MAX_DEC 512      // M * taps_per_phase (liquid_primitives.cpp:388)
+#define FMX_DEC_PAD 32       // zero taps each side of dec_pad (>= 3*M)
 #define FMX_IQ_DESIGNS 31    // 30 XDR bandwidth filters + the FMDemod ctor filter
 #define FMX_IQ_CTOR 30       // index of the ctor filter (fm_demod.cpp:103-105)
 #define FMX_IQ_MAXLEN 121
@@ -40,6 +41,7 @@ typedef struct {
   float dec_taps[FMX_MAX_DEC];
   float dec_taps_raw[FMX_MAX_DEC];
   float dec_poly[FMX_MAX_DEC]; // [p][q] = dec_taps[q*M + p]  (phase-major)
+  float dec_pad[FMX_MAX_DEC + 2 * FMX_DEC_PAD]; // [FMX_DEC_PAD + k] = dec_taps[k], zeros around
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
   int iq_len[FMX_IQ_DESIGNS];
   float iq_scale[FMX_IQ_DESIGNS];

@@ -128,7 +128,9 @@ struct RdsArgs {
 };
 
 // launchers (fmx_kernels.hip); stream is a hipStream_t
-int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream);
+// vec: the caller guarantees every channel's decimator history is full
+// (dec_valid == L-1); 16-B row alignment is checked here.
+int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec = false);
 int launch_pll(const PllArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);

@@ -101,6 +101,44 @@ __device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const flo
   }
 }
 
+// Decimator on natural-order u8 IQ in LDS (VEC path).  raw holds samples
+// s = 0.. of the window origin n0*M - L, 2 bytes each; outputs j = 3*tid + r
+// need s in [j*M + 1, j*M + L].  Thread t reads dwords (3M/2)*t + e: for
+// M = 10 the stride is 15 dwords, conflict-free.  hpad = dec_pad (+PAD);
+// (I, Q) pairs go through packed FP32 FMAs.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int M, int TPP>
+__device__ __forceinline__ void fe_decimate_u8(const uint8_t *raw, const float *__restrict__ hpad, int tid,
+                                               f32x2 (&acc)[3]) {
+  constexpr int L = M * TPP;
+  constexpr int NB = TPP + 3;  // blocks of M samples covering s in [0, 2M + L]
+  const uint32_t *rw = reinterpret_cast<const uint32_t *>(raw) + (3 * M / 2) * tid;
+  const f32x2 off = {-127.5f, -127.5f};
+#pragma unroll
+  for (int r = 0; r < 3; ++r) acc[r] = f32x2{0.0f, 0.0f};
+#pragma unroll 1
+  for (int qb = 0; qb < NB; ++qb) {
+    const float *hq = hpad + FMX_DEC_PAD + L - qb * M;  // tap of sample u, output r: hq[r*M - u]
+    uint32_t w[M / 2];
+#pragma unroll
+    for (int e = 0; e < M / 2; ++e) w[e] = rw[qb * (M / 2) + e];
+#pragma unroll
+    for (int u = 0; u < M; ++u) {
+      const uint32_t ww = w[u >> 1];
+      f32x2 x;
+      const int sh0 = (u & 1) ? 16 : 0;  // v_cvt_f32_ubyte{0..3}
+      x.x = (float)((ww >> sh0) & 255u);
+      x.y = (float)((ww >> (sh0 + 8)) & 255u);
+      x = x + off;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const float h = hq[r * M - u];
+        acc[r] = __builtin_elementwise_fma(f32x2{h, h}, x, acc[r]);
+      }
+    }
+  }
+}
+
 // Real-tap FIR of runtime length L on a complex LDS signal, 3 outputs per
 // thread at x[base + r]; hp = taps padded with 5 zeros on each side
 // (hp[k + 5] = h[k]), x needs 3 samples of slack past base + 2.
@@ -196,19 +234,40 @@ __device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i
   return lo;
 }
 
-template <int M, int TPP>
+// LDS layout of k_frontend (shared with the launcher's size computation).
+// VEC: the decimator input is natural-order u8 IQ (HB halo bytes + the
+// chunk); otherwise fp16 pairs in phase-major order.
+template <int M, int TPP, bool VEC> struct FeLayout {
+  static constexpr int L = (M > 1) ? M * TPP : 1;
+  static constexpr int Q = FE_T + ((M > 1) ? TPP : 1);
+  static constexpr int HB = ((2 * (L - 1)) + 15) & ~15;       // VEC halo bytes (16-B aligned)
+  static constexpr int RAW_BYTES = HB + 2 * FE_T * M + 64;     // + slack read past the chunk
+  static constexpr int IN_BYTES = (M > 1) ? (VEC ? RAW_BYTES : M * Q * 4) : 0;
+  static constexpr int YB_BYTES = (FE_T + 1) * 8;
+  static constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
+  static constexpr int XIN = R0;
+  static constexpr int MX = XIN + (FE_HALO_IQ + FE_T + 8) * 8;
+  static constexpr int RB = MX + (FMX_HIST + FE_T + 8) * 4;   // RDS resampler window: 32 history + chunk
+  static constexpr int SH = RB + (32 + FE_T + 8) * 4;
+  static constexpr int BYTES = SH + (int)sizeof(FeShared);
+  static constexpr int NPF = (M > 1) ? (RAW_BYTES - 64 + 16 * 256 - 1) / (16 * 256) : 1;  // 16-B loads / thread
+};
+
+template <int M, int TPP, bool VEC>
 __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  constexpr int L = (M > 1) ? M * TPP : 1;
-  constexpr int Q = FE_T + ((M > 1) ? TPP : 1);
-  constexpr int IN_BYTES = (M > 1) ? M * Q * 4 : 0;
-  constexpr int YB_BYTES = (FE_T + 1) * 8;
-  constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
+  using LY = FeLayout<M, TPP, VEC>;
+  static_assert(!VEC || LY::HB >= 2 * LY::L, "VEC halo must hold L samples");
+  static_assert(!VEC || 3 * M <= FMX_DEC_PAD, "dec_pad too short for this M");
+  constexpr int L = LY::L;
+  constexpr int Q = LY::Q;
   __half2 *inq = reinterpret_cast<__half2 *>(smem);
+  uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem);
-  float2 *xin = reinterpret_cast<float2 *>(smem + R0);
-  float *mx = reinterpret_cast<float *>(smem + R0 + (FE_HALO_IQ + FE_T + 8) * 8);
-  FeShared *sh = reinterpret_cast<FeShared *>(smem + R0 + (FE_HALO_IQ + FE_T + 8) * 8 + (FMX_HIST + FE_T + 8) * 4);
+  float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
+  float *mx = reinterpret_cast<float *>(smem + LY::MX);
+  float *rb = reinterpret_cast<float *>(smem + LY::RB);
+  FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
 
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -267,13 +326,72 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     sched_n = a.rds_sched_n[g];
   }
   const float *rhist = a.rds_hist + (size_t)c * 32;
+  if (rds && tid < 32) rb[tid] = rhist[tid];
   int e_pos = 0;
+  // VEC: chunk bytes [2*n0*M - HB, 2*(n0+cnt)*M) are fetched with 16-B loads
+  // one chunk ahead into registers (HBM latency hidden behind the previous
+  // chunk); the host guarantees 16-B aligned rows and a full decimator history.
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 pf[LY::NPF];
+  auto prefetch = [&](int n0p) {
+    const long nb = LY::HB + 2L * min(FE_T, n - n0p) * M;
+    const uint8_t *base = a.iq + (size_t)c * a.iq_stride + 2L * n0p * M - LY::HB;
+#pragma unroll
+    for (int j = 0; j < LY::NPF; ++j) {
+      const long off = 16L * (tid + 256 * j);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (off < nb && (n0p > 0 || off >= LY::HB))  // nb is a multiple of 16 (host check)
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off));
+      pf[j] = v;
+    }
+  };
+  if constexpr (VEC && M > 1) {
+    if (n > 0) prefetch(0);
+  }
   __syncthreads();
 
   for (int n0 = 0; n0 < n; n0 += FE_T) {
     const int cnt = min(FE_T, n - n0);
     // ================= baseband x[j] =================
-    if (a.in_mode == FE_IN_U8_DECIM) {
+    if constexpr (VEC && M > 1) {
+#pragma unroll
+      for (int j = 0; j < LY::NPF; ++j) {
+        const int off = 16 * (tid + 256 * j);
+        if (off < LY::HB + 2 * FE_T * M && (n0 > 0 || off >= LY::HB))
+          *reinterpret_cast<u32x4 *>(raw + off) = pf[j];
+      }
+      if (n0 == 0) {  // halo = the carried history (dec_valid == L-1 here)
+        for (int h = tid; h < LY::HB / 2; h += 256) {
+          const int hh = h - (LY::HB / 2 - (L - 1));  // history index, < 0 unused
+          uint16_t v = 0;
+          if (hh >= 0) v = (uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8);
+          reinterpret_cast<uint16_t *>(raw)[h] = v;
+        }
+      }
+      if (n0 + FE_T < n) prefetch(n0 + FE_T);
+      __syncthreads();
+      f32x2 acc[3];
+      // window origin in raw: sample HB/2 - L (so that s = j*M + 1 .. j*M + L)
+      fe_decimate_u8<M, TPP>(raw + (LY::HB - 2 * L), D->dec_pad, tid, acc);
+      int myclip = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int j = 3 * tid + r;
+        if (j < cnt) {
+          const float yr = acc[r].x * D->dec_scale;
+          const float yi = acc[r].y * D->dec_scale;
+          if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
+          xin[FE_HALO_IQ + j] = make_float2(yr, yi);
+          if (a.bb_out) {
+            float *o = a.bb_out + (size_t)c * a.bb_stride + 2 * (size_t)(n0 + j);
+            o[0] = yr;
+            o[1] = yi;
+          }
+        }
+      }
+      if (myclip) atomicAdd(&sh->clip, myclip);
+      __syncthreads();  // raw aliases yb
+    } else if (a.in_mode == FE_IN_U8_DECIM) {
       if constexpr (M > 1) {
         const long g0 = (long)n0 * M - (L - 1);
         const int span = (cnt - 1) * M + L;
@@ -438,10 +556,15 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         const float im = p.x * r.y - p.y * r.x;
         const float m = atan2f(im, re) * ref;
         mx[FMX_HIST + j] = m;
+        if (rds) rb[32 + j] = m;
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
     } else if (a.in_mode == FE_IN_MPX) {
-      for (int j = tid; j < cnt; j += 256) mx[FMX_HIST + j] = a.in_f[(size_t)c * a.in_stride + n0 + j];
+      for (int j = tid; j < cnt; j += 256) {
+        const float m = a.in_f[(size_t)c * a.in_stride + n0 + j];
+        mx[FMX_HIST + j] = m;
+        if (rds) rb[32 + j] = m;
+      }
     }
     __syncthreads();
 
@@ -465,10 +588,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       const int eb = sh->e_begin, ee = sh->e_end;
       for (int e = eb + tid; e < ee; e += 256) {
         const FmxSched en = sched[e];
-        auto get = [&](int ii) -> float {
-          if (ii >= n0 - FMX_HIST + 1 && (n0 > 0 || ii >= 0)) return mx[FMX_HIST + ii - n0];
-          return rhist[32 + ii];
-        };
+        auto get = [&](int ii) -> float { return rb[32 + ii - n0]; };
         a.rds_out[(size_t)c * a.rds_stride + e] = resamp_out<FMX_RDS_RS_SUB>(D->rds_rs_h, en.packed, en.mu, get);
       }
       e_pos = ee;
@@ -482,7 +602,9 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       cm0 = mx[tid + cnt];
       cm1 = mx[tid + 256 + cnt];
       const float2 cy = yb[cnt];
+      const float crb = (rds && tid < 32) ? rb[cnt + tid] : 0.0f;
       __syncthreads();
+      if (rds && tid < 32) rb[tid] = crb;
       if (demod && tid < FE_HALO_IQ) xin[tid] = cx;
       mx[tid] = cm0;
       mx[tid + 256] = cm1;
@@ -544,14 +666,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[h];
   }
   if (rds) {
-    // new RDS resampler window: last 32 MPX samples
-    float v = 0.0f;
-    if (tid < 32) {
-      const int ii = n - 32 + tid;
-      v = (ii >= 0) ? mx[FMX_HIST - 32 + tid] : rhist[32 + ii];
-    }
-    __syncthreads();
-    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = v;
+    // new RDS resampler window: last 32 MPX samples (carried in rb)
+    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = rb[tid];
     if (tid == 0) a.rds_count[c] = sched_n;
   }
   if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
@@ -1604,24 +1720,16 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
 /* ================================================================== */
 /* launchers                                                           */
 /* ================================================================== */
-template <int M, int TPP> static size_t fe_smem() {
-  constexpr int Q = FE_T + ((M > 1) ? TPP : 1);
-  constexpr int IN_BYTES = (M > 1) ? M * Q * 4 : 0;
-  constexpr int YB_BYTES = (FE_T + 1) * 8;
-  constexpr int R0 = ((IN_BYTES > YB_BYTES ? IN_BYTES : YB_BYTES) + 15) & ~15;
-  return (size_t)R0 + (FE_HALO_IQ + FE_T + 8) * 8 + (FMX_HIST + FE_T + 8) * 4 + sizeof(FeShared);
-}
-
-template <int M, int TPP> static int fe_launch(const FeArgs &a, hipStream_t st) {
-  const size_t smem = fe_smem<M, TPP>();
+template <int M, int TPP, bool VEC> static int fe_launch(const FeArgs &a, hipStream_t st) {
+  const size_t smem = (size_t)FeLayout<M, TPP, VEC>::BYTES;
   static bool configured = false;
   if (!configured) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_frontend<M, TPP>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_frontend<M, TPP, VEC>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
       return FMX_E_HIP;
     configured = true;
   }
-  hipLaunchKernelGGL((k_frontend<M, TPP>), dim3(a.C), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((k_frontend<M, TPP, VEC>), dim3(a.C), dim3(256), smem, st, a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 
@@ -1630,13 +1738,14 @@ template <int M, int TPP> static int fe_launch(const FeArgs &a, hipStream_t st) 
 // The decimation factor is a host-known constant of the handle; expose
 // explicit launchers so fmx_capi can pick the instantiation.
 namespace fmx {
-int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream) {
+int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1>(a, st);
-  if (M == 10 && tpp == 28) return fe_launch<10, 28>(a, st);
-  if (M == 8 && tpp == 28) return fe_launch<8, 28>(a, st);
-  if (M == 4 && tpp == 20) return fe_launch<4, 20>(a, st);
-  if (M == 2 && tpp == 12) return fe_launch<2, 12>(a, st);
+  if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1, false>(a, st);
+  vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
+  if (M == 10 && tpp == 28) return vec ? fe_launch<10, 28, true>(a, st) : fe_launch<10, 28, false>(a, st);
+  if (M == 8 && tpp == 28) return vec ? fe_launch<8, 28, true>(a, st) : fe_launch<8, 28, false>(a, st);
+  if (M == 4 && tpp == 20) return vec ? fe_launch<4, 20, true>(a, st) : fe_launch<4, 20, false>(a, st);
+  if (M == 2 && tpp == 12) return vec ? fe_launch<2, 12, true>(a, st) : fe_launch<2, 12, false>(a, st);
   return FMX_E_INVALID;
 }
 
