@@ -74,6 +74,11 @@ struct Handle {
   uint8_t *dec_hist = nullptr;
   int *dec_valid = nullptr;
   float *dc_v = nullptr, *agc = nullptr, *fd_prev = nullptr, *clip = nullptr;
+  // RF level (computeSignalLevel arguments per channel; smoother state)
+  std::vector<double> hsig;   // [C][4] gain*factor, bias, floor, ceil
+  double *dsig = nullptr;
+  float *sig_smooth = nullptr;
+  bool sig_dirty = true;
   float2_t *iq_hist = nullptr;
   float *st_hist = nullptr, *lr_hist = nullptr, *af_win = nullptr, *af_iir = nullptr;
   float *mono_win = nullptr, *mono_iir = nullptr, *rds_hist = nullptr, *ring = nullptr;
@@ -330,6 +335,12 @@ static int apply_resets(Handle *h) {
 }
 
 static int sync_params(Handle *h) {
+  if (h->sig_dirty) {
+    int rc = join_into_A(h);
+    if (rc != FMX_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(h->dsig, h->hsig.data(), sizeof(double) * h->hsig.size(), hipMemcpyHostToDevice, h->sA));
+    h->sig_dirty = false;
+  }
   if (!h->par_dirty) return FMX_OK;
   int rc = join_into_A(h);
   if (rc != FMX_OK) return rc;
@@ -460,6 +471,16 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->agc, C * 2)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->fd_prev, C * 2)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->dsig, C * 4)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
+  HIP_TRY(hipMemset(h->sig_smooth, 0, sizeof(float) * 2 * C));
+  h->hsig.resize(static_cast<size_t>(C) * 4);
+  for (int c = 0; c < C; ++c) {  // gain 0, config.h:27-29 defaults
+    h->hsig[4 * c] = 0.0;
+    h->hsig[4 * c + 1] = -4.0;
+    h->hsig[4 * c + 2] = -55.0;
+    h->hsig[4 * c + 3] = -19.0;
+  }
   if ((rc = dalloc(h, &h->iq_hist, C * (FMX_IQ_MAXLEN - 1))) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->st_hist, FMX_ST_BUFS * C * FMX_HIST)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->lr_hist, C * 2 * (FMX_LR_LEN - 1))) != FMX_OK) return rc;
@@ -518,6 +539,8 @@ static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   a.fd_prev = h->fd_prev;
   a.rds_hist = h->rds_hist;
   a.clip_out = h->clip;
+  a.sig_par = h->dsig;
+  a.sig_smooth = h->sig_smooth;
   a.rds_count = h->rds_count[buf];
   a.rds_sched = h->t_rds.d_sched[h->t_rds.cur];
   a.rds_sched_n = h->t_rds.d_count[h->t_rds.cur];
@@ -633,6 +656,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.rds_stride = h->rds_stride;
     }
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
+    a.sig_out = o->d_signal;
     KTimer t(h, FMX_K_FRONTEND, h->sA);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
@@ -821,6 +845,26 @@ int fmx_set_param(void *handle, int channel, int key, int value) {
       default: h->err = "unknown parameter key"; return FMX_E_INVALID;
     }
   }
+  return FMX_OK;
+}
+
+int fmx_set_signal_params(void *handle, int channel, int applied_gain_db, double gain_comp_factor, double bias_db,
+                          double floor_dbfs, double ceil_dbfs) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  if (channel >= h->C) {
+    h->err = "channel out of range";
+    return FMX_E_INVALID;
+  }
+  const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
+  for (int c = c0; c < c1; ++c) {
+    // computeSignalLevel: compensated = (dbfs - gain * factor) + bias
+    h->hsig[4 * c] = static_cast<double>(applied_gain_db) * gain_comp_factor;
+    h->hsig[4 * c + 1] = bias_db;
+    h->hsig[4 * c + 2] = floor_dbfs;
+    h->hsig[4 * c + 3] = ceil_dbfs;
+  }
+  h->sig_dirty = true;
   return FMX_OK;
 }
 

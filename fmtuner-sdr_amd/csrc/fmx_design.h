@@ -64,7 +64,7 @@ typedef struct {
   float rds_rs_h[FMX_NPFB * FMX_RDS_RS_SUB];
   float af_del, rds_del;
   // RDS subcarrier (subcarrier.cpp:94-106, liquid_wrappers.cpp)
-  float rds_fir[FMX_RDS_FIR];
+  float rds_fir[FMX_RDS_NACC * FMX_RDS_DECIM]; // 255 taps + zeros to 264 (k_rds reads rows jp + 24 i)
   float rds_fir_scale;
   float agc_bw, agc_g0;
   uint32_t rds_dtheta0;

@@ -55,6 +55,9 @@ struct FeArgs {
   int rds_stride;
   int *rds_count;    // [C]
   float *clip_out;   // [C]
+  fmx_signal_level *sig_out;  // [C] RF level (u8 inputs), may be null
+  const double *sig_par;      // [C][4] gain*factor, bias, floor, ceil
+  float *sig_smooth;          // [C][2] smoother value, initialized flag
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
   // state

@@ -54,6 +54,14 @@ __device__ __forceinline__ uint32_t d_nco_constrain(float x) {
 __device__ __forceinline__ float d_nco_phase(uint32_t theta) {
   return (float)(6.283185307179586 * (double)(float)theta / 4294967296.0);
 }
+// x / c correctly rounded for a constant c with rc = RN(1/c) (Markstein:
+// residual exact by FMA); 3 dependent ops instead of the IEEE divide
+// sequence.  Checked against IEEE division on 6e6 phase increments (c = 57000).
+__device__ __forceinline__ float d_div_const(float x, float c, float rc) {
+  const float q = x * rc;
+  const float r = fmaf(-q, c, x);
+  return fmaf(r, rc, q);
+}
 __device__ __forceinline__ float d_clamp(float v, float lo, float hi) {
   return (v < lo) ? lo : ((hi < v) ? hi : v);
 }
@@ -234,6 +242,25 @@ __device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i
   return lo;
 }
 
+// RF level accumulators of the raw u8 IQ (computeSignalLevel,
+// signal_level.cpp:145-204): exact integer sums, clip counts per sample.
+struct SigAcc {
+  uint32_t sI = 0, sQ = 0, sII = 0, sQQ = 0, hard = 0, nearc = 0;
+  __device__ __forceinline__ void sample(uint32_t i, uint32_t q) {
+    sI += i;
+    sQ += q;
+    sII += i * i;
+    sQQ += q * q;
+    const uint32_t lo = min(i, q), hi = max(i, q);
+    hard += (lo <= 1u || hi >= 254u) ? 1u : 0u;
+    nearc += (lo <= 8u || hi >= 247u) ? 1u : 0u;
+  }
+  __device__ __forceinline__ void word(uint32_t w) {  // bytes I0 Q0 I1 Q1
+    sample(w & 255u, (w >> 8) & 255u);
+    sample((w >> 16) & 255u, w >> 24);
+  }
+};
+
 // LDS layout of k_frontend (shared with the launcher's size computation).
 // VEC: the decimator input is natural-order u8 IQ (HB halo bytes + the
 // chunk); otherwise fp16 pairs in phase-major order.
@@ -248,7 +275,8 @@ template <int M, int TPP, bool VEC> struct FeLayout {
   static constexpr int XIN = R0;
   static constexpr int MX = XIN + (FE_HALO_IQ + FE_T + 8) * 8;
   static constexpr int RB = MX + (FMX_HIST + FE_T + 8) * 4;   // RDS resampler window: 32 history + chunk
-  static constexpr int SH = RB + (32 + FE_T + 8) * 4;
+  static constexpr int SG = RB + (32 + FE_T + 8) * 4;            // 4 waves x 6 u64 RF-level partials
+  static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (M > 1) ? (RAW_BYTES - 64 + 16 * 256 - 1) / (16 * 256) : 1;  // 16-B loads / thread
 };
@@ -267,7 +295,10 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
   float *mx = reinterpret_cast<float *>(smem + LY::MX);
   float *rb = reinterpret_cast<float *>(smem + LY::RB);
+  unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
+  const bool want_sig = a.sig_out != nullptr && a.in_mode != FE_IN_CF && a.in_mode != FE_IN_MPX;
+  SigAcc sig;
 
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -359,6 +390,12 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         const int off = 16 * (tid + 256 * j);
         if (off < LY::HB + 2 * FE_T * M && (n0 > 0 || off >= LY::HB))
           *reinterpret_cast<u32x4 *>(raw + off) = pf[j];
+        if (want_sig && off >= LY::HB && off < LY::HB + 2 * cnt * M) {
+          sig.word(pf[j].x);
+          sig.word(pf[j].y);
+          sig.word(pf[j].z);
+          sig.word(pf[j].w);
+        }
       }
       if (n0 == 0) {  // halo = the carried history (dec_valid == L-1 here)
         for (int h = tid; h < LY::HB / 2; h += 256) {
@@ -393,6 +430,11 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       __syncthreads();  // raw aliases yb
     } else if (a.in_mode == FE_IN_U8_DECIM) {
       if constexpr (M > 1) {
+        if (want_sig)
+          for (int j = tid; j < cnt * M; j += 256) {
+            const uint16_t w = iq16[(long)n0 * M + j];
+            sig.sample(w & 255u, w >> 8);
+          }
         const long g0 = (long)n0 * M - (L - 1);
         const int span = (cnt - 1) * M + L;
         for (int li = tid; li < span; li += 256) {
@@ -448,6 +490,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       for (int j = tid; j < cnt; j += 256) {
         const uint8_t ib = p[2 * (size_t)(n0 + j)], qb = p[2 * (size_t)(n0 + j) + 1];
         if (ib == 0 || ib == 255 || qb == 0 || qb == 255) myclip++;
+        if (want_sig) sig.sample(ib, qb);
         xin[FE_HALO_IQ + j] = make_float2(((float)ib - 127.0f) / 127.5f, ((float)qb - 127.0f) / 127.5f);
       }
       if (myclip) atomicAdd(&sh->clip, myclip);
@@ -672,6 +715,57 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   }
   if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
     a.clip_out[c] = (n > 0) ? (float)sh->clip / (float)n : 0.0f;
+  if (want_sig) {
+    unsigned long long v[6] = {sig.sI, sig.sQ, sig.sII, sig.sQQ, sig.hard, sig.nearc};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      for (int d = 32; d >= 1; d >>= 1) v[k] += __shfl_xor(v[k], d);
+    if (lane == 0)
+      for (int k = 0; k < 6; ++k) sgp[wave * 6 + k] = v[k];
+    __syncthreads();
+    if (tid == 0) {
+      double t[6];
+      for (int k = 0; k < 6; ++k) t[k] = (double)(sgp[k] + sgp[6 + k] + sgp[12 + k] + sgp[18 + k]);
+      fmx_signal_level r;
+      r.level120 = 0.0f;
+      r.dbfs = -120.0;
+      r.compensated_dbfs = -120.0;
+      r.hard_clip_ratio = 0.0;
+      r.near_clip_ratio = 0.0;
+      const long samples = (long)n * ((a.in_mode == FE_IN_U8_DECIM) ? M : 1);
+      if (samples > 0) {
+        // sums of (b - 127.5) / 127.5 and its square from the exact byte sums
+        const double nn = (double)samples, k1 = 1.0 / 127.5;
+        const double sumI = (t[0] - 127.5 * nn) * k1, sumQ = (t[1] - 127.5 * nn) * k1;
+        const double sumII = (t[2] - 255.0 * t[0] + 16256.25 * nn) * (k1 * k1);
+        const double sumQQ = (t[3] - 255.0 * t[1] + 16256.25 * nn) * (k1 * k1);
+        const double meanI = sumI / nn, meanQ = sumQ / nn;
+        const double varI = fmax(0.0, (sumII / nn) - (meanI * meanI));
+        const double varQ = fmax(0.0, (sumQQ / nn) - (meanQ * meanQ));
+        const double rms = sqrt(fmax(1e-15, 0.5 * (varI + varQ)));
+        const double *sp = a.sig_par + 4 * (size_t)c;  // gain*factor, bias, floor, ceil
+        r.dbfs = 20.0 * log10(rms + 1e-12);
+        r.compensated_dbfs = r.dbfs - sp[0] + sp[1];
+        const double safeCeil = fmax(sp[3], sp[2] + 1.0);
+        const double norm = (r.compensated_dbfs - sp[2]) / (safeCeil - sp[2]);
+        const float l = (float)(norm * 120.0);
+        r.level120 = l < 0.0f ? 0.0f : (l > 120.0f ? 120.0f : l);
+        r.hard_clip_ratio = t[4] / nn;
+        r.near_clip_ratio = t[5] / nn;
+      }
+      // smoothSignalLevel (signal_level.cpp:206-214)
+      float *sm = a.sig_smooth + 2 * (size_t)c;
+      if (sm[1] == 0.0f) {
+        sm[0] = r.level120;
+        sm[1] = 1.0f;
+      } else {
+        const float alpha = (r.level120 > sm[0]) ? 0.42f : 0.18f;
+        sm[0] += (r.level120 - sm[0]) * alpha;
+      }
+      r.level120_smoothed = sm[0];
+      a.sig_out[c] = r;
+    }
+  }
 }
 
 /* ================================================================== */
@@ -1422,9 +1516,6 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     s.rebuild = 0;
   }
   int ng = 0;
-  // wave-wide max sample count
-  int nmax = count;
-  for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d));
   const float fscale = D->rds_fir_scale;
   const float agc_bw = D->agc_bw;
   const float ss_b0 = D->ss_b0, ss_a1 = D->ss_a1, ss_adj = D->ss_rate_adj;
@@ -1433,158 +1524,245 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   const float dphi_psk = (float)(3.14159265358979323846 * (1.0 - 1.0 / 2));
   const uint32_t ring0 = s.ring_pos;
 
-  for (int n0 = 0; n0 < nmax; n0 += 64) {
+  // one mixed sample into the 11 streaming partial sums (reference order)
+  auto acc_add = [&](float mr, float mi, int t, const float *tp, int tstride) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC; ++i) {
+      const float h = tp[i * tstride];
+      const float pr = h * mr, pi = h * mi;
+      s.acc_re[i] = s.acc_re[i] + pr;
+      s.acc_im[i] = s.acc_im[i] + pi;
+    }
+    if (t >= count - FMX_RDS_RING) {
+      const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
+      ring[2 * idx] = mr;
+      ring[2 * idx + 1] = mi;
+    }
+  };
+  auto mix_acc = [&](float x, int t, const float *tp, int tstride) __attribute__((always_inline)) {
+    float sn, cs;
+    sincosf(-s.phase0, &sn, &cs);
+    acc_add(x * cs, x * sn, t, tp, tstride);
+  };
+  // NCO step + quad-phase wrapper (liquid_wrappers.cpp:271-312)
+  auto nco_step = [&]() __attribute__((always_inline)) {
+    s.theta += s.dtheta;
+    const float now = d_nco_phase(s.theta);
+    float delta = now - s.prev_f0;
+    if (delta > kPiF) delta = delta - 2.f * kPiF;
+    else if (delta < -kPiF) delta = delta + 2.f * kPiF;
+    s.prev_f0 = now;
+    const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
+    float ph = s.phase0 + scaled;
+    if (ph > kPiF) ph = ph - 2.f * kPiF;
+    else if (ph < -kPiF) ph = ph + 2.f * kPiF;
+    s.phase0 = ph;
+    s.sample_since_reset++;
+  };
+  // FIR output (every 24th sample) -> AGC -> symsync -> PSK2 PLL -> bits
+  auto fir_output = [&]() __attribute__((always_inline)) {
+    const float fr = s.acc_re[0] * fscale, fi = s.acc_im[0] * fscale;
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC - 1; ++i) {
+      s.acc_re[i] = s.acc_re[i + 1];
+      s.acc_im[i] = s.acc_im[i + 1];
+    }
+    s.acc_re[FMX_RDS_NACC - 1] = 0.0f;
+    s.acc_im[FMX_RDS_NACC - 1] = 0.0f;
+    const float yr = fr * s.agc_g, yi = fi * s.agc_g;
+    const float y2 = yr * yr + yi * yi;
+    s.agc_y2p = (float)((1.0 - (double)agc_bw) * (double)s.agc_y2p + (double)(agc_bw * y2));
+    if (s.agc_y2p > 1e-6f) s.agc_g *= expf(-0.5f * agc_bw * logf(s.agc_y2p));
+    if (s.agc_g > 1e6f) s.agc_g = 1e6f;
+    // ---- symsync ----
+#pragma unroll
+    for (int m = 0; m < FMX_SS_SUB - 1; ++m) {
+      s.ss_win_re[m] = s.ss_win_re[m + 1];
+      s.ss_win_im[m] = s.ss_win_im[m + 1];
+    }
+    s.ss_win_re[FMX_SS_SUB - 1] = yr;
+    s.ss_win_im[FMX_SS_SUB - 1] = yi;
+    if (s.ss_mf_valid < FMX_SS_SUB) s.ss_mf_valid++;
+    int ns = 0;
+    float symr = 0.0f, symi = 0.0f;
+    while (s.ss_b < FMX_NPFB && ns < 16) {
+      const float *hm = L.mf + s.ss_b * FMX_SS_SUB;
+      float ar = 0.0f, ai = 0.0f;
+      const int first = FMX_SS_SUB - s.ss_mf_valid;
+#pragma unroll
+      for (int m = 0; m < FMX_SS_SUB; ++m) {
+        const float h = hm[FMX_SS_SUB - 1 - m];
+        const float wr = (m >= first) ? s.ss_win_re[m] : 0.0f;
+        const float wi = (m >= first) ? s.ss_win_im[m] : 0.0f;
+        const float pr = h * wr, pi = h * wi;
+        ar = ar + pr;
+        ai = ai + pi;
+      }
+      if (ns == 0) {
+        symr = ar / 3.0f;
+        symi = ai / 3.0f;
+      }
+      if (s.ss_decim == 1) {
+        s.ss_decim = 0;
+        const float *hd = L.dmf + s.ss_b * FMX_SS_SUB;
+        float dr = 0.0f, di = 0.0f;
+#pragma unroll
+        for (int m = 0; m < FMX_SS_SUB; ++m) {
+          const float h = hd[FMX_SS_SUB - 1 - m];
+          const float pr = h * s.ss_win_re[m], pi = h * s.ss_win_im[m];
+          dr = dr + pr;
+          di = di + pi;
+        }
+        float q = ar * dr + ai * di;
+        if (q > 1.0f) q = 1.0f;
+        else if (q < -1.0f) q = -1.0f;
+        const float t1 = ss_a1 * s.ss_v1;
+        const float v0 = q - t1;
+        s.ss_q_hat = ss_b0 * v0;
+        s.ss_v1 = v0;
+        s.ss_rate += ss_adj * s.ss_q_hat;
+        s.ss_del = s.ss_rate + s.ss_q_hat;
+      }
+      s.ss_decim++;
+      s.ss_tau += s.ss_del;
+      s.ss_b = (int)roundf(s.ss_tau * (float)FMX_NPFB);
+      ns++;
+    }
+    s.ss_tau -= 1.0f;
+    s.ss_b -= FMX_NPFB;
+    if (ns == 1) {
+      // ---- PSK2 modem phase error -> NCO PLL ----
+      float th = atan2f(symi, symr) - dphi_psk;
+      if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
+      const bool s1 = th > 0.0f;
+      const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
+      float pe = symi * xr - symr * xi;
+      pe = d_clamp(pe, -kPiF, kPiF);
+      const float dphi = pe * 12.0f;
+      s.dtheta += d_nco_constrain(dphi * alpha);
+      s.theta += d_nco_constrain(dphi * beta);
+      // ---- biphase + delta ----
+      const float bir = (symr - s.bi_prev_re) * 0.5f;
+      const int val = bir >= 0.0f;
+      const bool has = (s.bi_clock % 2u) == s.bi_polarity;
+      s.bi_prev_re = symr;
+      s.bi_prev_im = symi;
+      if ((s.bi_clock & 1u) == 0) s.bi_even += fabsf(bir);
+      else s.bi_odd += fabsf(bir);
+      s.bi_clock++;
+      if (s.bi_clock == 128u) {
+        if (s.bi_even > s.bi_odd) s.bi_polarity = 0;
+        else if (s.bi_odd > s.bi_even) s.bi_polarity = 1;
+        s.bi_even = 0.0f;
+        s.bi_odd = 0.0f;
+        s.bi_clock = 0;
+      }
+      if (has) {
+        const int bit = (val != s.delta_prev) ? 1 : 0;
+        s.delta_prev = val;
+        rds_push_bit(s, bit, L, a, c, ng);
+      }
+    }
+  };
+  // Inputs are staged in LDS in tiles of 64 samples x 64 channels with
+  // coalesced loads; all lanes sit at the same sample index t.
+  int nmax = count, cmin = act ? count : 0x7fffffff;
+  for (int d = 32; d >= 1; d >>= 1) {
+    nmax = max(nmax, __shfl_xor(nmax, d));
+    cmin = min(cmin, __shfl_xor(cmin, d));
+  }
+  int tb = -1 << 30;  // sample index of L.tin[.][0]
+  auto tile_at = [&](int t0) __attribute__((always_inline)) {
+    __syncthreads();
     for (int idx = lane; idx < 64 * 64; idx += 64) {
       const int row = idx >> 6, col = idx & 63;
       const int ch = c0 + row;
       if (ch < a.C) {
         const int cn = a.in_count[ch];
-        L.tin[row][col] = (n0 + col < cn) ? a.in[(size_t)ch * a.in_stride + n0 + col] : 0.0f;
+        L.tin[row][col] = (t0 + col < cn) ? a.in[(size_t)ch * a.in_stride + t0 + col] : 0.0f;
       }
     }
     __syncthreads();
-    const int kend = act ? min(64, count - n0) : 0;
-    for (int k = 0; k < kend; ++k) {
-      const float x = L.tin[lane][k];
-      float sn, cs;
-      sincosf(-s.phase0, &sn, &cs);
-      const float mr = x * cs, mi = x * sn;
+    tb = t0;
+  };
+  // one sample for every lane that still has input: own tap row from LDS
+  auto step_one = [&](int t) __attribute__((always_inline)) {
+    if (t >= tb + 64 || t < tb) tile_at(t);
+    if (act && t < count) {
       const int j = (int)(s.sample_since_reset % FMX_RDS_DECIM);
       const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
-#pragma unroll
-      for (int i = 0; i < FMX_RDS_NACC; ++i) {
-        const float h = L.taps[jp][i];
-        const float pr = h * mr, pi = h * mi;
-        s.acc_re[i] = s.acc_re[i] + pr;
-        s.acc_im[i] = s.acc_im[i] + pi;
-      }
-      const int t = n0 + k;
-      if (t >= count - FMX_RDS_RING) {
-        const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
-        ring[2 * idx] = mr;
-        ring[2 * idx + 1] = mi;
-      }
-      if (j == 0) {
-        // ---- FIR output, AGC ----
-        const float fr = s.acc_re[0] * fscale, fi = s.acc_im[0] * fscale;
-#pragma unroll
-        for (int i = 0; i < FMX_RDS_NACC - 1; ++i) {
-          s.acc_re[i] = s.acc_re[i + 1];
-          s.acc_im[i] = s.acc_im[i + 1];
-        }
-        s.acc_re[FMX_RDS_NACC - 1] = 0.0f;
-        s.acc_im[FMX_RDS_NACC - 1] = 0.0f;
-        const float yr = fr * s.agc_g, yi = fi * s.agc_g;
-        const float y2 = yr * yr + yi * yi;
-        s.agc_y2p = (float)((1.0 - (double)agc_bw) * (double)s.agc_y2p + (double)(agc_bw * y2));
-        if (s.agc_y2p > 1e-6f) s.agc_g *= expf(-0.5f * agc_bw * logf(s.agc_y2p));
-        if (s.agc_g > 1e6f) s.agc_g = 1e6f;
-        // ---- symsync ----
-#pragma unroll
-        for (int m = 0; m < FMX_SS_SUB - 1; ++m) {
-          s.ss_win_re[m] = s.ss_win_re[m + 1];
-          s.ss_win_im[m] = s.ss_win_im[m + 1];
-        }
-        s.ss_win_re[FMX_SS_SUB - 1] = yr;
-        s.ss_win_im[FMX_SS_SUB - 1] = yi;
-        if (s.ss_mf_valid < FMX_SS_SUB) s.ss_mf_valid++;
-        int ns = 0;
-        float symr = 0.0f, symi = 0.0f;
-        while (s.ss_b < FMX_NPFB && ns < 16) {
-          const float *hm = L.mf + s.ss_b * FMX_SS_SUB;
-          float ar = 0.0f, ai = 0.0f;
-          const int first = FMX_SS_SUB - s.ss_mf_valid;
-#pragma unroll
-          for (int m = 0; m < FMX_SS_SUB; ++m) {
-            const float h = hm[FMX_SS_SUB - 1 - m];
-            const float wr = (m >= first) ? s.ss_win_re[m] : 0.0f;
-            const float wi = (m >= first) ? s.ss_win_im[m] : 0.0f;
-            const float pr = h * wr, pi = h * wi;
-            ar = ar + pr;
-            ai = ai + pi;
-          }
-          if (ns == 0) {
-            symr = ar / 3.0f;
-            symi = ai / 3.0f;
-          }
-          if (s.ss_decim == 1) {
-            s.ss_decim = 0;
-            const float *hd = L.dmf + s.ss_b * FMX_SS_SUB;
-            float dr = 0.0f, di = 0.0f;
-#pragma unroll
-            for (int m = 0; m < FMX_SS_SUB; ++m) {
-              const float h = hd[FMX_SS_SUB - 1 - m];
-              const float pr = h * s.ss_win_re[m], pi = h * s.ss_win_im[m];
-              dr = dr + pr;
-              di = di + pi;
-            }
-            float q = ar * dr + ai * di;
-            if (q > 1.0f) q = 1.0f;
-            else if (q < -1.0f) q = -1.0f;
-            const float t1 = ss_a1 * s.ss_v1;
-            const float v0 = q - t1;
-            s.ss_q_hat = ss_b0 * v0;
-            s.ss_v1 = v0;
-            s.ss_rate += ss_adj * s.ss_q_hat;
-            s.ss_del = s.ss_rate + s.ss_q_hat;
-          }
-          s.ss_decim++;
-          s.ss_tau += s.ss_del;
-          s.ss_b = (int)roundf(s.ss_tau * (float)FMX_NPFB);
-          ns++;
-        }
-        s.ss_tau -= 1.0f;
-        s.ss_b -= FMX_NPFB;
-        if (ns == 1) {
-          // ---- PSK2 modem phase error -> NCO PLL ----
-          float th = atan2f(symi, symr) - dphi_psk;
-          if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
-          const bool s1 = th > 0.0f;
-          const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
-          float pe = symi * xr - symr * xi;
-          pe = d_clamp(pe, -kPiF, kPiF);
-          const float dphi = pe * 12.0f;
-          s.dtheta += d_nco_constrain(dphi * alpha);
-          s.theta += d_nco_constrain(dphi * beta);
-          // ---- biphase + delta ----
-          const float bir = (symr - s.bi_prev_re) * 0.5f;
-          const int val = bir >= 0.0f;
-          const bool has = (s.bi_clock % 2u) == s.bi_polarity;
-          s.bi_prev_re = symr;
-          s.bi_prev_im = symi;
-          if ((s.bi_clock & 1u) == 0) s.bi_even += fabsf(bir);
-          else s.bi_odd += fabsf(bir);
-          s.bi_clock++;
-          if (s.bi_clock == 128u) {
-            if (s.bi_even > s.bi_odd) s.bi_polarity = 0;
-            else if (s.bi_odd > s.bi_even) s.bi_polarity = 1;
-            s.bi_even = 0.0f;
-            s.bi_odd = 0.0f;
-            s.bi_clock = 0;
-          }
-          if (has) {
-            const int bit = (val != s.delta_prev) ? 1 : 0;
-            s.delta_prev = val;
-            rds_push_bit(s, bit, L, a, c, ng);
-          }
-        }
-      }
-      // ---- NCO step + quad-phase wrapper ----
-      s.theta += s.dtheta;
-      const float now = d_nco_phase(s.theta);
-      float delta = now - s.prev_f0;
-      if (delta > kPiF) delta = delta - 2.f * kPiF;
-      else if (delta < -kPiF) delta = delta + 2.f * kPiF;
-      s.prev_f0 = now;
-      const float scaled = delta * 57000.f / 57000.f;
-      float ph = s.phase0 + scaled;
-      if (ph > kPiF) ph = ph - 2.f * kPiF;
-      else if (ph < -kPiF) ph = ph + 2.f * kPiF;
-      s.phase0 = ph;
-      s.sample_since_reset++;
+      mix_acc(L.tin[lane][t - tb], t, &L.taps[jp][0], 1);
+      if (j == 0) fir_output();
+      nco_step();
     }
-    __syncthreads();
+  };
+  const uint32_t j_mine = act ? (s.sample_since_reset % FMX_RDS_DECIM) : 0xFFFFFFFFu;
+  uint32_t j_first = j_mine;
+  for (int d = 32; d >= 1; d >>= 1) j_first = min(j_first, (uint32_t)__shfl_xor((int)j_first, d));
+  const bool uniform_j = __ballot(act && j_mine != j_first) == 0;
+  int t = 0;
+  if (uniform_j) {
+    // Every lane shares the decimation phase (the normal case: channels of a
+    // wave see identical resampler timing unless reset one by one).  Step to
+    // the first period start (j == 1), then run chunks of 8 samples
+    // (3 per period, the FIR output at the end of the third): the NCO phases
+    // of a chunk (no PLL update inside) are computed with the 8 theta values
+    // in parallel and only the wrapped phase sum serial, then 8 sincos in
+    // parallel, then the partial sums in sample order.  Same arithmetic and
+    // order as step_one; only the schedule differs.
+    while (t < nmax && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) != 1u) step_one(t++);
+    constexpr int U = 8;
+    while (t + U <= cmin) {
+      if (t + U > tb + 64 || t < tb) tile_at(t);
+      const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;  // 1, 9 or 17
+      const bool out_end = (j0 == 17u);
+      float ph[U];
+      ph[0] = s.phase0;
+      {
+        uint32_t th[U - 1];
+        float nw[U - 1];
+#pragma unroll
+        for (int v = 0; v < U - 1; ++v) {
+          th[v] = s.theta + (uint32_t)(v + 1) * s.dtheta;
+          nw[v] = d_nco_phase(th[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < U - 1; ++v) {
+          float delta = nw[v] - (v == 0 ? s.prev_f0 : nw[v - 1]);
+          if (delta > kPiF) delta = delta - 2.f * kPiF;
+          else if (delta < -kPiF) delta = delta + 2.f * kPiF;
+          const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
+          float p2 = ph[v] + scaled;
+          if (p2 > kPiF) p2 = p2 - 2.f * kPiF;
+          else if (p2 < -kPiF) p2 = p2 + 2.f * kPiF;
+          ph[v + 1] = p2;
+        }
+        s.theta = th[U - 2];
+        s.prev_f0 = nw[U - 2];
+        s.phase0 = ph[U - 1];
+        s.sample_since_reset += U - 1;
+      }
+      float mr[U], mi[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float sn, cs;
+        sincosf(-ph[u], &sn, &cs);
+        const float x = L.tin[lane][t + u - tb];
+        mr[u] = x * cs;
+        mi[u] = x * sn;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t j = j0 + (uint32_t)u;  // 1..24
+        const int jp = (j == FMX_RDS_DECIM) ? 0 : FMX_RDS_DECIM - (int)j;
+        acc_add(mr[u], mi[u], t + u, &L.taps[jp][0], 1);
+      }
+      if (out_end) fir_output();
+      nco_step();  // the chunk's last sample, after a PLL update if any
+      t += U;
+    }
   }
+  while (t < nmax) step_one(t++);
   if (!act) return;
   s.ring_pos = ring0 + (uint32_t)count;
   a.st[c] = s;

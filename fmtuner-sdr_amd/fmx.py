@@ -34,13 +34,20 @@ class RdsGroup(C.Structure):
                 ("block_index", C.c_uint32)]
 
 
+class SignalLevel(C.Structure):
+    _fields_ = [("level120", C.c_float), ("level120_smoothed", C.c_float), ("dbfs", C.c_double),
+                ("compensated_dbfs", C.c_double), ("hard_clip_ratio", C.c_double),
+                ("near_clip_ratio", C.c_double)]
+
+
 class BlockOut(C.Structure):
     _fields_ = [("d_mpx", C.c_void_p), ("mpx_stride", C.c_int),
                 ("d_pcm_l", C.c_void_p), ("d_pcm_r", C.c_void_p),
                 ("pcm_stride", C.c_int), ("d_pcm_count", C.c_void_p),
                 ("d_stereo", C.c_void_p), ("d_pilot_tenths", C.c_void_p),
                 ("d_clip_ratio", C.c_void_p), ("d_groups", C.c_void_p),
-                ("groups_stride", C.c_int), ("d_group_count", C.c_void_p)]
+                ("groups_stride", C.c_int), ("d_group_count", C.c_void_p),
+                ("d_signal", C.c_void_p)]
 
 
 class SynthConfig(C.Structure):
@@ -71,6 +78,7 @@ def lib():
         "fmx_num_channels": (i, [vp]),
         "fmx_reset": (i, [vp, i]),
         "fmx_set_param": (i, [vp, i, i, i]),
+        "fmx_set_signal_params": (i, [vp, i, i, C.c_double, C.c_double, C.c_double, C.c_double]),
         "fmx_process_block": (i, [vp, vp, sz, i, C.POINTER(BlockOut)]),
         "fmx_decimate": (i, [vp, vp, sz, i, vp, i]),
         "fmx_demod": (i, [vp, vp, i, i, vp, i, vp, i, vp]),
@@ -156,6 +164,11 @@ class Handle:
     def set_param(self, key, value, channel=-1):
         k = PARAM[key] if isinstance(key, str) else key
         self._ck(self.L.fmx_set_param(self.h, channel, k, value), "fmx_set_param")
+
+    def set_signal_params(self, applied_gain_db=0, gain_comp_factor=0.5, bias_db=-4.0, floor_dbfs=-55.0,
+                          ceil_dbfs=-19.0, channel=-1):
+        self._ck(self.L.fmx_set_signal_params(self.h, channel, applied_gain_db, gain_comp_factor, bias_db,
+                                              floor_dbfs, ceil_dbfs), "fmx_set_signal_params")
 
     def process_block(self, d_iq, iq_stride, n, out):
         self._ck(self.L.fmx_process_block(self.h, C.c_void_p(d_iq), iq_stride, n, C.byref(out)),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 1
+#define FMX_ABI_VERSION 2
 
 enum {
   FMX_OK = 0,
@@ -80,6 +80,18 @@ typedef struct {
   uint32_t block_index; /* fmx_process_block call that emitted it */
 } fmx_rds_group;
 
+/* RF-domain level of the raw u8 IQ of one call, as computeSignalLevel
+ * (src/signal_level.cpp:145-204) + smoothSignalLevel (:206-214) of the
+ * reference's per-read path (main.cpp:1166-1174). */
+typedef struct {
+  float level120;          /* SignalLevelResult::level120                     */
+  float level120_smoothed; /* smoothSignalLevel(level120, per-channel state)  */
+  double dbfs;
+  double compensated_dbfs;
+  double hard_clip_ratio;
+  double near_clip_ratio;
+} fmx_signal_level;
+
 /* Device output buffers of fmx_process_block (all optional except where
  * noted; pass NULL to skip).  Strides are in elements. */
 typedef struct {
@@ -95,6 +107,7 @@ typedef struct {
   fmx_rds_group *d_groups; /* [C][groups_stride]                              */
   int groups_stride;
   int *d_group_count;      /* [C]                                             */
+  fmx_signal_level *d_signal; /* [C] RF level of this call's IQ (u8 input)    */
 } fmx_block_out;
 
 /* ---- lifetime ---- */
@@ -122,6 +135,12 @@ enum {
   FMX_PARAM_BANDWIDTH_MODE = 8 /* FMDemod::setBandwidthMode (TEF table)        */
 };
 int fmx_set_param(void *handle, int channel, int key, int value);
+/* computeSignalLevel's arguments (main.cpp:1166-1170): applied tuner gain
+ * (dB), gain compensation factor (kSignalGainCompFactor 0.5, main.cpp:513),
+ * config sdr.signal_bias_db / signal_floor_dbfs / signal_ceil_dbfs
+ * (config.h:27-29; defaults -4 / -55 / -19).  channel = -1 = all. */
+int fmx_set_signal_params(void *handle, int channel, int applied_gain_db, double gain_comp_factor,
+                          double bias_db, double floor_dbfs, double ceil_dbfs);
 
 /* One reference block for every channel.  d_iq: [C][iq_stride] bytes, each
  * row holding 2*n*M interleaved u8 I/Q (M = iq_rate / dsp_rate); n <= block.

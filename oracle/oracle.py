@@ -205,3 +205,67 @@ def run_many(cfg, iq, n_blocks, threads):
     secs = lib().oracle_run_many(C.byref(cfg), iq.shape[0], iq.ctypes.data, n_blocks,
                                  threads, C.byref(chk))
     return secs, chk.value
+
+
+# ---- RF signal level (restates src/signal_level.cpp:145-214) ----
+def signal_level(iq, gain_db=0, comp=0.5, bias=-4.0, floor_db=-55.0, ceil_db=-19.0):
+    """computeSignalLevel on interleaved u8 IQ (numpy restatement, sequential
+    double accumulation as the reference's scalar loop)."""
+    iq = np.ascontiguousarray(iq, dtype=np.uint8)
+    n = iq.size // 2
+    out = dict(level120=0.0, dbfs=-120.0, compensated_dbfs=-120.0, hard_clip_ratio=0.0, near_clip_ratio=0.0)
+    if n == 0:
+        return out
+    i = iq[0::2].astype(np.float64)
+    q = iq[1::2].astype(np.float64)
+    inorm = (i - 127.5) * (1.0 / 127.5)
+    qnorm = (q - 127.5) * (1.0 / 127.5)
+    # sequential sums (np.cumsum adds left to right in double)
+    sumI = float(np.cumsum(inorm)[-1])
+    sumQ = float(np.cumsum(qnorm)[-1])
+    sumII = float(np.cumsum(inorm * inorm)[-1])
+    sumQQ = float(np.cumsum(qnorm * qnorm)[-1])
+    ib, qb = iq[0::2], iq[1::2]
+    hard = int(np.count_nonzero((ib <= 1) | (ib >= 254) | (qb <= 1) | (qb >= 254))) * 2
+    near = int(np.count_nonzero((ib <= 8) | (ib >= 247) | (qb <= 8) | (qb >= 247))) * 2
+    nn = float(n)
+    meanI, meanQ = sumI / nn, sumQ / nn
+    varI = max(0.0, (sumII / nn) - meanI * meanI)
+    varQ = max(0.0, (sumQQ / nn) - meanQ * meanQ)
+    rms = np.sqrt(max(1e-15, 0.5 * (varI + varQ)))
+    dbfs = 20.0 * np.log10(rms + 1e-12)
+    comp_db = dbfs - (float(gain_db) * comp) + bias
+    safe_ceil = max(ceil_db, floor_db + 1.0)
+    norm = (comp_db - floor_db) / (safe_ceil - floor_db)
+    out.update(level120=float(np.clip(np.float32(norm * 120.0), np.float32(0.0), np.float32(120.0))),
+               dbfs=float(dbfs), compensated_dbfs=float(comp_db), hard_clip_ratio=hard / (2.0 * nn),
+               near_clip_ratio=near / (2.0 * nn))
+    return out
+
+
+class SignalSmoother:
+    """smoothSignalLevel (signal_level.cpp:206-214), float arithmetic."""
+
+    def __init__(self):
+        self.initialized = False
+        self.value = np.float32(0.0)
+
+    def __call__(self, x):
+        x = np.float32(x)
+        if not self.initialized:
+            self.value = x
+            self.initialized = True
+            return float(self.value)
+        alpha = np.float32(0.42) if x > self.value else np.float32(0.18)
+        self.value = np.float32(self.value + np.float32(np.float32(x - self.value) * alpha))
+        return float(self.value)
+
+
+def ref_signal_level(iq, gain_db=0, comp=0.5, bias=-4.0, floor_db=-55.0, ceil_db=-19.0):
+    """The reference's own computeSignalLevel (oracle/_ref)."""
+    R = ref()
+    iq = np.ascontiguousarray(iq, dtype=np.uint8)
+    out = (C.c_double * 5)()
+    R.ref_signal_level(iq.ctypes.data if iq.size else None, iq.size // 2, gain_db, comp, bias, floor_db, ceil_db, out)
+    return dict(level120=out[0], dbfs=out[1], compensated_dbfs=out[2], hard_clip_ratio=out[3],
+                near_clip_ratio=out[4])
