@@ -232,6 +232,43 @@ __device__ __forceinline__ float resamp_out(const float *__restrict__ hb, int pa
   return w0 + w1;
 }
 
+// Block-wide (256 threads) exclusive scan of affine maps v -> A v + B with
+// two B lanes (left/right sharing A), applied to the carries (cl, cr):
+// returns v_{k-1} for element k = tid.  `ws` is 3*4 floats of LDS.
+__device__ __forceinline__ void block_affine_prev(float A, float BL, float BR, float cl, float cr, float *ws,
+                                                  float &pl, float &pr) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float pA = __shfl_up(A, d), pL = __shfl_up(BL, d), pR = __shfl_up(BR, d);
+    if (lane >= d) {
+      BL = A * pL + BL;
+      BR = A * pR + BR;
+      A = A * pA;
+    }
+  }
+  if (lane == 63) {
+    ws[wave] = A;
+    ws[4 + wave] = BL;
+    ws[8 + wave] = BR;
+  }
+  float eA = __shfl_up(A, 1), eL = __shfl_up(BL, 1), eR = __shfl_up(BR, 1);
+  if (lane == 0) {
+    eA = 1.0f;
+    eL = 0.0f;
+    eR = 0.0f;
+  }
+  __syncthreads();
+  float vl = cl, vr = cr;
+  for (int w = 0; w < wave; ++w) {
+    vl = ws[w] * vl + ws[4 + w];
+    vr = ws[w] * vr + ws[8 + w];
+  }
+  pl = eA * vl + eL;
+  pr = eA * vr + eR;
+  __syncthreads();  // ws reusable
+}
+
 __device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i) {
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -1116,6 +1153,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   __shared__ float lf[AU_RHALO + AU_T], rf[AU_RHALO + AU_T];
   __shared__ float ol[AU_MAXOUT], orr[AU_MAXOUT];
   __shared__ int s_eb, s_ee, s_count;
+  __shared__ float s_iir[4], s_ws[12];  // [de_L, de_R, dc_L, dc_R]; scan scratch
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
@@ -1149,16 +1187,14 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     rf[h] = mono ? 0.0f : win[32 + h];
   }
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
-  // serial IIR state: [de_v, dc_v] per side
-  float de_v = 0.0f, dc_v = 0.0f;
-  if (af && (tid == 0 || tid == 64)) {
-    const int side = (tid == 0) ? 0 : 1;
+  if (af && tid == 0) {
     if (mono) {
-      de_v = iir[0];
-      dc_v = iir[1];
+      s_iir[0] = iir[0];
+      s_iir[1] = 0.0f;
+      s_iir[2] = iir[1];
+      s_iir[3] = 0.0f;
     } else {
-      de_v = iir[side];
-      dc_v = iir[2 + side];
+      for (int k = 0; k < 4; ++k) s_iir[k] = iir[k];
     }
   }
   const FmxSched *sched = nullptr;
@@ -1220,31 +1256,44 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         }
       }
       __syncthreads();
-      // serial de-emphasis + DC block (DF-II), one thread per side
-      if (tid == 0 || (tid == 64 && !mono)) {
-        const bool left = (tid == 0);
-        const float *src = left ? ol : orr;
-        float *dst = left ? a.out_l : a.out_r;
-        const int base = s_count;
-        for (int k = 0; k < ee - eb; ++k) {
-          float x = src[k];
-          if (de_on) {
-            const float t = de_a1 * de_v;
-            const float v0 = x - t;
-            de_v = v0;
-            x = dalpha * v0;
+      // de-emphasis + DC block (DF-II, af_post_processor.cpp:66-75 /
+      // fm_demod.cpp:218-224): each IIR as a block affine scan for the
+      // state before output k, then output k in the reference's op order.
+      {
+        const int m = ee - eb;  // <= AU_MAXOUT
+        const bool on = tid < m;
+        float xl = on ? ol[tid] : 0.0f;
+        float xr = (on && !mono) ? orr[tid] : 0.0f;
+        if (de_on) {
+          float pl, pr;
+          block_affine_prev(on ? -de_a1 : 1.0f, xl, xr, s_iir[0], s_iir[1], s_ws, pl, pr);
+          const float vl = xl - de_a1 * pl, vr = xr - de_a1 * pr;
+          if (tid == m - 1) {
+            s_iir[0] = vl;
+            s_iir[1] = vr;
           }
-          const float t2 = dc_a1 * dc_v;
-          const float v0 = x - t2;
-          x = v0 - dc_v;
-          dc_v = v0;
-          if (pipe_mono) x = x * 0.5f;
-          if (a.clamp) x = d_clamp(x, -1.0f, 1.0f);
-          const int o = base + k;
-          if (o < a.cap) {
-            dst[(size_t)c * a.out_stride + o] = x;
-            if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = x;
-          }
+          xl = dalpha * vl;
+          xr = dalpha * vr;
+        }
+        float ql, qr;
+        block_affine_prev(on ? -dc_a1 : 1.0f, xl, xr, s_iir[2], s_iir[3], s_ws, ql, qr);
+        const float vl = xl - dc_a1 * ql, vr = xr - dc_a1 * qr;
+        float yl = vl - ql, yr = vr - qr;
+        __syncthreads();
+        if (tid == m - 1) {
+          s_iir[2] = vl;
+          s_iir[3] = vr;
+        }
+        if (pipe_mono) yl = yl * 0.5f;
+        if (a.clamp) {
+          yl = d_clamp(yl, -1.0f, 1.0f);
+          yr = d_clamp(yr, -1.0f, 1.0f);
+        }
+        const int o = s_count + tid;
+        if (on && o < a.cap) {
+          a.out_l[(size_t)c * a.out_stride + o] = yl;
+          if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = yl;
+          else if (!mono) a.out_r[(size_t)c * a.out_stride + o] = yr;
         }
       }
       __syncthreads();
@@ -1286,14 +1335,12 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       win[h] = lf[h];
       if (!mono) win[32 + h] = rf[h];
     }
-    if (tid == 0 || (tid == 64 && !mono)) {
-      const int side = (tid == 0) ? 0 : 1;
+    if (tid == 0) {
       if (mono) {
-        iir[0] = de_v;
-        iir[1] = dc_v;
+        iir[0] = s_iir[0];
+        iir[1] = s_iir[2];
       } else {
-        iir[side] = de_v;
-        iir[2 + side] = dc_v;
+        for (int k = 0; k < 4; ++k) iir[k] = s_iir[k];
       }
     }
     if (tid == 0 && a.out_count) a.out_count[c] = s_count < a.cap ? s_count : a.cap;
