@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -79,6 +80,7 @@ struct Handle {
   double *dsig = nullptr;
   float *sig_smooth = nullptr;
   bool sig_dirty = true;
+  unsigned long long *dbg = nullptr;  // frontend stage clocks when FMX_STAMPS=1
   float2_t *iq_hist = nullptr;
   float *st_hist = nullptr, *lr_hist = nullptr, *af_win = nullptr, *af_iir = nullptr;
   float *mono_win = nullptr, *mono_iir = nullptr, *rds_hist = nullptr, *ring = nullptr;
@@ -472,6 +474,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->fd_prev, C * 2)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->dsig, C * 4)) != FMX_OK) return rc;
+  if (const char *e = std::getenv("FMX_STAMPS"); e && e[0] == '1') {
+    if ((rc = dalloc(h, &h->dbg, 8)) != FMX_OK) return rc;
+    HIP_TRY(hipMemset(h->dbg, 0, 8 * sizeof(unsigned long long)));
+  }
   if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
   HIP_TRY(hipMemset(h->sig_smooth, 0, sizeof(float) * 2 * C));
   h->hsig.resize(static_cast<size_t>(C) * 4);
@@ -540,6 +546,7 @@ static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   a.rds_hist = h->rds_hist;
   a.clip_out = h->clip;
   a.sig_par = h->dsig;
+  a.dbg = h->dbg;
   a.sig_smooth = h->sig_smooth;
   a.rds_count = h->rds_count[buf];
   a.rds_sched = h->t_rds.d_sched[h->t_rds.cur];
@@ -845,6 +852,16 @@ int fmx_set_param(void *handle, int channel, int key, int value) {
       default: h->err = "unknown parameter key"; return FMX_E_INVALID;
     }
   }
+  return FMX_OK;
+}
+
+/* diagnostic: frontend stage clocks (s_memtime ticks summed over
+ * workgroups) when the handle was created with FMX_STAMPS=1 */
+int fmx_debug_stamps(void *handle, unsigned long long *out, int n) {
+  Handle *h = H(handle);
+  if (!h || !h->dbg || n < 8) return FMX_E_INVALID;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, h->dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return FMX_OK;
 }
 

@@ -316,7 +316,15 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
   for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
     for (int k = 0; k < d->iq_len[i]; ++k) d->iq_pad[i][k + 5] = d->iq_taps[i][k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
+  for (int k = 0; k + 1 < FMX_PILOT_MAX + FMX_PAD; ++k) {
+    d->pilot_pair[k][0] = d->pilot_pad[k];
+    d->pilot_pair[k][1] = d->pilot_pad[k + 1];
+  }
   for (int k = 0; k < FMX_LR_LEN; ++k) d->lr_pad[k + 5] = d->lr_taps[k];
+  for (int k = 0; k + 1 < FMX_LR_LEN + FMX_PAD; ++k) {
+    d->lr_pair[k][0] = d->lr_pad[k];
+    d->lr_pair[k][1] = d->lr_pad[k + 1];
+  }
   if (ex) {
     ex->proto_af = proto_af;
     ex->proto_rds = proto_rds;

@@ -53,9 +53,11 @@ typedef struct {
   int pilot_len, delay_len; // delay_len = delaySamples + 1 (ring size)
   float pilot_taps[FMX_PILOT_MAX];
   float pilot_pad[FMX_PILOT_MAX + FMX_PAD];
+  float pilot_pair[FMX_PILOT_MAX + FMX_PAD][2] __attribute__((aligned(8))); // {pad[k], pad[k+1]}: packed-FMA tap pairs
   float lr_scale;
   float lr_taps[FMX_LR_LEN];
   float lr_pad[FMX_LR_LEN + FMX_PAD];
+  float lr_pair[FMX_LR_LEN + FMX_PAD][2] __attribute__((aligned(8)));
   float nominal, pll_min, pll_max, pll_alpha, pll_beta;
   uint32_t pll_dtheta0;
   float blend_attack[3], blend_release[3], gate[3];

@@ -58,6 +58,7 @@ struct FeArgs {
   fmx_signal_level *sig_out;  // [C] RF level (u8 inputs), may be null
   const double *sig_par;      // [C][4] gain*factor, bias, floor, ceil
   float *sig_smooth;          // [C][2] smoother value, initialized flag
+  unsigned long long *dbg;    // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
   // state

@@ -196,6 +196,29 @@ __device__ __forceinline__ void fir_r3(const float *x, int base, const float *__
   z[2] = a2;
 }
 
+// fir_r3 with the (y0, y1) pair on packed FP32 FMAs: hq[k] = {hp[k], hp[k+1]}.
+// Same FMA sequence per output as fir_r3, so bit-identical results.
+__device__ __forceinline__ void fir_r3p(const float *x, int base, const float *__restrict__ hp,
+                                        const float (*__restrict__ hq)[2], int P, float (&z)[3]) {
+  f32x2 a01 = {0.0f, 0.0f};
+  float a2 = 0.0f;
+#pragma unroll 1
+  for (int s = -(P - 1); s <= 2; s += 4) {
+    const float *h = hp + 5 - s;
+    const float(*h2)[2] = hq + 5 - s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = x[base + s + u];
+      const f32x2 hh = {h2[-u][0], h2[-u][1]};  // taps of y0, y1
+      a01 = __builtin_elementwise_fma(hh, f32x2{v, v}, a01);
+      a2 = fmaf(h[2 - u], v, a2);
+    }
+  }
+  z[0] = a01.x;
+  z[1] = a01.y;
+  z[2] = a2;
+}
+
 // Resampler output from a window accessor; reference dot order (oldest first)
 template <int SUB, typename Get>
 __device__ __forceinline__ float resamp_out(const float *__restrict__ hb, int packed, float mu, Get get) {
@@ -336,6 +359,21 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
   const bool want_sig = a.sig_out != nullptr && a.in_mode != FE_IN_CF && a.in_mode != FE_IN_MPX;
   SigAcc sig;
+  // diagnostic stage clock (thread 0's view, barrier waits included):
+  // compiled only with -DFMX_STAMPS (make STAMPS=1) and read through
+  // fmx_debug_stamps when the handle was created with FMX_STAMPS=1
+#ifdef FMX_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
+#define FE_STAMP(k)                                              \
+  if (a.dbg && tid == 0) {                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+    st_acc[k] += t_ - st_last;                                   \
+    st_last = t_;                                                \
+  }
+#else
+#define FE_STAMP(k)
+#endif
 
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -420,6 +458,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 
   for (int n0 = 0; n0 < n; n0 += FE_T) {
     const int cnt = min(FE_T, n - n0);
+    if (rds && tid == 0) sh->e_end = e_pos;  // raised by atomicMax in the RDS stage
+    FE_STAMP(7)
     // ================= baseband x[j] =================
     if constexpr (VEC && M > 1) {
 #pragma unroll
@@ -535,6 +575,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     __syncthreads();
 
     if (demod) {
+      FE_STAMP(0)
       // ================= DC blockers: affine scan =================
       // v_k = x_k - a1 * v_{k-1} (DF-II); y_k = v_k - v_{k-1}
       float A = 1.0f, BI = 0.0f, BQ = 0.0f;
@@ -601,6 +642,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         }
       }
       __syncthreads();
+      FE_STAMP(1)
       // ================= IQ FIR =================
       {
         float zr[3], zi[3];
@@ -628,6 +670,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         }
         __syncthreads();
       }
+      FE_STAMP(2)
       // ================= discriminator =================
       const float ref = D->fd_ref;
       for (int j = tid; j < cnt; j += 256) {
@@ -648,32 +691,48 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     }
     __syncthreads();
 
+    FE_STAMP(3)
+    // RDS resampler schedule entries of this chunk (<= FE_T of them, the
+    // rate ratio is < 1), fetched now so their latency hides behind the
+    // pilot FIR; the chunk's end index is found from them in parallel.
+    FmxSched en3[3];
+    if (rds) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = e_pos + tid + 256 * k;
+        en3[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
+      }
+    }
     // ================= 19 kHz pilot band-pass =================
     if (pilot) {
       float z[3];
-      fir_r3(mx, FMX_HIST + 3 * tid, D->pilot_pad, D->pilot_len, z);
+      fir_r3p(mx, FMX_HIST + 3 * tid, D->pilot_pad, D->pilot_pair, D->pilot_len, z);
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int j = 3 * tid + r;
         if (j < cnt) a.pilot_out[(size_t)c * a.pilot_stride + n0 + j] = z[r];
       }
     }
+    FE_STAMP(4)
     // ================= RDS resampler 240k -> 171k =================
     if (rds) {
-      if (tid == 0) {
-        sh->e_begin = e_pos;
-        sh->e_end = sched_lower_bound(sched, sched_n, n0 + cnt);
+      int last = -1;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = e_pos + tid + 256 * k;
+        if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
+          auto get = [&](int ii) -> float { return rb[32 + ii - n0]; };
+          a.rds_out[(size_t)c * a.rds_stride + e] =
+              resamp_out<FMX_RDS_RS_SUB>(D->rds_rs_h, en3[k].packed, en3[k].mu, get);
+          last = e;
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __syncthreads();
-      const int eb = sh->e_begin, ee = sh->e_end;
-      for (int e = eb + tid; e < ee; e += 256) {
-        const FmxSched en = sched[e];
-        auto get = [&](int ii) -> float { return rb[32 + ii - n0]; };
-        a.rds_out[(size_t)c * a.rds_stride + e] = resamp_out<FMX_RDS_RS_SUB>(D->rds_rs_h, en.packed, en.mu, get);
-      }
-      e_pos = ee;
+      if (last >= 0) atomicMax(&sh->e_end, last + 1);
     }
     __syncthreads();
+    if (rds) e_pos = sh->e_end;
+    FE_STAMP(5)
     // ================= carry halos to the next chunk =================
     {
       float2 cx = make_float2(0.0f, 0.0f);
@@ -750,6 +809,12 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
     if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = rb[tid];
     if (tid == 0) a.rds_count[c] = sched_n;
   }
+  FE_STAMP(6)
+#ifdef FMX_STAMPS
+  if (a.dbg && tid == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, st_acc[k]);
+#endif
+#undef FE_STAMP
   if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
     a.clip_out[c] = (n > 0) ? (float)sh->clip / (float)n : 0.0f;
   if (want_sig) {
@@ -1213,6 +1278,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   __syncthreads();
   for (int n0 = 0; n0 < n; n0 += AU_T) {
     const int cnt = min(AU_T, n - n0);
+    FmxSched en3[3];  // this chunk's resampler schedule entries (see k_frontend)
+    if (af) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = s_eb + tid + 256 * k;
+        en3[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
+      }
+      if (tid == 0) s_ee = s_eb;
+    }
     for (int j = tid; j < cnt; j += 256) {
       if (lrfir) {
         li[AU_HALO + j] = inl[n0 + j];
@@ -1225,8 +1299,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     __syncthreads();
     if (lrfir) {
       float zl[3], zr[3];
-      fir_r3(li, AU_HALO + 3 * tid, D->lr_pad, FMX_LR_LEN, zl);
-      fir_r3(ri, AU_HALO + 3 * tid, D->lr_pad, FMX_LR_LEN, zr);
+      fir_r3p(li, AU_HALO + 3 * tid, D->lr_pad, D->lr_pair, FMX_LR_LEN, zl);
+      fir_r3p(ri, AU_HALO + 3 * tid, D->lr_pad, D->lr_pair, FMX_LR_LEN, zr);
       const float sc = D->lr_scale;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -1243,19 +1317,24 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       __syncthreads();
     }
     if (af) {
-      if (tid == 0) s_ee = sched_lower_bound(sched, sched_n, n0 + cnt);
-      __syncthreads();
-      const int eb = s_eb, ee = s_ee;
-      for (int e = eb + tid; e < ee; e += 256) {
-        const FmxSched en = sched[e];
-        auto gl = [&](int ii) -> float { return lf[AU_RHALO + ii - n0]; };
-        ol[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en.packed, en.mu, gl);
-        if (!mono) {
-          auto gr = [&](int ii) -> float { return rf[AU_RHALO + ii - n0]; };
-          orr[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en.packed, en.mu, gr);
+      const int eb = s_eb;
+      int last = -1;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = eb + tid + 256 * k;
+        if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
+          auto gl = [&](int ii) -> float { return lf[AU_RHALO + ii - n0]; };
+          ol[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en3[k].packed, en3[k].mu, gl);
+          if (!mono) {
+            auto gr = [&](int ii) -> float { return rf[AU_RHALO + ii - n0]; };
+            orr[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en3[k].packed, en3[k].mu, gr);
+          }
+          last = e;
         }
       }
+      if (last >= 0) atomicMax(&s_ee, last + 1);
       __syncthreads();
+      const int ee = s_ee;
       // de-emphasis + DC block (DF-II, af_post_processor.cpp:66-75 /
       // fm_demod.cpp:218-224): each IIR as a block affine scan for the
       // state before output k, then output k in the reference's op order.
@@ -1718,7 +1797,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     nmax = max(nmax, __shfl_xor(nmax, d));
     cmin = min(cmin, __shfl_xor(cmin, d));
   }
-  int tb = -1 << 30;  // sample index of L.tin[.][0]
+  int tb = -(1 << 30);  // sample index of L.tin[.][0]
   auto tile_at = [&](int t0) __attribute__((always_inline)) {
     __syncthreads();
     for (int idx = lane; idx < 64 * 64; idx += 64) {

@@ -194,6 +194,9 @@ enum {
   FMX_K_COUNT = 4
 };
 int fmx_timing_enable(void *handle, int enable);
+/* diagnostic: frontend per-stage clocks, 8 values (handle created with the
+ * environment variable FMX_STAMPS=1; FMX_E_INVALID otherwise) */
+int fmx_debug_stamps(void *handle, unsigned long long *out, int n);
 int fmx_kernel_times(void *handle, double *ms, int *launches, int n);
 
 /* ---- synthetic IQ (bench / tests input; see fmx_synth.h) ---- */

@@ -1,0 +1,38 @@
+"""Diagnostic: per-stage clocks of k_frontend on the bench workload.
+Needs libfmx.so built with `make -C fmtuner-sdr_amd STAMPS=1 -B`; runs with
+FMX_STAMPS=1 (set here).  Prints
+the share of each stage in thread 0's timeline."""
+import ctypes as C
+import os
+import sys
+
+os.environ["FMX_STAMPS"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fmtuner-sdr_amd"))
+import torch  # noqa: E402
+import fmx  # noqa: E402
+
+NAMES = ["decim", "dc", "iqfir+agc", "discrim", "pilot", "rds_rs", "carry", "tail"]
+L = fmx.lib()
+L.fmx_debug_stamps.restype = C.c_int
+L.fmx_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+Cn, B, M, nblk = int(os.environ.get("C", "4096")), 4096, 10, 4
+h = fmx.Handle(fmx.make_config(), Cn)
+dev = torch.device("cuda")
+scfg = fmx.make_synth(kind=2, n_bits=6000)
+bits, _ = fmx.synth_rds_bits(scfg, 0, Cn)
+d_bits = torch.from_numpy(bits).to(dev)
+row = 2 * B * M * nblk
+d_iq = torch.empty((Cn, row), dtype=torch.uint8, device=dev)
+h.synth_device(scfg, 0, Cn, 0, B * M * nblk, d_bits.data_ptr(), d_iq.data_ptr(), row)
+pl = torch.empty((Cn, B), device=dev)
+pr = torch.empty((Cn, B), device=dev)
+cnt = torch.empty(Cn, dtype=torch.int32, device=dev)
+out = fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr())
+for b in range(nblk):
+    h.process_block(d_iq.data_ptr() + b * 2 * B * M, row, B, out)
+h.sync()
+v = (C.c_ulonglong * 8)()
+assert L.fmx_debug_stamps(h.h, v, 8) == 0
+tot = sum(v)
+for k in range(8):
+    print(f"{NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
