@@ -43,6 +43,16 @@ namespace fmx {
 static constexpr float kPiF = 3.14159265358979323846f;
 
 /* ------------------------------------------------------------------ */
+// Wave-uniform reads of the design tables (taps) through the scalar cache:
+// the constant address space makes the backend emit s_load instead of a
+// per-lane global_load + wait in every FIR iteration.  Only for addresses
+// that are uniform across the wave.
+#define FMX_CONST __attribute__((address_space(4)))
+template <typename T> __device__ __forceinline__ const FMX_CONST T *cptr(const T *p) {
+  return (const FMX_CONST T *)p;
+}
+
+/* ------------------------------------------------------------------ */
 /* liquid NCO fixed-point helpers (nco.proto.c restated)               */
 __device__ __forceinline__ uint32_t d_nco_constrain(float x) {
   const float p = (float)((double)x * 0.159154943091895);
@@ -91,7 +101,7 @@ __device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const flo
 #pragma unroll 1
   for (int p = 0; p < M; ++p) {
     const __half2 *row = inq + (M - 1 - p) * Q + 3 * tid + (TPP - 1);
-    const float *h = poly + p * TPP;
+    const FMX_CONST float *h = cptr(poly) + p * TPP;
 #pragma unroll
     for (int s = -(TPP - 1); s <= 2; ++s) {
       const __half2 hv = row[s];
@@ -126,7 +136,7 @@ __device__ __forceinline__ void fe_decimate_u8(const uint8_t *raw, const float *
   for (int r = 0; r < 3; ++r) acc[r] = f32x2{0.0f, 0.0f};
 #pragma unroll 1
   for (int qb = 0; qb < NB; ++qb) {
-    const float *hq = hpad + FMX_DEC_PAD + L - qb * M;  // tap of sample u, output r: hq[r*M - u]
+    const FMX_CONST float *hq = cptr(hpad) + FMX_DEC_PAD + L - qb * M;  // tap of sample u, output r: hq[r*M - u]
     uint32_t w[M / 2];
 #pragma unroll
     for (int e = 0; e < M / 2; ++e) w[e] = rw[qb * (M / 2) + e];
@@ -155,7 +165,7 @@ __device__ __forceinline__ void fir_c3(const float2 *x, int base, const float *_
   float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, i0 = 0.0f, i1 = 0.0f, i2 = 0.0f;
 #pragma unroll 1
   for (int s = -(L - 1); s <= 2; s += 4) {
-    const float *h = hp + 5 - s; // h[r - u] = taps[r - (s + u)]
+    const FMX_CONST float *h = cptr(hp) + 5 - s; // h[r - u] = taps[r - (s + u)]
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float2 v = x[base + s + u];
@@ -182,7 +192,7 @@ __device__ __forceinline__ void fir_r3(const float *x, int base, const float *__
   float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
 #pragma unroll 1
   for (int s = -(P - 1); s <= 2; s += 4) {
-    const float *h = hp + 5 - s;
+    const FMX_CONST float *h = cptr(hp) + 5 - s;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float v = x[base + s + u];
@@ -204,8 +214,8 @@ __device__ __forceinline__ void fir_r3p(const float *x, int base, const float *_
   float a2 = 0.0f;
 #pragma unroll 1
   for (int s = -(P - 1); s <= 2; s += 4) {
-    const float *h = hp + 5 - s;
-    const float(*h2)[2] = hq + 5 - s;
+    const FMX_CONST float *h = cptr(hp) + 5 - s;
+    const FMX_CONST float(*h2)[2] = cptr(hq) + 5 - s;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float v = x[base + s + u];
@@ -335,7 +345,8 @@ template <int M, int TPP, bool VEC> struct FeLayout {
   static constexpr int XIN = R0;
   static constexpr int MX = XIN + (FE_HALO_IQ + FE_T + 8) * 8;
   static constexpr int RB = MX + (FMX_HIST + FE_T + 8) * 4;   // RDS resampler window: 32 history + chunk
-  static constexpr int SG = RB + (32 + FE_T + 8) * 4;            // 4 waves x 6 u64 RF-level partials
+  static constexpr int RSH = RB + (32 + FE_T + 8) * 4;           // RDS resampler filter bank (per-lane branch)
+  static constexpr int SG = RSH + FMX_NPFB * FMX_RDS_RS_SUB * 4;  // 4 waves x 6 u64 RF-level partials
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (M > 1) ? (RAW_BYTES - 64 + 16 * 256 - 1) / (16 * 256) : 1;  // 16-B loads / thread
@@ -356,6 +367,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   float *mx = reinterpret_cast<float *>(smem + LY::MX);
   float *rb = reinterpret_cast<float *>(smem + LY::RB);
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
+  float *rsh = reinterpret_cast<float *>(smem + LY::RSH);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
   const bool want_sig = a.sig_out != nullptr && a.in_mode != FE_IN_CF && a.in_mode != FE_IN_MPX;
   SigAcc sig;
@@ -433,6 +445,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   }
   const float *rhist = a.rds_hist + (size_t)c * 32;
   if (rds && tid < 32) rb[tid] = rhist[tid];
+  if (rds)
+    for (int k = tid; k < FMX_NPFB * FMX_RDS_RS_SUB; k += 256) rsh[k] = D->rds_rs_h[k];
   int e_pos = 0;
   // VEC: chunk bytes [2*n0*M - HB, 2*(n0+cnt)*M) are fetched with 16-B loads
   // one chunk ahead into registers (HBM latency hidden behind the previous
@@ -723,7 +737,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
           auto get = [&](int ii) -> float { return rb[32 + ii - n0]; };
           a.rds_out[(size_t)c * a.rds_stride + e] =
-              resamp_out<FMX_RDS_RS_SUB>(D->rds_rs_h, en3[k].packed, en3[k].mu, get);
+              resamp_out<FMX_RDS_RS_SUB>(rsh, en3[k].packed, en3[k].mu, get);
           last = e;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1219,6 +1233,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   __shared__ float ol[AU_MAXOUT], orr[AU_MAXOUT];
   __shared__ int s_eb, s_ee, s_count;
   __shared__ float s_iir[4], s_ws[12];  // [de_L, de_R, dc_L, dc_R]; scan scratch
+  __shared__ float afh[FMX_NPFB * FMX_AF_SUB];  // resampler bank (per-lane branch -> LDS)
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
@@ -1273,6 +1288,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     s_eb = 0;
     s_count = 0;
   }
+  if (af)
+    for (int k = tid; k < FMX_NPFB * FMX_AF_SUB; k += 256) afh[k] = D->af_h[k];
   const float *inl = a.in_l + (size_t)c * a.in_stride;
   const float *inr = mono ? nullptr : a.in_r + (size_t)c * a.in_stride;
   __syncthreads();
@@ -1324,10 +1341,10 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         const int e = eb + tid + 256 * k;
         if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
           auto gl = [&](int ii) -> float { return lf[AU_RHALO + ii - n0]; };
-          ol[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en3[k].packed, en3[k].mu, gl);
+          ol[e - eb] = resamp_out<FMX_AF_SUB>(afh, en3[k].packed, en3[k].mu, gl);
           if (!mono) {
             auto gr = [&](int ii) -> float { return rf[AU_RHALO + ii - n0]; };
-            orr[e - eb] = resamp_out<FMX_AF_SUB>(D->af_h, en3[k].packed, en3[k].mu, gr);
+            orr[e - eb] = resamp_out<FMX_AF_SUB>(afh, en3[k].packed, en3[k].mu, gr);
           }
           last = e;
         }
