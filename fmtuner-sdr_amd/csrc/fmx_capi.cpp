@@ -396,8 +396,9 @@ static void destroy(Handle *h) {
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
-  for (hipStream_t st : {h->sA, h->sB, h->sC})
-    if (st) hipStreamDestroy(st);
+  if (h->sC && h->sC != h->sA) hipStreamDestroy(h->sC);
+  if (h->sB && h->sB != h->sA) hipStreamDestroy(h->sB);
+  if (h->sA) hipStreamDestroy(h->sA);
   delete h->hdes;
   delete h;
 }
@@ -437,8 +438,12 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     return FMX_E_INVALID;
   }
   HIP_TRY(hipStreamCreateWithFlags(&h->sA, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+  if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
+    h->sB = h->sC = h->sA; // diagnostic: one stream, kernels timed in isolation
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+  }
   for (int b = 0; b < 2; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->evB[b], hipEventDisableTiming));

@@ -1478,13 +1478,17 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
          ((uint32_t)bs_block_number(ooff) + d / 26) % 4 == (uint32_t)bs_block_number(off);
 }
 
+// k_rds input tiles: RDS_TW samples per channel, advanced by 64 with an
+// RDS_TW-64 sample overlap so a chunk of 8 never straddles two tiles.
+#define RDS_TW 72
 struct RdsLds {
   float taps[24][12];
   float mf[FMX_NPFB * FMX_SS_SUB];
   float dmf[FMX_NPFB * FMX_SS_SUB];
   uint32_t esyn[5][52];
   uint32_t eerr[5][52];
-  float tin[64][65];
+  float tin[64][RDS_TW + 1]; // 64 channels x RDS_TW samples (odd row stride: conflict-free column reads)
+  int cnt[64];
 };
 
 __device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
@@ -1814,23 +1818,52 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     nmax = max(nmax, __shfl_xor(nmax, d));
     cmin = min(cmin, __shfl_xor(cmin, d));
   }
-  int tb = -(1 << 30);  // sample index of L.tin[.][0]
-  auto tile_at = [&](int t0) __attribute__((always_inline)) {
-    __syncthreads();
-    for (int idx = lane; idx < 64 * 64; idx += 64) {
-      const int row = idx >> 6, col = idx & 63;
-      const int ch = c0 + row;
-      if (ch < a.C) {
-        const int cn = a.in_count[ch];
-        L.tin[row][col] = (t0 + col < cn) ? a.in[(size_t)ch * a.in_stride + t0 + col] : 0.0f;
-      }
+  // Tiles [tb, tb + RDS_TW) of 64 channels are staged in LDS; the next 64
+  // samples of every row are prefetched into registers (one coalesced 256-B
+  // row per load, 64 loads in flight) while the current tile is consumed.
+  if (lane < 64) L.cnt[lane] = (c0 + lane < a.C) ? a.in_count[c0 + lane] : 0;
+  __syncthreads();
+  float pre[64];
+  auto prefetch = [&](int base) __attribute__((always_inline)) {
+    const int col = base + lane;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+      const int ch = c0 + r;
+      pre[r] = (ch < a.C && col < L.cnt[r]) ? a.in[(size_t)ch * a.in_stride + col] : 0.0f;
     }
-    __syncthreads();
-    tb = t0;
+  };
+  int tb = 0;  // sample index of L.tin[.][0]
+  prefetch(0);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) L.tin[r][lane] = pre[r];
+  if (lane < RDS_TW - 64) {
+    for (int r = 0; r < 64; ++r) {
+      const int ch = c0 + r, col = 64 + lane;
+      L.tin[r][col] = (ch < a.C && col < L.cnt[r]) ? a.in[(size_t)ch * a.in_stride + col] : 0.0f;
+    }
+  }
+  prefetch(RDS_TW);
+  __syncthreads();
+  // make [t, t + len) resident (t only moves forward, len <= RDS_TW - 64 + 1)
+  auto need = [&](int t, int len) __attribute__((always_inline)) {
+    while (t + len > tb + RDS_TW) {
+      // own row: overlap columns move to the front, then the prefetched 64
+      float keep[RDS_TW - 64];
+#pragma unroll
+      for (int k = 0; k < RDS_TW - 64; ++k) keep[k] = L.tin[lane][64 + k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < RDS_TW - 64; ++k) L.tin[lane][k] = keep[k];
+#pragma unroll
+      for (int r = 0; r < 64; ++r) L.tin[r][RDS_TW - 64 + lane] = pre[r];
+      tb += 64;
+      prefetch(tb + RDS_TW);
+      __syncthreads();
+    }
   };
   // one sample for every lane that still has input: own tap row from LDS
   auto step_one = [&](int t) __attribute__((always_inline)) {
-    if (t >= tb + 64 || t < tb) tile_at(t);
+    need(t, 1);
     if (act && t < count) {
       const int j = (int)(s.sample_since_reset % FMX_RDS_DECIM);
       const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
@@ -1856,7 +1889,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     while (t < nmax && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) != 1u) step_one(t++);
     constexpr int U = 8;
     while (t + U <= cmin) {
-      if (t + U > tb + 64 || t < tb) tile_at(t);
+      need(t, U);
       const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;  // 1, 9 or 17
       const bool out_end = (j0 == 17u);
       float ph[U];
