@@ -54,13 +54,15 @@ struct Handle {
   // (capped at L-1): a full history lets the frontend take its VEC path
   long dec_fill = 0;
   std::string err;
-  // sA: frontend, resets, uploads; sB: stereo + audio; sC: RDS.  Step k's
-  // frontend runs while step k-1's stereo/RDS kernels (latency-bound, one
-  // lane per channel) still occupy a few SIMDs.
-  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr;
-  hipEvent_t evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr}, evC[2] = {nullptr, nullptr};
-  hipEvent_t evTmpB = nullptr, evTmpC = nullptr;
-  bool evB_set[2] = {false, false}, evC_set[2] = {false, false};
+  // sA: frontend, resets, uploads; sB: stereo PLL; sC: RDS; sD: audio.
+  // Step k's frontend runs while step k-1's PLL / RDS kernels (latency-bound,
+  // one lane per channel, a few SIMDs) and step k-1's audio still run; the
+  // audio of step k overlaps the PLL of step k+1 (raw L/R double-buffered).
+  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
+  hipEvent_t evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr}, evC[2] = {nullptr, nullptr},
+             evD[2] = {nullptr, nullptr};
+  hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr;
+  bool evB_set[2] = {false, false}, evC_set[2] = {false, false}, evD_set[2] = {false, false};
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -91,7 +93,7 @@ struct Handle {
   // intermediates (double-buffered by step parity)
   float *mpx[2] = {nullptr, nullptr}, *pilot[2] = {nullptr, nullptr}, *rds_in[2] = {nullptr, nullptr};
   int *rds_count[2] = {nullptr, nullptr};
-  float *lraw = nullptr, *rraw = nullptr;
+  float *lraw[2] = {nullptr, nullptr}, *rraw[2] = {nullptr, nullptr};
   int rds_stride = 0;
   uint32_t block_index = 0;
   TimingSet t_af, t_mono, t_rds;
@@ -278,13 +280,15 @@ static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count)
   return FMX_OK;
 }
 
-// Make sA wait for everything queued on sB and sC (used before resets,
+// Make sA wait for everything queued on sB, sC and sD (used before resets,
 // parameter uploads and the single-stream stage entry points).
 static int join_into_A(Handle *h) {
   HIP_TRY(hipEventRecord(h->evTmpB, h->sB));
   HIP_TRY(hipEventRecord(h->evTmpC, h->sC));
+  HIP_TRY(hipEventRecord(h->evTmpD, h->sD));
   HIP_TRY(hipStreamWaitEvent(h->sA, h->evTmpB, 0));
   HIP_TRY(hipStreamWaitEvent(h->sA, h->evTmpC, 0));
+  HIP_TRY(hipStreamWaitEvent(h->sA, h->evTmpD, 0));
   return FMX_OK;
 }
 
@@ -385,6 +389,7 @@ static void destroy(Handle *h) {
   if (h->sA) hipStreamSynchronize(h->sA);
   if (h->sB) hipStreamSynchronize(h->sB);
   if (h->sC) hipStreamSynchronize(h->sC);
+  if (h->sD) hipStreamSynchronize(h->sD);
   for (auto &p : h->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -392,10 +397,12 @@ static void destroy(Handle *h) {
   for (auto e : h->pool) hipEventDestroy(e);
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < 2; ++b)
-    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b]})
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
+  if (h->evTmpD) hipEventDestroy(h->evTmpD);
+  if (h->sD && h->sD != h->sA) hipStreamDestroy(h->sD);
   if (h->sC && h->sC != h->sA) hipStreamDestroy(h->sC);
   if (h->sB && h->sB != h->sA) hipStreamDestroy(h->sB);
   if (h->sA) hipStreamDestroy(h->sA);
@@ -439,18 +446,21 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   }
   HIP_TRY(hipStreamCreateWithFlags(&h->sA, hipStreamNonBlocking));
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
-    h->sB = h->sC = h->sA; // diagnostic: one stream, kernels timed in isolation
+    h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
   } else {
     HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
   }
   for (int b = 0; b < 2; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->evB[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->evC[b], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->evD[b], hipEventDisableTiming));
   }
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpD, hipEventDisableTiming));
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
@@ -480,8 +490,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->dsig, C * 4)) != FMX_OK) return rc;
   if (const char *e = std::getenv("FMX_STAMPS"); e && e[0] == '1') {
-    if ((rc = dalloc(h, &h->dbg, 8)) != FMX_OK) return rc;
-    HIP_TRY(hipMemset(h->dbg, 0, 8 * sizeof(unsigned long long)));
+    if ((rc = dalloc(h, &h->dbg, 32)) != FMX_OK) return rc; // [0,8) frontend, [8,16) k_rds, [16,26) k_pll
+    HIP_TRY(hipMemset(h->dbg, 0, 32 * sizeof(unsigned long long)));
   }
   if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
   HIP_TRY(hipMemset(h->sig_smooth, 0, sizeof(float) * 2 * C));
@@ -509,12 +519,14 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->mpx[b], C * B)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->pilot[b], C * B)) != FMX_OK) return rc;
   }
-  if ((rc = dalloc(h, &h->lraw, C * B)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->rraw, C * B)) != FMX_OK) return rc;
+  for (int b = 0; b < 2; ++b) {
+    if ((rc = dalloc(h, &h->lraw[b], C * B)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rraw[b], C * B)) != FMX_OK) return rc;
+  }
   if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
-  h->rds_stride = h->t_rds.stride;
+  h->rds_stride = (h->t_rds.stride + 63) & ~63; // 256-B rows: k_rds stages 16-B aligned pieces
   for (int b = 0; b < 2; ++b) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
@@ -593,10 +605,11 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.mpx = mpx;
   a.mpx_stride = mpx_stride;
   a.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
-  a.lraw = h->lraw;
-  a.rraw = h->rraw;
+  a.lraw = h->lraw[buf];
+  a.rraw = h->rraw[buf];
   a.lr_stride = h->cfg.block;
   a.st = h->st;
+  a.dbg = h->dbg ? h->dbg + 16 : nullptr;
   return a;
 }
 
@@ -610,6 +623,7 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.st = h->rds;
   a.ring = h->ring;
   a.block_index = h->block_index;
+  a.dbg = h->dbg ? h->dbg + 8 : nullptr;
   return a;
 }
 
@@ -639,12 +653,14 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
   const int buf = static_cast<int>(h->step & 1);
-  // buffers of parity `buf` were last read by step k-2 on sB / sC
+  // buffers of parity `buf` were last read by step k-2 on sB / sC / sD
   if (h->evB_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf], 0));
   if (h->evC_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf], 0));
-  if (o->d_mpx) { // a caller-owned MPX buffer is read by step k-1's stereo/RDS kernels
+  if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
+  if (o->d_mpx) { // a caller-owned MPX buffer is read by step k-1's stereo/RDS/audio kernels
     if (h->evB_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf ^ 1], 0));
     if (h->evC_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf ^ 1], 0));
+    if (h->evD_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf ^ 1], 0));
   }
   if (rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
@@ -694,22 +710,30 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
   h->evC_set[buf] = true;
-  // ---- stereo + audio (sB) ----
+  // ---- stereo PLL (sB), audio (sD) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   if (stereo) {
-    {
-      PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
-      a.stereo_out = o->d_stereo;
-      a.pilot_tenths_out = o->d_pilot_tenths;
-      KTimer t(h, FMX_K_STEREO, h->sB);
-      if ((rc = launch_pll(a, h->sB)) != FMX_OK) {
-        h->err = "pll launch failed";
-        return rc;
-      }
+    // raw L/R of parity buf were last read by step k-2's audio
+    if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[buf], 0));
+    PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
+    a.stereo_out = o->d_stereo;
+    a.pilot_tenths_out = o->d_pilot_tenths;
+    KTimer t(h, FMX_K_STEREO, h->sB);
+    if ((rc = launch_pll(a, h->sB)) != FMX_OK) {
+      h->err = "pll launch failed";
+      return rc;
     }
+  } else {
+    if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->sB));
+    if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->sB));
+  }
+  HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
+  h->evB_set[buf] = true;
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0)); // after the PLL (stereo) / the frontend (mono)
+  if (stereo) {
     AudioArgs a = audio_args(h, n, 0, &h->t_af);
-    a.in_l = h->lraw;
-    a.in_r = h->rraw;
+    a.in_l = h->lraw[buf];
+    a.in_r = h->rraw[buf];
     a.in_stride = h->cfg.block;
     a.out_l = o->d_pcm_l;
     a.out_r = o->d_pcm_r;
@@ -717,8 +741,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.out_count = o->d_pcm_count;
     a.cap = h->cfg.block;
     a.clamp = 1;
-    KTimer t(h, FMX_K_AUDIO, h->sB);
-    if ((rc = launch_audio(a, h->sB)) != FMX_OK) {
+    KTimer t(h, FMX_K_AUDIO, h->sD);
+    if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
       return rc;
     }
@@ -733,18 +757,14 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.out_count = o->d_pcm_count;
     a.cap = 1 << 30;
     a.clamp = 1;
-    {
-      KTimer t(h, FMX_K_AUDIO, h->sB);
-      if ((rc = launch_audio(a, h->sB)) != FMX_OK) {
-        h->err = "audio launch failed";
-        return rc;
-      }
+    KTimer t(h, FMX_K_AUDIO, h->sD);
+    if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
+      h->err = "audio launch failed";
+      return rc;
     }
-    if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->sB));
-    if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->sB));
   }
-  HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
-  h->evB_set[buf] = true;
+  HIP_TRY(hipEventRecord(h->evD[buf], h->sD));
+  h->evD_set[buf] = true;
   h->block_index++;
   step_done(h, stereo);
   return FMX_OK;
@@ -758,12 +778,13 @@ static int stage_begin(Handle *h, int n) {
   if ((rc = prepare(h)) != FMX_OK) return rc;
   return join_into_A(h);
 }
-// later pipelined work on sB / sC must see the stage's results
+// later pipelined work on sB / sC / sD must see the stage's results
 static int stage_end(Handle *h) {
   const int buf = static_cast<int>(h->step & 1);
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evA[buf], 0));
   return FMX_OK;
 }
 
@@ -801,6 +822,7 @@ int fmx_sync(void *handle) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
   HIP_TRY(hipStreamSynchronize(h->sC));
+  HIP_TRY(hipStreamSynchronize(h->sD));
   HIP_TRY(hipStreamSynchronize(h->sB));
   HIP_TRY(hipStreamSynchronize(h->sA));
   return FMX_OK;
@@ -866,7 +888,7 @@ int fmx_debug_stamps(void *handle, unsigned long long *out, int n) {
   Handle *h = H(handle);
   if (!h || !h->dbg || n < 8) return FMX_E_INVALID;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, h->dbg, (n >= 32 ? 32 : n >= 16 ? 16 : 8) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return FMX_OK;
 }
 
@@ -1033,8 +1055,8 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
   }
   {
     AudioArgs a = audio_args(h, n, 4, nullptr);
-    a.in_l = h->lraw;
-    a.in_r = h->rraw;
+    a.in_l = h->lraw[buf];
+    a.in_r = h->rraw[buf];
     a.in_stride = h->cfg.block;
     a.lr_out_l = d_left;
     a.lr_out_r = d_right;

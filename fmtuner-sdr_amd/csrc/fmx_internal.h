@@ -91,6 +91,7 @@ struct PllArgs {
   int lr_stride;
   FmxStereoState *st;
   int *stereo_out, *pilot_tenths_out;
+  unsigned long long *dbg; // [10] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
 };
 
 struct AudioArgs {
@@ -129,6 +130,7 @@ struct RdsArgs {
   int groups_stride;
   int *group_count;
   uint32_t block_index;
+  unsigned long long *dbg; // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
 };
 
 // launchers (fmx_kernels.hip); stream is a hipStream_t

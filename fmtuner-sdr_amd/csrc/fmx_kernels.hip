@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fmx_internal.h"
+#include "fmx_math.h"
 #include "fmx_synth.h"
 
 namespace fmx {
@@ -53,6 +54,12 @@ template <typename T> __device__ __forceinline__ const FMX_CONST T *cptr(const T
 }
 
 /* ------------------------------------------------------------------ */
+// Buffer resource over [base, base + bytes): out-of-range loads return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+/* ------------------------------------------------------------------ */
 /* liquid NCO fixed-point helpers (nco.proto.c restated)               */
 __device__ __forceinline__ uint32_t d_nco_constrain(float x) {
   const float p = (float)((double)x * 0.159154943091895);
@@ -62,7 +69,9 @@ __device__ __forceinline__ uint32_t d_nco_constrain(float x) {
   return (s >= 4294967296.0f) ? 0u : (uint32_t)s;
 }
 __device__ __forceinline__ float d_nco_phase(uint32_t theta) {
-  return (float)(6.283185307179586 * (double)(float)theta / 4294967296.0);
+  // (2pi * theta) / 2^32 in double: the power-of-two scaling is exact, so it
+  // is folded into the constant (one v_mul_f64, same rounding)
+  return (float)((double)(float)theta * (6.283185307179586 / 4294967296.0));
 }
 // x / c correctly rounded for a constant c with rc = RN(1/c) (Markstein:
 // residual exact by FMA); 3 dependent ops instead of the IEEE divide
@@ -71,6 +80,12 @@ __device__ __forceinline__ float d_div_const(float x, float c, float rc) {
   const float q = x * rc;
   const float r = fmaf(-q, c, x);
   return fmaf(r, rc, q);
+}
+// unwrapf (liquid_wrappers.cpp / stereo_decoder.cpp): one 2pi step into
+// [-pi, pi], as selects (no divergent branches in the sample loops)
+__device__ __forceinline__ float d_unwrap(float x) {
+  const float dn = x - 2.0f * kPiF, up = x + 2.0f * kPiF;
+  return (x > kPiF) ? dn : ((x < -kPiF) ? up : x);
 }
 __device__ __forceinline__ float d_clamp(float v, float lo, float hi) {
   return (v < lo) ? lo : ((hi < v) ? hi : v);
@@ -903,96 +918,143 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
   return 0.0f;
 }
 
-/* k_pll is a three-stage software pipeline over tiles of PLL_T samples for
- * PLL_CH channels, one stage per wave of the workgroup:
- *   wave 0  (lane = channel, serial)   PLL phase recursion, pilot/MPX
- *           envelopes, pilot I/Q integrators: only what feeds back.
- *   waves 2-3 (lane = (channel, t))    everything that is parallel in time:
- *           sqrt, the five divisions of the blend target, the L-R matrix.
- *   wave 1  (lane = channel, serial)   the blend recursion and the outputs,
- *           then the loads of the next input tiles.
- * Tile k is in stage 1 while tile k-1 is in stage 2 and tile k-2 in stage 3;
- * three LDS slots rotate.  The arithmetic of every value is the reference's
- * (stereo_decoder.cpp:226-288) in the same order; only WHERE it runs moved. */
+/* k_pll is a five-wave software pipeline over tiles of PLL_T samples for
+ * PLL_CH channels (lane = channel in the serial waves):
+ *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
+ *                 pll_step, step, phase, sin(phase)         stereo_decoder.cpp:251-256
+ *   W1 (serial)   what consumes the PLL without feeding it back: pilot/MPX
+ *                 envelopes, pilot I/Q integrators (cos(phase)), PLL
+ *                 frequency, cos(2 phase)                    stereo_decoder.cpp:246-250,257-266,275-279
+ *   W2a, W2b      (lane = (channel, t)) everything parallel in time: the
+ *                 blend target (sqrt, divisions) and the L-R matrix   :120-166,268-284
+ *   W3 (serial)   the blend recursion, the outputs, and the loads of later
+ *                 input tiles                               :286-288
+ * At iteration k, W0 runs tile k, W1 tile k-1, W2 tile k-2, W3 tile k-3;
+ * LDS slots rotate.  Every value is computed with the reference's arithmetic
+ * in the reference's order; only WHERE it runs moved. */
 #define PLL_CH 64
-#define PLL_TS (PLL_T + 4)                 // padded row (16-B aligned)
-#define PLL_NF 5                           // fields per (channel, t) in a slot
+#define PLL_TS (PLL_T + 4)                 // padded row (16-B aligned, conflict-free float4 rows)
+#define PLL_WAVES 5
 struct PllShared {
-  float slot[3][PLL_NF][PLL_CH][PLL_TS];   // S1 -> S2 (in place) -> S3
-  float in[2][2][PLL_CH][PLL_TS];          // pilot, mpx tiles for S1
-  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles for S2
+  float inp[3][PLL_CH][PLL_TS];            // pilot tiles (k+1 loading, k in W0, k-1 in W1)
+  float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k loading, k-1 in W1)
+  float s0[2][3][PLL_CH][PLL_TS];          // W0 -> W1: phase after the step, its sine and cosine
+  float s1[2][5][PLL_CH][PLL_TS];          // W1 -> W2: PBM, MM, MAG2, FREQ, COS2
+  float s2[2][4][PLL_CH][PLL_TS];          // W2 -> W3: TGT, MONO, DL, DR
+  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles for W2
   int s2_flags[PLL_CH];                    // bit0 fmono, bit1 fstereo, bit2 detected, bits 8.. blend mode
   float s2_gate[PLL_CH];
-  float blend_out[PLL_CH];                 // stage 3 -> stage 1 at block end
 };
-enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2, F_FREQ = 3, F_COS2 = 4 };  // S1 output
-enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };                 // S2 output
+enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2, F_FREQ = 3, F_COS2 = 4 };  // W1 output
+enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };                 // W2 output
 
-// pilot + MPX of tile (t0, cnt) into in[buf]; lanes of one wave, 16-B loads
-// when rows are aligned.
-__device__ __forceinline__ void pll_load_in(const PllArgs &a, PllShared *sh, int buf, int c0, int t0, int cnt,
-                                            int lane, bool vec) {
-  if (vec && cnt == PLL_T) {
-    constexpr int Q = PLL_T / 4;  // float4 per row
-    float4 v[2][PLL_CH * Q / 64];
+// One row-tile (PLL_CH rows x PLL_T samples from t0) of a [rows][stride]
+// array, staged through registers: issue() starts 16-B buffer loads (one
+// VGPR offset, the tile position in SGPRs; rows past C read 0), store()
+// writes them to an LDS tile after the next barrier.  Needs 16-B aligned
+// rows and a full tile; pll_load_sync covers the rest.
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+struct PllStage {
+  static constexpr int J = PLL_CH * PLL_T / 4 / 64; // float4 per lane
+  float4 v[J];
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t r, int stride, int t0, int lane) {
+    const uint32_t voff = (uint32_t)(((lane / (PLL_T / 4)) * stride + 4 * (lane % (PLL_T / 4))) * 4);
 #pragma unroll
-    for (int j = 0; j < PLL_CH * Q / 64; ++j) {
-      const int idx = lane + 64 * j;
-      const int row = idx / Q, q = idx % Q;
-      const int ch = min(c0 + row, a.C - 1);
-      v[0][j] = *reinterpret_cast<const float4 *>(a.pilot + (size_t)ch * a.pilot_stride + t0 + 4 * q);
-      v[1][j] = *reinterpret_cast<const float4 *>(a.mpx + (size_t)ch * a.mpx_stride + t0 + 4 * q);
-    }
-#pragma unroll
-    for (int j = 0; j < PLL_CH * Q / 64; ++j) {
-      const int idx = lane + 64 * j;
-      const int row = idx / Q, q = idx % Q;
-      *reinterpret_cast<float4 *>(&sh->in[buf][0][row][4 * q]) = v[0][j];
-      *reinterpret_cast<float4 *>(&sh->in[buf][1][row][4 * q]) = v[1][j];
-    }
-    return;
+    for (int j = 0; j < J; ++j)
+      v[j] = bload4(r, voff, (uint32_t)((t0 + j * (64 / (PLL_T / 4)) * stride) * 4));
   }
+  __device__ __forceinline__ void store(float (*dst)[PLL_TS], int lane) const {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int idx = lane + 64 * j;
+      const int row = idx / (PLL_T / 4), q = idx % (PLL_T / 4);
+      *reinterpret_cast<float4 *>(&dst[row][4 * q]) = v[j];
+    }
+  }
+};
+__device__ __forceinline__ void pll_load_sync(const float *src, int stride, int C, float (*dst)[PLL_TS], int c0,
+                                              int t0, int cnt, int lane) {
   for (int idx = lane; idx < PLL_CH * PLL_T; idx += 64) {
     const int row = idx / PLL_T, col = idx % PLL_T;
     const int ch = c0 + row;
-    float p = 0.0f, m = 0.0f;
-    if (ch < a.C && col < cnt) {
-      p = a.pilot[(size_t)ch * a.pilot_stride + t0 + col];
-      m = a.mpx[(size_t)ch * a.mpx_stride + t0 + col];
-    }
-    sh->in[buf][0][row][col] = p;
-    sh->in[buf][1][row][col] = m;
+    dst[row][col] = (ch < C && col < cnt) ? src[(size_t)ch * stride + t0 + col] : 0.0f;
   }
 }
 
-// delay-line outputs of tile (t0, cnt): mpx[t - Dly] or the previous call's
-// history (stereo_decoder.cpp delayLine).
-__device__ __forceinline__ void pll_load_dly(const PllArgs &a, PllShared *sh, int buf, int c0, int t0, int cnt,
-                                             int lane, int Dly) {
-  constexpr int J = PLL_CH * PLL_T / 64;
+// delay-line outputs of tile (t0, cnt): mpx[t - Dly], or the previous call's
+// history (stereo_decoder.cpp delayLine) for t < Dly, staged through
+// registers.  The source is wave-uniform except in the one tile that
+// straddles t = Dly.
+struct PllDlyStage {
+  static constexpr int J = PLL_CH * PLL_T / 64;
   float v[J];
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rm, int mstride, __amdgpu_buffer_rsrc_t rh, int t0,
+                                        int cnt, int lane, int Dly) {
+    const int row0 = lane / PLL_T, col = lane % PLL_T;
+    const bool colok = col < cnt;
+    // columns past cnt: an offset past the buffer range, read as 0 (no select
+    // after the load, so nothing waits for it before the next barrier)
+    const uint32_t vm = colok ? (uint32_t)((row0 * mstride + col) * 4) : 0x80000000u;
+    const uint32_t vh = colok ? (uint32_t)((row0 * FMX_HIST + col) * 4) : 0x80000000u;
+    const int d0 = t0 - Dly; // delay index of column 0
+    if (d0 >= 0) {
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int idx = lane + 64 * j;
-    const int row = idx / PLL_T, col = idx % PLL_T;
-    const int ch = c0 + row;
-    float x = 0.0f;
-    if (ch < a.C && col < cnt) {
-      const int di = t0 + col - Dly;
-      x = (di >= 0) ? a.mpx[(size_t)ch * a.mpx_stride + di] : a.st_hist_rd[(size_t)ch * FMX_HIST + FMX_HIST + di];
+      for (int j = 0; j < J; ++j) v[j] = bload1(rm, vm, (uint32_t)((d0 + j * (64 / PLL_T) * mstride) * 4));
+    } else if (d0 + PLL_T <= 0) {
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        v[j] = bload1(rh, vh, (uint32_t)((FMX_HIST + d0 + j * (64 / PLL_T) * FMX_HIST) * 4));
+    } else {
+      const bool from_m = d0 + col >= 0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const uint32_t om = (uint32_t)(((j * (64 / PLL_T)) * mstride + (from_m ? d0 : 0)) * 4);
+        const uint32_t oh = (uint32_t)(((j * (64 / PLL_T)) * FMX_HIST + FMX_HIST + (from_m ? 0 : d0)) * 4);
+        const float x = from_m ? bload1(rm, vm + om, 0) : bload1(rh, vh + oh, 0);
+        v[j] = colok ? x : 0.0f;
+      }
     }
-    v[j] = x;
   }
+  __device__ __forceinline__ void store(float (*dst)[PLL_TS], int lane) const {
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int idx = lane + 64 * j;
-    sh->dly[buf][idx / PLL_T][idx % PLL_T] = v[j];
+    for (int j = 0; j < J; ++j) {
+      const int idx = lane + 64 * j;
+      dst[idx / PLL_T][idx % PLL_T] = v[j];
+    }
   }
-}
+};
 
-__global__ __launch_bounds__(256) void k_pll(PllArgs a) {
+__global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
   __shared__ PllShared shm;
   PllShared *sh = &shm;
+  // Stage barrier: LDS writes complete (lgkmcnt) + s_barrier.  Not
+  // __syncthreads(): its fence would also drain W3's register-staged global
+  // loads (vmcnt), which are meant to stay in flight across the barrier.
+#define PLL_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#ifdef FMX_STAMPS
+  unsigned long long pw_work = 0, pw_wait = 0, pw_last = __builtin_amdgcn_s_memtime();
+#define PLL_SYNC()                                                   \
+  {                                                                  \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
+    pw_work += t_ - pw_last;                                         \
+    PLL_BARRIER();                                                   \
+    pw_last = __builtin_amdgcn_s_memtime();                          \
+    pw_wait += pw_last - t_;                                         \
+  }
+#define PLL_STAMP_OUT()                                              \
+  if (a.dbg && (threadIdx.x & 63) == 0) {                            \
+    atomicAdd(a.dbg + 2 * (threadIdx.x >> 6), pw_work);              \
+    atomicAdd(a.dbg + 2 * (threadIdx.x >> 6) + 1, pw_wait);          \
+  }
+#else
+#define PLL_SYNC() PLL_BARRIER();
+#define PLL_STAMP_OUT()
+#endif
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
@@ -1026,67 +1088,76 @@ __global__ __launch_bounds__(256) void k_pll(PllArgs a) {
     sh->s2_flags[tid] = f;
     sh->s2_gate[tid] = g;
   }
-  if (wave == 1) pll_load_in(a, sh, 0, c0, 0, min(PLL_T, n), lane, vec);
+  if (wave == 4) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
   __syncthreads();
 
   const int c = c0 + lane;
   const bool act = c < a.C;
+  const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
+  // block-end values gathered for W0, after the loop (aliases the pilot tiles)
+  float(*fin)[PLL_CH] = reinterpret_cast<float(*)[PLL_CH]>(&sh->inp[0][0][0]);
   if (wave == 0) {
-    // ---------------- stage 1: the feedback recursions ----------------
-    FmxStereoState s = act ? a.st[c] : FmxStereoState{};
-    const float nominal = D->nominal, pmin = D->pll_min, pmax = D->pll_max;
+    // ---------------- W0: the PLL feedback chain ----------------
+    uint32_t theta = s0.theta, dtheta = s0.dtheta;
     const float alpha = D->pll_alpha, beta = D->pll_beta;
-    float phaseNow = d_nco_phase(s.theta);
     float vcoQ, vcoI;
-    sincosf(phaseNow, &vcoQ, &vcoI);
-    for (int k = 0; k < NT + 2; ++k) {
+    fmx_sincos(d_nco_phase(theta), &vcoQ, &vcoI);
+    for (int k = 0; k < NT + 3; ++k) {
       if (k < NT) {
         const int cnt = min(PLL_T, n - k * PLL_T);
-        const int ib = k & 1, sb = k % 3;
-        float pv[PLL_T], mv[PLL_T];
+        const int ib = k % 3, ob = k & 1;
+        float pv[PLL_T];
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 x = *reinterpret_cast<const float4 *>(&sh->in[ib][0][lane][4 * q]);
-          const float4 y = *reinterpret_cast<const float4 *>(&sh->in[ib][1][lane][4 * q]);
+          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[ib][lane][4 * q]);
           pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
-          mv[4 * q] = y.x; mv[4 * q + 1] = y.y; mv[4 * q + 2] = y.z; mv[4 * q + 3] = y.w;
         }
+        float ph[PLL_T], sq[PLL_T], cq[PLL_T];
 #pragma unroll
         for (int t = 0; t < PLL_T; ++t) {
           if (t < cnt) {
-            const float pilot = pv[t];
-            const float mpx = mv[t];
-            s.pilot_band_mag = (s.pilot_band_mag * kS) + (fabsf(pilot) * kI);
-            s.mpx_mag = (s.mpx_mag * kS) + (fabsf(mpx) * kI);
-            const float err = pilot * vcoQ;
-            s.dtheta += d_nco_constrain(err * alpha);
-            s.theta += d_nco_constrain(err * beta);
-            s.theta += s.dtheta;
-            const float phaseNext = d_nco_phase(s.theta);
-            float dphi = phaseNext - phaseNow;
-            if (dphi > kPiF) dphi -= 2.0f * kPiF;
-            else if (dphi < -kPiF) dphi += 2.0f * kPiF;
-            s.pll_freq = d_clamp(dphi, pmin, pmax);
-            s.pilot_i = (s.pilot_i * kS) + ((pilot * vcoI) * kI);
-            s.pilot_q = (s.pilot_q * kS) + ((pilot * vcoQ) * kI);
+            const float err = pv[t] * vcoQ;
+            dtheta += d_nco_constrain(err * alpha);
+            theta += d_nco_constrain(err * beta);
+            theta += dtheta;
+            const float phaseNext = d_nco_phase(theta);
             float sN, cN;
-            sincosf(phaseNext, &sN, &cN);
-            sh->slot[sb][F_PBM][lane][t] = s.pilot_band_mag;
-            sh->slot[sb][F_MM][lane][t] = s.mpx_mag;
-            sh->slot[sb][F_MAG2][lane][t] = (s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q);
-            sh->slot[sb][F_FREQ][lane][t] = s.pll_freq;
-            sh->slot[sb][F_COS2][lane][t] = (cN * cN) - (sN * sN);
-            phaseNow = phaseNext;
-            vcoI = cN;
+            fmx_sincos(phaseNext, &sN, &cN); // both polynomials are needed for the quadrant anyway
             vcoQ = sN;
+            ph[t] = phaseNext;
+            sq[t] = sN;
+            cq[t] = cN;
+          } else {
+            ph[t] = sq[t] = cq[t] = 0.0f;
           }
         }
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          *reinterpret_cast<float4 *>(&sh->s0[ob][0][lane][4 * q]) =
+              make_float4(ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
+          *reinterpret_cast<float4 *>(&sh->s0[ob][1][lane][4 * q]) =
+              make_float4(sq[4 * q], sq[4 * q + 1], sq[4 * q + 2], sq[4 * q + 3]);
+          *reinterpret_cast<float4 *>(&sh->s0[ob][2][lane][4 * q]) =
+              make_float4(cq[4 * q], cq[4 * q + 1], cq[4 * q + 2], cq[4 * q + 3]);
+        }
       }
-      __syncthreads();
+      PLL_SYNC()
     }
+    PLL_SYNC() // W1 / W3 block-end values in sh->fin
+    PLL_STAMP_OUT()
     if (!act) return;
-    s.pll_phase = phaseNow;
     // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
+    FmxStereoState s = s0;
+    s.theta = theta;
+    s.dtheta = dtheta;
+    s.pll_phase = d_nco_phase(theta);
+    s.pilot_band_mag = fin[0][lane];
+    s.mpx_mag = fin[1][lane];
+    s.pilot_i = fin[2][lane];
+    s.pilot_q = fin[3][lane];
+    s.pll_freq = fin[4][lane];
+    s.blend = fin[5][lane];
+    const float nominal = D->nominal;
     const FmxChanParam par = a.par[c];
     const bool fstereo = par.force_stereo != 0;
     const float fsf = (float)D->fs;
@@ -1122,27 +1193,141 @@ __global__ __launch_bounds__(256) void k_pll(PllArgs a) {
     int lvl = (int)roundf(calibrated * 750.0f);
     s.level = lvl < 0 ? 0 : (lvl > 750 ? 750 : lvl);
     s.detected = detected ? 1 : 0;
-    s.blend = sh->blend_out[lane];  // stage 3 owns blend (stored before the last barrier)
     a.st[c] = s;
     if (a.stereo_out) a.stereo_out[c] = s.detected;
     if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
   } else if (wave == 1) {
-    // ---------------- stage 3: blend recursion + outputs; loader ----------------
-    float blend = act ? a.st[c].blend : 0.0f;
-    const int mode = sh->s2_flags[lane] >> 8;
-    const float attack = D->blend_attack[mode], release = D->blend_release[mode];
-    for (int k = 0; k < NT + 2; ++k) {
-      const int kt = k - 2;
+    // ---------------- W1: envelopes, pilot I/Q, frequency, cos 2phi ----------------
+    float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q, freq = s0.pll_freq;
+    const float pmin = D->pll_min, pmax = D->pll_max;
+    float phaseNow = d_nco_phase(s0.theta);
+    float vcoQ, vcoI;
+    fmx_sincos(phaseNow, &vcoQ, &vcoI);
+    for (int k = 0; k < NT + 3; ++k) {
+      const int kt = k - 1;
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
-        const int sb = kt % 3;
+        const int ib = kt % 3, sb = kt & 1;
+        float pv[PLL_T], mv[PLL_T], ph[PLL_T], sq[PLL_T], cq[PLL_T];
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[ib][lane][4 * q]);
+          const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[kt & 1][lane][4 * q]);
+          const float4 z = *reinterpret_cast<const float4 *>(&sh->s0[sb][0][lane][4 * q]);
+          const float4 w = *reinterpret_cast<const float4 *>(&sh->s0[sb][1][lane][4 * q]);
+          const float4 u = *reinterpret_cast<const float4 *>(&sh->s0[sb][2][lane][4 * q]);
+          pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
+          mv[4 * q] = y.x; mv[4 * q + 1] = y.y; mv[4 * q + 2] = y.z; mv[4 * q + 3] = y.w;
+          ph[4 * q] = z.x; ph[4 * q + 1] = z.y; ph[4 * q + 2] = z.z; ph[4 * q + 3] = z.w;
+          sq[4 * q] = w.x; sq[4 * q + 1] = w.y; sq[4 * q + 2] = w.z; sq[4 * q + 3] = w.w;
+          cq[4 * q] = u.x; cq[4 * q + 1] = u.y; cq[4 * q + 2] = u.z; cq[4 * q + 3] = u.w;
+        }
+        float o_pbm[PLL_T], o_mm[PLL_T], o_mag2[PLL_T], o_fr[PLL_T], o_c2[PLL_T];
+#pragma unroll
+        for (int t = 0; t < PLL_T; ++t) {
+          if (t < cnt) {
+            const float pilot = pv[t];
+            pbm = (pbm * kS) + (fabsf(pilot) * kI);
+            mm = (mm * kS) + (fabsf(mv[t]) * kI);
+            const float phaseNext = ph[t];
+            const float dphi = d_unwrap(phaseNext - phaseNow);
+            freq = d_clamp(dphi, pmin, pmax);
+            pi_ = (pi_ * kS) + ((pilot * vcoI) * kI);
+            pq = (pq * kS) + ((pilot * vcoQ) * kI);
+            const float sN = sq[t], cN = cq[t]; // W0's sine / cosine of phaseNext
+            o_pbm[t] = pbm;
+            o_mm[t] = mm;
+            o_mag2[t] = (pi_ * pi_) + (pq * pq);
+            o_fr[t] = freq;
+            o_c2[t] = (cN * cN) - (sN * sN);
+            phaseNow = phaseNext;
+            vcoI = cN;
+            vcoQ = sN;
+          } else {
+            o_pbm[t] = o_mm[t] = o_mag2[t] = o_fr[t] = o_c2[t] = 0.0f;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const int t = 4 * q;
+          *reinterpret_cast<float4 *>(&sh->s1[sb][F_PBM][lane][t]) = make_float4(o_pbm[t], o_pbm[t + 1], o_pbm[t + 2], o_pbm[t + 3]);
+          *reinterpret_cast<float4 *>(&sh->s1[sb][F_MM][lane][t]) = make_float4(o_mm[t], o_mm[t + 1], o_mm[t + 2], o_mm[t + 3]);
+          *reinterpret_cast<float4 *>(&sh->s1[sb][F_MAG2][lane][t]) = make_float4(o_mag2[t], o_mag2[t + 1], o_mag2[t + 2], o_mag2[t + 3]);
+          *reinterpret_cast<float4 *>(&sh->s1[sb][F_FREQ][lane][t]) = make_float4(o_fr[t], o_fr[t + 1], o_fr[t + 2], o_fr[t + 3]);
+          *reinterpret_cast<float4 *>(&sh->s1[sb][F_COS2][lane][t]) = make_float4(o_c2[t], o_c2[t + 1], o_c2[t + 2], o_c2[t + 3]);
+        }
+      }
+      PLL_SYNC()
+    }
+    fin[0][lane] = pbm;
+    fin[1][lane] = mm;
+    fin[2][lane] = pi_;
+    fin[3][lane] = pq;
+    fin[4][lane] = freq;
+    PLL_SYNC()
+    PLL_STAMP_OUT()
+  } else if (wave == 4) {
+    // ---------------- W3: blend recursion + outputs; loader ----------------
+    float blend = s0.blend;
+    const int mode = sh->s2_flags[lane] >> 8;
+    const float attack = D->blend_attack[mode], release = D->blend_release[mode];
+    // loads staged in registers one iteration ahead, across the barrier:
+    // iteration k stores pilot tile k+1, mpx tile k and delay tile k-1 (for
+    // W0, W1 and W2 at iteration k+1), then issues pilot k+2, mpx k+1, delay k
+    PllStage stp, stm;
+    PllDlyStage std_;
+#ifdef FMX_STAMPS
+    unsigned long long w3acc[2] = {0, 0}, w3last = 0;
+#define W3_STAMP(i)                                              \
+  {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+    if (i == 0) { w3last = t_; w3acc[1] += t_ - pw_last; }       \
+    else w3acc[0] += t_ - w3last;                                \
+  }
+#else
+#define W3_STAMP(i)
+#endif
+    auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
+    auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
+    const int rows_valid = min(PLL_CH, a.C - c0);
+    const __amdgpu_buffer_rsrc_t rp =
+        make_rsrc(a.pilot + (size_t)c0 * a.pilot_stride, (uint32_t)((size_t)rows_valid * a.pilot_stride * 4));
+    const __amdgpu_buffer_rsrc_t rm =
+        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, (uint32_t)((size_t)rows_valid * a.mpx_stride * 4));
+    const __amdgpu_buffer_rsrc_t rh =
+        make_rsrc(a.st_hist_rd + (size_t)c0 * FMX_HIST, (uint32_t)((size_t)rows_valid * FMX_HIST * 4));
+    // retire every load made so far (blend, attack, release): otherwise the
+    // waitcnt pass, merging states at the loop header, drains the staged
+    // tile loads (vmcnt(0)) at their first use inside the loop
+    __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
+    if (full(1)) stp.issue(rp, a.pilot_stride, PLL_T, lane);
+    if (full(0)) stm.issue(rm, a.mpx_stride, 0, lane);
+    for (int k = 0; k < NT + 3; ++k) {
+      if (k + 1 < NT) {
+        if (full(k + 1)) stp.store(sh->inp[(k + 1) % 3], lane);
+        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[(k + 1) % 3], c0, (k + 1) * PLL_T, tcnt(k + 1), lane);
+      }
+      if (k < NT) {
+        if (full(k)) stm.store(sh->inm[k & 1], lane);
+        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[k & 1], c0, k * PLL_T, tcnt(k), lane);
+      }
+      if (k - 1 >= 0 && k - 1 < NT) std_.store(sh->dly[(k - 1) & 1], lane);
+      W3_STAMP(0)
+      if (full(k + 2)) stp.issue(rp, a.pilot_stride, (k + 2) * PLL_T, lane);
+      if (full(k + 1)) stm.issue(rm, a.mpx_stride, (k + 1) * PLL_T, lane);
+      if (k < NT) std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
+      W3_STAMP(1)
+      const int kt = k - 3;
+      if (kt >= 0 && kt < NT) {
+        const int cnt = min(PLL_T, n - kt * PLL_T);
+        const int sb = kt & 1;
         float ov[2][PLL_T];
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 tg = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_TGT][lane][4 * q]);
-          const float4 mo = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_MONO][lane][4 * q]);
-          const float4 dl = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_DL][lane][4 * q]);
-          const float4 dr = *reinterpret_cast<const float4 *>(&sh->slot[sb][F_DR][lane][4 * q]);
+          const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lane][4 * q]);
+          const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lane][4 * q]);
+          const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lane][4 * q]);
+          const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lane][4 * q]);
           const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
           const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
 #pragma unroll
@@ -1154,48 +1339,64 @@ __global__ __launch_bounds__(256) void k_pll(PllArgs a) {
               blend += (tgt - blend) * ba;
               ov[0][t] = moa[u] + (dla[u] * blend);
               ov[1][t] = moa[u] + (dra[u] * blend);
+            } else {
+              ov[0][t] = ov[1][t] = 0.0f;
             }
           }
         }
         if (act) {
           float *ol = a.lraw + (size_t)c * a.lr_stride + kt * PLL_T;
           float *orr = a.rraw + (size_t)c * a.lr_stride + kt * PLL_T;
+          if (cnt == PLL_T && ((((uintptr_t)ol) | ((uintptr_t)orr)) & 15) == 0) {
 #pragma unroll
-          for (int t = 0; t < PLL_T; ++t) {
-            if (t < cnt) {
-              ol[t] = ov[0][t];
-              orr[t] = ov[1][t];
+            for (int q = 0; q < PLL_T / 4; ++q) {
+              reinterpret_cast<float4 *>(ol)[q] = make_float4(ov[0][4 * q], ov[0][4 * q + 1], ov[0][4 * q + 2], ov[0][4 * q + 3]);
+              reinterpret_cast<float4 *>(orr)[q] = make_float4(ov[1][4 * q], ov[1][4 * q + 1], ov[1][4 * q + 2], ov[1][4 * q + 3]);
+            }
+          } else {
+#pragma unroll
+            for (int t = 0; t < PLL_T; ++t) {
+              if (t < cnt) {
+                ol[t] = ov[0][t];
+                orr[t] = ov[1][t];
+              }
             }
           }
         }
       }
-      if (k == NT + 1) sh->blend_out[lane] = blend;
-      // loader: S1 input of tile k+1, delay-line tile k for S2
-      if (k + 1 < NT) pll_load_in(a, sh, (k + 1) & 1, c0, (k + 1) * PLL_T, min(PLL_T, n - (k + 1) * PLL_T), lane, vec);
-      if (k < NT) pll_load_dly(a, sh, k & 1, c0, k * PLL_T, min(PLL_T, n - k * PLL_T), lane, Dly);
-      __syncthreads();
+      PLL_SYNC()
     }
+    fin[5][lane] = blend;
+    PLL_SYNC()
+    PLL_STAMP_OUT()
+#ifdef FMX_STAMPS
+    if (a.dbg && lane == 0) {
+      atomicAdd(a.dbg + 10, w3acc[0]);
+      atomicAdd(a.dbg + 11, w3acc[1]);
+    }
+#endif
+#undef W3_STAMP
   } else {
-    // ---------------- stage 2: time-parallel work ----------------
+    // ---------------- W2a/W2b: time-parallel work ----------------
     const int t2 = tid - 128;  // 0..127
     const float nominal = D->nominal;
     const float fsf = (float)D->fs;
-    for (int k = 0; k < NT + 2; ++k) {
-      const int kt = k - 1;
+    for (int k = 0; k < NT + 3; ++k) {
+      const int kt = k - 2;
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
-        const int sb = kt % 3, db = kt & 1;
+        const int sb = kt & 1;
 #pragma unroll 2
         for (int j = 0; j < PLL_CH * PLL_T / 128; ++j) {
           const int idx = t2 + 128 * j;
           const int row = idx / PLL_T, t = idx % PLL_T;
           const int fl = sh->s2_flags[row];
-          const float pbm = sh->slot[sb][F_PBM][row][t];
-          const float mm = sh->slot[sb][F_MM][row][t];
-          const float mag2 = sh->slot[sb][F_MAG2][row][t];
-          const float pf = sh->slot[sb][F_FREQ][row][t];
-          const float cos2 = sh->slot[sb][F_COS2][row][t];
-          const float delayed = sh->dly[db][row][t];
+          const float pbm = sh->s1[sb][F_PBM][row][t];
+          const float mm = sh->s1[sb][F_MM][row][t];
+          const float mag2 = sh->s1[sb][F_MAG2][row][t];
+          const float pf = sh->s1[sb][F_FREQ][row][t];
+          const float cos2 = sh->s1[sb][F_COS2][row][t];
+          const float delayed = sh->dly[sb][row][t];
           float tgt;
           if (fl & 1) tgt = 0.0f;
           else if (fl & 2) tgt = 1.0f;
@@ -1212,16 +1413,21 @@ __global__ __launch_bounds__(256) void k_pll(PllArgs a) {
           const float sl = (delayed + lr) * 0.5f;
           const float sr = (delayed - lr) * 0.5f;
           if (t < cnt) {
-            sh->slot[sb][F_TGT][row][t] = tgt;
-            sh->slot[sb][F_MONO][row][t] = monoNorm;
-            sh->slot[sb][F_DL][row][t] = sl - monoNorm;
-            sh->slot[sb][F_DR][row][t] = sr - monoNorm;
+            sh->s2[sb][F_TGT][row][t] = tgt;
+            sh->s2[sb][F_MONO][row][t] = monoNorm;
+            sh->s2[sb][F_DL][row][t] = sl - monoNorm;
+            sh->s2[sb][F_DR][row][t] = sr - monoNorm;
           }
         }
       }
-      __syncthreads();
+      PLL_SYNC()
     }
+    PLL_SYNC()
+    PLL_STAMP_OUT()
   }
+#undef PLL_SYNC
+#undef PLL_STAMP_OUT
+#undef PLL_BARRIER
 }
 
 /* ================================================================== */
@@ -1478,17 +1684,33 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
          ((uint32_t)bs_block_number(ooff) + d / 26) % 4 == (uint32_t)bs_block_number(off);
 }
 
-// k_rds input tiles: RDS_TW samples per channel, advanced by 64 with an
-// RDS_TW-64 sample overlap so a chunk of 8 never straddles two tiles.
-#define RDS_TW 72
+// k_rds input tiles: 64 samples x 64 channels, filled by 16-B LDS-DMA.
+// One DMA instruction writes a 1-KiB piece = 4 channel rows of 16 segments
+// of 4 samples; piece p holds rows 4p..4p+3, row q at dword q*64, its
+// segment s rotated to slot (s + 4q) & 15, pieces RDS_PIECE dwords apart.
+// A wave reading one segment per lane (lane = row) then hits all 64 banks
+// once per 16 lanes (conflict-free ds_read_b128).
+#define RDS_PIECE 260
+#define RDS_SYMQ 48 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
+// Per-lane state lives in LDS (odd dword stride: conflict-free across lanes);
+// only the per-sample quantities (NCO, FIR partial sums, AGC, symsync
+// scalars) are held in registers.  Block sync / biphase state is touched once
+// per symbol.
+struct RdsCold {
+  FmxRdsState s;
+  uint32_t pad_;
+};
+static_assert((sizeof(RdsCold) / 4) % 2 == 1, "RdsCold must have an odd dword stride");
 struct RdsLds {
-  float taps[24][12];
+  float taps[24][12] __attribute__((aligned(16))); // row jp: h[jp + 24 i], i = 0..10, zero pad
   float mf[FMX_NPFB * FMX_SS_SUB];
   float dmf[FMX_NPFB * FMX_SS_SUB];
   uint32_t esyn[5][52];
   uint32_t eerr[5][52];
-  float tin[64][RDS_TW + 1]; // 64 channels x RDS_TW samples (odd row stride: conflict-free column reads)
-  int cnt[64];
+  float tin[2][16 * RDS_PIECE]; // double-buffered tiles of 64 samples x 64 channels (rds_tile_* layout)
+  f32x2 win[2 * FMX_SS_SUB][64]; // symsync window ring per lane: sample at p and p + 18
+  float symq[RDS_SYMQ][64];      // symbols (real part) awaiting biphase / block sync
+  RdsCold cold[64];
 };
 
 __device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
@@ -1512,12 +1734,13 @@ __device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a,
   ng++;
 }
 
+// BlockStream::pushBit / findBlockInInputRegister / acquireSync
+// (block_sync.cpp:235-313) and Group::setBlock (group.cpp:103-128)
 __device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
   s.bs_reg = (s.bs_reg << 1u) + (uint32_t)bit;
   s.bs_until_next--;
   s.bs_bitcount++;
   if (s.bs_until_next != 0) return;
-  // findBlockInInputRegister
   const uint32_t raw = s.bs_reg & ((1u << 26) - 1u);
   const uint32_t syn = bs_syndrome(raw);
   int off = bs_offset_for(syn);
@@ -1532,9 +1755,7 @@ __device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsL
       s.bs_pulse_off[3] = off;
       s.bs_pulse_pos[3] = s.bs_bitcount;
       bool found = false;
-#pragma unroll
       for (int i = 0; i < 2; ++i)
-#pragma unroll
         for (int j = i + 1; j < 3; ++j)
           found = found ||
                   (pulse_follows(s.bs_pulse_pos[3], s.bs_pulse_off[3], s.bs_pulse_pos[j], s.bs_pulse_off[j]) &&
@@ -1584,13 +1805,9 @@ __device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsL
       }
       if (off == s.bs_expected) {
         const int bn = bs_block_number(s.bs_expected);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (i == bn) {
-            s.bs_blk_raw[i] = raw;
-            s.bs_blk_data[i] = data;
-            s.bs_blk_flags[i] = (uint8_t)(1 | (had ? 2 : 0));
-          }
+        s.bs_blk_raw[bn] = raw;
+        s.bs_blk_data[bn] = data;
+        s.bs_blk_flags[bn] = (uint8_t)(1 | (had ? 2 : 0));
       }
       const int next = bs_next(s.bs_expected);
       if (next == OA) {
@@ -1607,8 +1824,35 @@ __device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsL
   s.bs_until_next = s.bs_in_sync ? 26u : 1u;
 }
 
+/* k_rds: one lane per channel, 64 channels per workgroup (one wave).  The
+ * per-sample chain of SubcarrierSet::processSample (subcarrier.cpp:153-235,
+ * liquid_wrappers.cpp:125-139,271-353) in the reference's order:
+ *   mix x * polar(1, -phase0)            (fmx_sincos)
+ *   255-tap FIR push: 11 streaming partial sums acc[i] (the i-th next
+ *   decimation instant), accumulated oldest -> newest exactly as the
+ *   window dot product, with packed (re, im) multiplies and adds
+ *   every 24th sample: FIR output -> AGC -> symsync (MF / dMF in an LDS ring)
+ *   -> PSK2 phase error -> NCO PLL -> biphase -> delta -> block sync
+ *   NCO step + quad-phase wrapper.
+ * When every lane of the wave shares the decimation phase (all channels in
+ * step, the normal case) the samples run in chunks of 8 (three per FIR
+ * period): the 7 NCO phases with no PLL update in between are evaluated
+ * independently, only their wrapped sum is serial, then 8 sincos and the
+ * partial sums with wave-uniform (LDS broadcast) tap rows. */
 __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   __shared__ RdsLds L;
+#ifdef FMX_STAMPS
+  unsigned long long rs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long rs_last = __builtin_amdgcn_s_memtime();
+#define RDS_STAMP(k)                                      \
+  if (a.dbg) {                                            \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    rs_acc[k] += t_ - rs_last;                            \
+    rs_last = t_;                                         \
+  }
+#else
+#define RDS_STAMP(k)
+#endif
   const int lane = threadIdx.x;
   const int c0 = blockIdx.x * 64;
   const int c = c0 + lane;
@@ -1635,150 +1879,160 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
         idx++;
       }
   }
-  FmxRdsState s;
+  FmxRdsState &S = L.cold[lane].s;
   int count = 0;
   if (act) {
-    s = a.st[c];
+    S = a.st[c];
     count = a.in_count[c];
+  } else {
+    S = FmxRdsState{};
   }
-  __syncthreads();
   float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
-  if (act && s.rebuild) {
+  // ---- hot state -> registers ----
+  uint32_t theta = S.theta, dtheta = S.dtheta, ssr = S.sample_since_reset;
+  float prev_f0 = S.prev_f0, phase0 = S.phase0;
+  f32x2 acc[FMX_RDS_NACC];
+  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{S.acc_re[i], S.acc_im[i]};
+  float agc_g = S.agc_g, agc_y2p = S.agc_y2p;
+  float ss_rate = S.ss_rate, ss_del = S.ss_del, ss_tau = S.ss_tau, ss_q_hat = S.ss_q_hat, ss_v1 = S.ss_v1;
+  int ss_b = S.ss_b, ss_decim = S.ss_decim, ss_valid = S.ss_mf_valid;
+  for (int m = 0; m < FMX_SS_SUB; ++m) {
+    const f32x2 w = f32x2{S.ss_win_re[m], S.ss_win_im[m]};
+    L.win[m][lane] = w;
+    L.win[m + FMX_SS_SUB][lane] = w;
+  }
+  int wp = FMX_SS_SUB - 1; // newest window sample at wp (and wp + 18)
+  if (act && S.rebuild) {
     // decimation phase changed by a reset: rebuild the partial sums from the
     // last mixed samples (the reference's FIR window survives the reset)
-#pragma unroll
     for (int i = 0; i < FMX_RDS_NACC; ++i) {
       float ar = 0.0f, ai = 0.0f;
       for (int kp = FMX_RDS_FIR - 1 - 24 * i; kp >= 1; --kp) {
-        const uint32_t idx = (s.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
+        const uint32_t idx = (S.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
         const float h = D->rds_fir[24 * i + kp];
         const float pr = h * ring[2 * idx];
         const float pi = h * ring[2 * idx + 1];
         ar = ar + pr;
         ai = ai + pi;
       }
-      s.acc_re[i] = ar;
-      s.acc_im[i] = ai;
+      acc[i] = f32x2{ar, ai};
     }
-    s.rebuild = 0;
+    S.rebuild = 0;
   }
   int ng = 0;
-  const float fscale = D->rds_fir_scale;
+  const f32x2 fscale2 = f32x2{D->rds_fir_scale, D->rds_fir_scale};
   const float agc_bw = D->agc_bw;
   const float ss_b0 = D->ss_b0, ss_a1 = D->ss_a1, ss_adj = D->ss_rate_adj;
   const float psk_xr1 = D->psk_xr1, psk_xi1 = D->psk_xi1;
   const float alpha = D->rds_alpha, beta = D->rds_beta;
   const float dphi_psk = (float)(3.14159265358979323846 * (1.0 - 1.0 / 2));
-  const uint32_t ring0 = s.ring_pos;
+  const uint32_t ring0 = S.ring_pos;
+  int nmax = count, cmin = act ? count : 0x7fffffff;
+  for (int d = 32; d >= 1; d >>= 1) {
+    nmax = max(nmax, __shfl_xor(nmax, d));
+    cmin = min(cmin, __shfl_xor(cmin, d));
+  }
+  const int ring_from = cmin - FMX_RDS_RING;
+  int nq = 0;
+  float last_symi = 0.0f;
 
   // one mixed sample into the 11 streaming partial sums (reference order)
-  auto acc_add = [&](float mr, float mi, int t, const float *tp, int tstride) __attribute__((always_inline)) {
+  auto acc_add = [&](f32x2 m, int t, const float *tp) __attribute__((always_inline)) {
+    const float4 h0 = *reinterpret_cast<const float4 *>(tp);
+    const float4 h1 = *reinterpret_cast<const float4 *>(tp + 4);
+    const float4 h2 = *reinterpret_cast<const float4 *>(tp + 8);
+    const float h[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
 #pragma unroll
     for (int i = 0; i < FMX_RDS_NACC; ++i) {
-      const float h = tp[i * tstride];
-      const float pr = h * mr, pi = h * mi;
-      s.acc_re[i] = s.acc_re[i] + pr;
-      s.acc_im[i] = s.acc_im[i] + pi;
+      const f32x2 p = f32x2{h[i], h[i]} * m;
+      acc[i] = acc[i] + p;
     }
-    if (t >= count - FMX_RDS_RING) {
-      const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
-      ring[2 * idx] = mr;
-      ring[2 * idx + 1] = mi;
+    if (t >= ring_from) { // wave-uniform test first: only the last FMX_RDS_RING samples are kept
+      if (t >= count - FMX_RDS_RING) {
+        const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
+        *reinterpret_cast<f32x2 *>(ring + 2 * idx) = m;
+      }
     }
   };
-  auto mix_acc = [&](float x, int t, const float *tp, int tstride) __attribute__((always_inline)) {
+  auto mix = [&](float x, float ph) __attribute__((always_inline)) {
     float sn, cs;
-    sincosf(-s.phase0, &sn, &cs);
-    acc_add(x * cs, x * sn, t, tp, tstride);
+    fmx_sincos(-ph, &sn, &cs);
+    return f32x2{x, x} * f32x2{cs, sn};
   };
   // NCO step + quad-phase wrapper (liquid_wrappers.cpp:271-312)
   auto nco_step = [&]() __attribute__((always_inline)) {
-    s.theta += s.dtheta;
-    const float now = d_nco_phase(s.theta);
-    float delta = now - s.prev_f0;
-    if (delta > kPiF) delta = delta - 2.f * kPiF;
-    else if (delta < -kPiF) delta = delta + 2.f * kPiF;
-    s.prev_f0 = now;
+    theta += dtheta;
+    const float now = d_nco_phase(theta);
+    float delta = now - prev_f0;
+    delta = d_unwrap(delta);
+    prev_f0 = now;
     const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
-    float ph = s.phase0 + scaled;
-    if (ph > kPiF) ph = ph - 2.f * kPiF;
-    else if (ph < -kPiF) ph = ph + 2.f * kPiF;
-    s.phase0 = ph;
-    s.sample_since_reset++;
+    float ph = phase0 + scaled;
+    ph = d_unwrap(ph);
+    phase0 = ph;
+    ssr++;
   };
   // FIR output (every 24th sample) -> AGC -> symsync -> PSK2 PLL -> bits
   auto fir_output = [&]() __attribute__((always_inline)) {
-    const float fr = s.acc_re[0] * fscale, fi = s.acc_im[0] * fscale;
+    const f32x2 f = acc[0] * fscale2;
 #pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC - 1; ++i) {
-      s.acc_re[i] = s.acc_re[i + 1];
-      s.acc_im[i] = s.acc_im[i + 1];
-    }
-    s.acc_re[FMX_RDS_NACC - 1] = 0.0f;
-    s.acc_im[FMX_RDS_NACC - 1] = 0.0f;
-    const float yr = fr * s.agc_g, yi = fi * s.agc_g;
+    for (int i = 0; i < FMX_RDS_NACC - 1; ++i) acc[i] = acc[i + 1];
+    acc[FMX_RDS_NACC - 1] = f32x2{0.0f, 0.0f};
+    const float yr = f.x * agc_g, yi = f.y * agc_g;
     const float y2 = yr * yr + yi * yi;
-    s.agc_y2p = (float)((1.0 - (double)agc_bw) * (double)s.agc_y2p + (double)(agc_bw * y2));
-    if (s.agc_y2p > 1e-6f) s.agc_g *= expf(-0.5f * agc_bw * logf(s.agc_y2p));
-    if (s.agc_g > 1e6f) s.agc_g = 1e6f;
-    // ---- symsync ----
-#pragma unroll
-    for (int m = 0; m < FMX_SS_SUB - 1; ++m) {
-      s.ss_win_re[m] = s.ss_win_re[m + 1];
-      s.ss_win_im[m] = s.ss_win_im[m + 1];
-    }
-    s.ss_win_re[FMX_SS_SUB - 1] = yr;
-    s.ss_win_im[FMX_SS_SUB - 1] = yi;
-    if (s.ss_mf_valid < FMX_SS_SUB) s.ss_mf_valid++;
+    agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
+    if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
+    if (agc_g > 1e6f) agc_g = 1e6f;
+    // ---- symsync: push into both MF banks' window ----
+    wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
+    L.win[wp][lane] = f32x2{yr, yi};
+    L.win[wp + FMX_SS_SUB][lane] = f32x2{yr, yi};
+    if (ss_valid < FMX_SS_SUB) ss_valid++;
+    const int w0 = wp + 1; // oldest
     int ns = 0;
-    float symr = 0.0f, symi = 0.0f;
-    while (s.ss_b < FMX_NPFB && ns < 16) {
-      const float *hm = L.mf + s.ss_b * FMX_SS_SUB;
-      float ar = 0.0f, ai = 0.0f;
-      const int first = FMX_SS_SUB - s.ss_mf_valid;
+    f32x2 sym = f32x2{0.0f, 0.0f};
+    while (ss_b < FMX_NPFB && ns < 16) {
+      const float *hm = L.mf + ss_b * FMX_SS_SUB;
+      f32x2 acm = f32x2{0.0f, 0.0f};
+      const int first = FMX_SS_SUB - ss_valid;
 #pragma unroll
       for (int m = 0; m < FMX_SS_SUB; ++m) {
         const float h = hm[FMX_SS_SUB - 1 - m];
-        const float wr = (m >= first) ? s.ss_win_re[m] : 0.0f;
-        const float wi = (m >= first) ? s.ss_win_im[m] : 0.0f;
-        const float pr = h * wr, pi = h * wi;
-        ar = ar + pr;
-        ai = ai + pi;
+        const f32x2 w = (m >= first) ? L.win[w0 + m][lane] : f32x2{0.0f, 0.0f};
+        const f32x2 p = f32x2{h, h} * w;
+        acm = acm + p;
       }
-      if (ns == 0) {
-        symr = ar / 3.0f;
-        symi = ai / 3.0f;
-      }
-      if (s.ss_decim == 1) {
-        s.ss_decim = 0;
-        const float *hd = L.dmf + s.ss_b * FMX_SS_SUB;
-        float dr = 0.0f, di = 0.0f;
+      if (ns == 0) sym = f32x2{acm.x / 3.0f, acm.y / 3.0f};
+      if (ss_decim == 1) {
+        ss_decim = 0;
+        const float *hd = L.dmf + ss_b * FMX_SS_SUB;
+        f32x2 acd = f32x2{0.0f, 0.0f};
 #pragma unroll
         for (int m = 0; m < FMX_SS_SUB; ++m) {
           const float h = hd[FMX_SS_SUB - 1 - m];
-          const float pr = h * s.ss_win_re[m], pi = h * s.ss_win_im[m];
-          dr = dr + pr;
-          di = di + pi;
+          const f32x2 p = f32x2{h, h} * L.win[w0 + m][lane];
+          acd = acd + p;
         }
-        float q = ar * dr + ai * di;
+        float q = acm.x * acd.x + acm.y * acd.y;
         if (q > 1.0f) q = 1.0f;
         else if (q < -1.0f) q = -1.0f;
-        const float t1 = ss_a1 * s.ss_v1;
+        const float t1 = ss_a1 * ss_v1;
         const float v0 = q - t1;
-        s.ss_q_hat = ss_b0 * v0;
-        s.ss_v1 = v0;
-        s.ss_rate += ss_adj * s.ss_q_hat;
-        s.ss_del = s.ss_rate + s.ss_q_hat;
+        ss_q_hat = ss_b0 * v0;
+        ss_v1 = v0;
+        ss_rate += ss_adj * ss_q_hat;
+        ss_del = ss_rate + ss_q_hat;
       }
-      s.ss_decim++;
-      s.ss_tau += s.ss_del;
-      s.ss_b = (int)roundf(s.ss_tau * (float)FMX_NPFB);
+      ss_decim++;
+      ss_tau += ss_del;
+      ss_b = (int)roundf(ss_tau * (float)FMX_NPFB);
       ns++;
     }
-    s.ss_tau -= 1.0f;
-    s.ss_b -= FMX_NPFB;
+    ss_tau -= 1.0f;
+    ss_b -= FMX_NPFB;
     if (ns == 1) {
       // ---- PSK2 modem phase error -> NCO PLL ----
+      const float symr = sym.x, symi = sym.y;
       float th = atan2f(symi, symr) - dphi_psk;
       if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
       const bool s1 = th > 0.0f;
@@ -1786,163 +2040,245 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
       float pe = symi * xr - symr * xi;
       pe = d_clamp(pe, -kPiF, kPiF);
       const float dphi = pe * 12.0f;
-      s.dtheta += d_nco_constrain(dphi * alpha);
-      s.theta += d_nco_constrain(dphi * beta);
-      // ---- biphase + delta ----
-      const float bir = (symr - s.bi_prev_re) * 0.5f;
+      dtheta += d_nco_constrain(dphi * alpha);
+      theta += d_nco_constrain(dphi * beta);
+      // biphase / delta / block sync only consume symbols: queue them and
+      // run those decoders outside the sample loop (flush_symbols)
+      L.symq[nq][lane] = symr;
+      last_symi = symi;
+      nq++;
+    }
+  };
+  // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued symbols
+  auto flush_symbols = [&]() __attribute__((always_inline)) {
+    const int nrun = act ? nq : 0; // lanes past C run the DSP in lockstep but decode nothing
+    for (int k = 0; k < nrun; ++k) {
+      const float symr = L.symq[k][lane];
+      const float bir = (symr - S.bi_prev_re) * 0.5f;
       const int val = bir >= 0.0f;
-      const bool has = (s.bi_clock % 2u) == s.bi_polarity;
-      s.bi_prev_re = symr;
-      s.bi_prev_im = symi;
-      if ((s.bi_clock & 1u) == 0) s.bi_even += fabsf(bir);
-      else s.bi_odd += fabsf(bir);
-      s.bi_clock++;
-      if (s.bi_clock == 128u) {
-        if (s.bi_even > s.bi_odd) s.bi_polarity = 0;
-        else if (s.bi_odd > s.bi_even) s.bi_polarity = 1;
-        s.bi_even = 0.0f;
-        s.bi_odd = 0.0f;
-        s.bi_clock = 0;
+      const bool has = (S.bi_clock % 2u) == S.bi_polarity;
+      S.bi_prev_re = symr;
+      if ((S.bi_clock & 1u) == 0) S.bi_even += fabsf(bir);
+      else S.bi_odd += fabsf(bir);
+      S.bi_clock++;
+      if (S.bi_clock == 128u) {
+        if (S.bi_even > S.bi_odd) S.bi_polarity = 0;
+        else if (S.bi_odd > S.bi_even) S.bi_polarity = 1;
+        S.bi_even = 0.0f;
+        S.bi_odd = 0.0f;
+        S.bi_clock = 0;
       }
       if (has) {
-        const int bit = (val != s.delta_prev) ? 1 : 0;
-        s.delta_prev = val;
-        rds_push_bit(s, bit, L, a, c, ng);
+        const int bit = (val != S.delta_prev) ? 1 : 0;
+        S.delta_prev = val;
+        rds_push_bit(S, bit, L, a, c, ng);
       }
     }
+    if (nq > 0) S.bi_prev_im = last_symi;
+    nq = 0;
   };
-  // Inputs are staged in LDS in tiles of 64 samples x 64 channels with
-  // coalesced loads; all lanes sit at the same sample index t.
-  int nmax = count, cmin = act ? count : 0x7fffffff;
-  for (int d = 32; d >= 1; d >>= 1) {
-    nmax = max(nmax, __shfl_xor(nmax, d));
-    cmin = min(cmin, __shfl_xor(cmin, d));
-  }
-  // Tiles [tb, tb + RDS_TW) of 64 channels are staged in LDS; the next 64
-  // samples of every row are prefetched into registers (one coalesced 256-B
-  // row per load, 64 loads in flight) while the current tile is consumed.
-  if (lane < 64) L.cnt[lane] = (c0 + lane < a.C) ? a.in_count[c0 + lane] : 0;
+  // ---- input tiles [tb, tb + RDS_TW) of 64 channels in LDS; the next 64
+  // samples of every row prefetched into registers (one coalesced 256-B row
+  // per load, 64 loads in flight) while the current tile is consumed ----
   __syncthreads();
-  float pre[64];
-  auto prefetch = [&](int base) __attribute__((always_inline)) {
-    const int col = base + lane;
+  // Tile k = samples [64k, 64k + 64) of the 64 channels; tiles k and k+1 sit
+  // in L.tin[cur] / L.tin[cur ^ 1].  Tile k+2 is requested by LDS-DMA as soon
+  // as tile k is left behind.  Rows past C read as 0 (buffer range check).
+  const int rows_valid = min(64, a.C - c0);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + (size_t)c0 * a.in_stride,
+                                               (uint32_t)((size_t)rows_valid * a.in_stride * sizeof(float)));
+  const int my_row = (lane >> 2) * RDS_PIECE + (lane & 3) * 64; // dword of this lane's row in a tile
+  const int my_rot = (lane & 3) * 4;
+  // DMA lane i of a piece: row q = i / 16, slot i & 15 holds segment (slot - 4q) & 15
+  const uint32_t dma_lane_off =
+      (uint32_t)(((lane >> 4) * a.in_stride + 4 * (((lane & 15) - 4 * (lane >> 4)) & 15)) * 4);
+  auto dma_tile = [&](int buf, int base) __attribute__((always_inline)) {
+    uint32_t off = dma_lane_off + (uint32_t)base * 4u;
 #pragma unroll
-    for (int r = 0; r < 64; ++r) {
-      const int ch = c0 + r;
-      pre[r] = (ch < a.C && col < L.cnt[r]) ? a.in[(size_t)ch * a.in_stride + col] : 0.0f;
+    for (int p = 0; p < 16; ++p) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rin, (__attribute__((address_space(3))) void *)&L.tin[buf][p * RDS_PIECE], 16, off, 0, 0, 0);
+      off += (uint32_t)a.in_stride * 16u; // 4 rows
+      asm volatile("" : "+v"(off));
     }
   };
-  int tb = 0;  // sample index of L.tin[.][0]
-  prefetch(0);
-#pragma unroll
-  for (int r = 0; r < 64; ++r) L.tin[r][lane] = pre[r];
-  if (lane < RDS_TW - 64) {
-    for (int r = 0; r < 64; ++r) {
-      const int ch = c0 + r, col = 64 + lane;
-      L.tin[r][col] = (ch < a.C && col < L.cnt[r]) ? a.in[(size_t)ch * a.in_stride + col] : 0.0f;
-    }
-  }
-  prefetch(RDS_TW);
+  // segment g (0..31, counted from the start of tile cur) of this lane's row
+  auto seg_ptr = [&](int cur_, int g) __attribute__((always_inline)) {
+    return &L.tin[cur_ ^ (g >> 4)][my_row + (((g & 15) + my_rot) & 15) * 4];
+  };
+  RDS_STAMP(0)
+  int tb = 0, cur = 0; // sample index of L.tin[cur] column 0
+  dma_tile(0, 0);
+  dma_tile(1, 64);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // make [t, t + len) resident (t only moves forward, len <= RDS_TW - 64 + 1)
+  bool nxt_ok = true; // tile k+1 has landed
+  // make [t, t + len) resident (t moves forward, len <= 8)
   auto need = [&](int t, int len) __attribute__((always_inline)) {
-    while (t + len > tb + RDS_TW) {
-      // own row: overlap columns move to the front, then the prefetched 64
-      float keep[RDS_TW - 64];
-#pragma unroll
-      for (int k = 0; k < RDS_TW - 64; ++k) keep[k] = L.tin[lane][64 + k];
+    if (t >= tb + 64) {
+      RDS_STAMP(2)
+      // tile k is done: its buffer takes tile k+2
+      if (!nxt_ok) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-#pragma unroll
-      for (int k = 0; k < RDS_TW - 64; ++k) L.tin[lane][k] = keep[k];
-#pragma unroll
-      for (int r = 0; r < 64; ++r) L.tin[r][RDS_TW - 64 + lane] = pre[r];
+      dma_tile(cur, tb + 128);
       tb += 64;
-      prefetch(tb + RDS_TW);
-      __syncthreads();
+      cur ^= 1;
+      nxt_ok = false;
+      RDS_STAMP(1)
     }
+    if (t + len > tb + 64 && !nxt_ok) { // first read reaching into tile k+1
+      RDS_STAMP(2)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      nxt_ok = true;
+      RDS_STAMP(1)
+    }
+  };
+  auto read1 = [&](int t) __attribute__((always_inline)) {
+    const int d = t - tb;
+    return seg_ptr(cur, d >> 2)[d & 3];
   };
   // one sample for every lane that still has input: own tap row from LDS
   auto step_one = [&](int t) __attribute__((always_inline)) {
     need(t, 1);
     if (act && t < count) {
-      const int j = (int)(s.sample_since_reset % FMX_RDS_DECIM);
+      const int j = (int)(ssr % FMX_RDS_DECIM);
       const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
-      mix_acc(L.tin[lane][t - tb], t, &L.taps[jp][0], 1);
+      acc_add(mix(read1(t), phase0), t, &L.taps[jp][0]);
       if (j == 0) fir_output();
       nco_step();
     }
   };
-  const uint32_t j_mine = act ? (s.sample_since_reset % FMX_RDS_DECIM) : 0xFFFFFFFFu;
+  const uint32_t j_mine = act ? (ssr % FMX_RDS_DECIM) : 0xFFFFFFFFu;
   uint32_t j_first = j_mine;
   for (int d = 32; d >= 1; d >>= 1) j_first = min(j_first, (uint32_t)__shfl_xor((int)j_first, d));
   const bool uniform_j = __ballot(act && j_mine != j_first) == 0;
-  int t = 0;
-  if (uniform_j) {
-    // Every lane shares the decimation phase (the normal case: channels of a
-    // wave see identical resampler timing unless reset one by one).  Step to
-    // the first period start (j == 1), then run chunks of 8 samples
-    // (3 per period, the FIR output at the end of the third): the NCO phases
-    // of a chunk (no PLL update inside) are computed with the 8 theta values
-    // in parallel and only the wrapped phase sum serial, then 8 sincos in
-    // parallel, then the partial sums in sample order.  Same arithmetic and
-    // order as step_one; only the schedule differs.
-    while (t < nmax && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) != 1u) step_one(t++);
-    constexpr int U = 8;
-    while (t + U <= cmin) {
-      need(t, U);
-      const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;  // 1, 9 or 17
-      const bool out_end = (j0 == 17u);
-      float ph[U];
-      ph[0] = s.phase0;
-      {
-        uint32_t th[U - 1];
-        float nw[U - 1];
+  constexpr int U = 8;
+  // one chunk of U samples starting at a period phase of 1, 9 or 17
+  auto chunk = [&](int t) __attribute__((always_inline)) {
+    need(t, U);
+    const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;
+    float ph[U];
+    ph[0] = phase0;
+    {
+      float nw[U - 1];
 #pragma unroll
-        for (int v = 0; v < U - 1; ++v) {
-          th[v] = s.theta + (uint32_t)(v + 1) * s.dtheta;
-          nw[v] = d_nco_phase(th[v]);
-        }
+      for (int v = 0; v < U - 1; ++v) nw[v] = d_nco_phase(theta + (uint32_t)(v + 1) * dtheta);
 #pragma unroll
-        for (int v = 0; v < U - 1; ++v) {
-          float delta = nw[v] - (v == 0 ? s.prev_f0 : nw[v - 1]);
-          if (delta > kPiF) delta = delta - 2.f * kPiF;
-          else if (delta < -kPiF) delta = delta + 2.f * kPiF;
-          const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
-          float p2 = ph[v] + scaled;
-          if (p2 > kPiF) p2 = p2 - 2.f * kPiF;
-          else if (p2 < -kPiF) p2 = p2 + 2.f * kPiF;
-          ph[v + 1] = p2;
-        }
-        s.theta = th[U - 2];
-        s.prev_f0 = nw[U - 2];
-        s.phase0 = ph[U - 1];
-        s.sample_since_reset += U - 1;
+      for (int v = 0; v < U - 1; ++v) {
+        float delta = nw[v] - (v == 0 ? prev_f0 : nw[v - 1]);
+        delta = d_unwrap(delta);
+        const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
+        float p2 = ph[v] + scaled;
+        p2 = d_unwrap(p2);
+        ph[v + 1] = p2;
       }
-      float mr[U], mi[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float sn, cs;
-        sincosf(-ph[u], &sn, &cs);
-        const float x = L.tin[lane][t + u - tb];
-        mr[u] = x * cs;
-        mi[u] = x * sn;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t j = j0 + (uint32_t)u;  // 1..24
-        const int jp = (j == FMX_RDS_DECIM) ? 0 : FMX_RDS_DECIM - (int)j;
-        acc_add(mr[u], mi[u], t + u, &L.taps[jp][0], 1);
-      }
-      if (out_end) fir_output();
-      nco_step();  // the chunk's last sample, after a PLL update if any
-      t += U;
+      theta += (uint32_t)(U - 1) * dtheta;
+      prev_f0 = nw[U - 2];
+      phase0 = ph[U - 1];
+      ssr += U - 1;
     }
+    float xs[U];
+    {
+      // 8 samples from 3 16-B segments, offset o = d & 3 is wave-uniform
+      const int d = t - tb, g = d >> 2, o = d & 3;
+      const float4 A = *reinterpret_cast<const float4 *>(seg_ptr(cur, g));
+      const float4 B4 = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + 1));
+      const float4 C4 = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + 2));
+      const float v[12] = {A.x, A.y, A.z, A.w, B4.x, B4.y, B4.z, B4.w, C4.x, C4.y, C4.z, C4.w};
+      switch (o) {
+        case 0:
+#pragma unroll
+          for (int u = 0; u < U; ++u) xs[u] = v[u];
+          break;
+        case 1:
+#pragma unroll
+          for (int u = 0; u < U; ++u) xs[u] = v[u + 1];
+          break;
+        case 2:
+#pragma unroll
+          for (int u = 0; u < U; ++u) xs[u] = v[u + 2];
+          break;
+        default:
+#pragma unroll
+          for (int u = 0; u < U; ++u) xs[u] = v[u + 3];
+          break;
+      }
+    }
+    f32x2 mx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) mx[u] = mix(xs[u], ph[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = j0 + (uint32_t)u; // 1..24
+      const int jp = (j == FMX_RDS_DECIM) ? 0 : FMX_RDS_DECIM - (int)j;
+      acc_add(mx[u], t + u, &L.taps[jp][0]);
+    }
+    RDS_STAMP(2)
+    if (j0 == 17u) {
+      fir_output();
+      RDS_STAMP(3)
+    }
+    nco_step(); // the chunk's last sample, after a PLL update if any
+  };
+  // Segments of <= RDS_SEG samples (<= RDS_SYMQ - 2 symbols), the queued
+  // symbols decoded at each segment end.  One call site each for the chunk,
+  // the generic sample step and the decoders keeps the code (and the exec-mask
+  // nesting) small.
+  constexpr int RDS_SEG = FMX_RDS_DECIM * (RDS_SYMQ - 4);
+  int t = 0;
+  while (t < nmax) {
+    int tend = t + RDS_SEG;
+    if (uniform_j) tend -= (int)(((j_first + (uint32_t)tend) % FMX_RDS_DECIM + FMX_RDS_DECIM - 1) % FMX_RDS_DECIM);
+    tend = min(tend, nmax);
+    const int cend = min(tend, cmin);
+    while (t < tend) {
+      if (uniform_j && t + U <= cend && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) % 8u == 1u) {
+        chunk(t);
+        t += U;
+      } else {
+        step_one(t++);
+        RDS_STAMP(4)
+      }
+    }
+    flush_symbols();
+    RDS_STAMP(5)
   }
-  while (t < nmax) step_one(t++);
   if (!act) return;
-  s.ring_pos = ring0 + (uint32_t)count;
-  a.st[c] = s;
+  // ---- registers -> state ----
+  S.theta = theta;
+  S.dtheta = dtheta;
+  S.sample_since_reset = ssr;
+  S.prev_f0 = prev_f0;
+  S.phase0 = phase0;
+  for (int i = 0; i < FMX_RDS_NACC; ++i) {
+    S.acc_re[i] = acc[i].x;
+    S.acc_im[i] = acc[i].y;
+  }
+  S.agc_g = agc_g;
+  S.agc_y2p = agc_y2p;
+  S.ss_rate = ss_rate;
+  S.ss_del = ss_del;
+  S.ss_tau = ss_tau;
+  S.ss_q_hat = ss_q_hat;
+  S.ss_v1 = ss_v1;
+  S.ss_b = ss_b;
+  S.ss_decim = ss_decim;
+  S.ss_mf_valid = ss_valid;
+  for (int m = 0; m < FMX_SS_SUB; ++m) {
+    const f32x2 w = L.win[wp + 1 + m][lane];
+    S.ss_win_re[m] = w.x;
+    S.ss_win_im[m] = w.y;
+  }
+  S.ring_pos = ring0 + (uint32_t)count;
+  a.st[c] = S;
   if (a.group_count) a.group_count[c] = ng;
+  RDS_STAMP(6)
+#ifdef FMX_STAMPS
+  if (a.dbg && lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, rs_acc[k]);
+#endif
+#undef RDS_STAMP
 }
 
 /* ================================================================== */
@@ -2104,7 +2440,7 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {

@@ -1,0 +1,52 @@
+// fmx_math.h -- small fp32 math kernels shared by the HIP kernels and the
+// host-side accuracy test (tests/cpp/math_test.cpp).
+//
+// fmx_sincos: sin and cos of one fp32 phase, |x| <= 8 (the NCO phases of the
+// stereo PLL, stereo_decoder.cpp:251-253 / 277-278, and the RDS mix-down,
+// subcarrier.cpp:158, are wrapped to [-pi, 2pi]).  Three-part Cody-Waite
+// reduction by pi/2 with FMA (exact for |q| <= 5) and the cephes sinf/cosf
+// minimax polynomials on [-pi/4, pi/4] with the reduced argument carried as
+// a float pair: one shared reduction and ~30 VALU
+// instead of the libm sincosf path with its large-argument branch.  Max error
+// against the correctly rounded result is checked by tests/test_math.py:
+// < 1 ulp, ~95 % correctly rounded over [-2pi, 2pi] (the oracle's glibc
+// sinf/cosf are the reference; parity bars on the PLL outputs are tolerances).
+#ifndef FMX_MATH_H
+#define FMX_MATH_H
+
+#ifdef __HIPCC__
+#define FMX_HD __host__ __device__ __forceinline__
+#else
+#include <cmath>
+#define FMX_HD inline
+#endif
+
+FMX_HD void fmx_sincos(float x, float *s, float *c) {
+  const float q = rintf(x * 0.636619772367581343f);
+  // r = x - q pi/2 as rh + rl (pi/2 in three parts)
+  const float r1 = fmaf(-q, 1.57079637050628662109375f, x);
+  const float rh = fmaf(-q, -4.3711388286737929e-08f, r1);
+  float rl = fmaf(-q, -4.3711388286737929e-08f, r1 - rh);
+  rl = fmaf(-q, -1.7151245100058819e-15f, rl);
+  const float z = rh * rh;
+  // sin: rh + (rl + rh z P(z)),  degree-9 minimax
+  float ps = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
+  ps = fmaf(z, ps, 0.00833307858556509017944336f);
+  ps = fmaf(z, ps, -0.166666597127914428710938f);
+  const float sr = rh + fmaf(rh * z, ps, rl);
+  // cos: (1 - z/2) split exactly, + z^2 Q(z) - rh rl
+  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(z, pc, 4.166664568298827e-2f);
+  const float hz = 0.5f * z;
+  const float w = 1.0f - hz;
+  const float tail = (1.0f - w) - hz;
+  const float cr = w + (fmaf(z * z, pc, tail) - rh * rl);
+  const int qi = (int)q;
+  const bool swap = (qi & 1) != 0;
+  const float s0 = swap ? cr : sr;
+  const float c0 = swap ? sr : cr;
+  *s = (qi & 2) ? -s0 : s0;
+  *c = ((qi + 1) & 2) ? -c0 : c0;
+}
+
+#endif

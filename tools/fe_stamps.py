@@ -1,4 +1,4 @@
-"""Diagnostic: per-stage clocks of k_frontend on the bench workload.
+"""Diagnostic: per-stage clocks of k_frontend and k_rds on the bench workload.
 Needs libfmx.so built with `make -C fmtuner-sdr_amd STAMPS=1 -B`; runs with
 FMX_STAMPS=1 (set here).  Prints
 the share of each stage in thread 0's timeline."""
@@ -31,8 +31,22 @@ out = fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr())
 for b in range(nblk):
     h.process_block(d_iq.data_ptr() + b * 2 * B * M, row, B, out)
 h.sync()
-v = (C.c_ulonglong * 8)()
-assert L.fmx_debug_stamps(h.h, v, 8) == 0
-tot = sum(v)
+v = (C.c_ulonglong * 32)()
+assert L.fmx_debug_stamps(h.h, v, 32) == 0
+tot = sum(v[:8])
+print("k_frontend (thread 0 of each workgroup)")
 for k in range(8):
-    print(f"{NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
+    print(f"  {NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
+RN = ["setup", "tile-wait", "chunk", "fir_out", "step_one", "decode", "store", "-"]
+tot = sum(v[8:]) or 1
+nwg = (Cn + 63) // 64
+print("k_rds (lane 0 of each workgroup)")
+for k in range(8):
+    print(f"  {RN[k]:10s} {v[8 + k] / tot * 100:6.1f} %  {v[8 + k] / (nwg * nblk):10.0f} ticks/launch-WG")
+nwg = (Cn + 63) // 64
+print("k_pll per wave (lane 0): work / barrier-wait ticks per launch-WG")
+for w, nm in enumerate(["W0 chain", "W1 env", "W2a", "W2b", "W3 blend+load"]):
+    wk, wt = v[16 + 2 * w], v[17 + 2 * w]
+    print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}")
+print(f"  W3 issue part {v[26] / (nwg * nblk):10.0f}")
+print(f"  W3 store part {v[27] / (nwg * nblk):10.0f}")
