@@ -1433,13 +1433,75 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 /* ================================================================== */
 /* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
 /* ================================================================== */
+/* k_audio: one workgroup (256 threads) per channel, the call in chunks of
+ * AU2_T DSP samples, L and R carried together as packed (L, R) pairs:
+ *   L/R 121-tap FIR          8 consecutive outputs per thread, every input
+ *                            pair read once per thread and fed to 8 packed
+ *                            FMAs (per output the same FMA chain, oldest
+ *                            sample first, as before)           stereo_decoder.cpp:281-282
+ *   resampler Fs -> 32 kHz   one output per thread and entry of the host
+ *                            timing schedule (branch-transposed bank)   af_post_processor.cpp:56-64
+ *   de-emphasis, DC block    block affine scans, 3 outputs per thread,
+ *                            then the reference's op order            :66-75, fm_demod.cpp:218-224
+ *   clamp (main.cpp:1305-1308), stores.
+ * Modes: 0 stereo (FIR + AF), 1 AF only, 2 mono FMDemod::downsampleAudio,
+ * 3 mono pipeline (x0.5, L = R), 4 FIR only (fmx_stereo). */
+#define AU2_T 2048
+#define AU2_PT 8                        // FIR outputs per thread (AU2_T / 256)
+#define AU2_MAXOUT (AU2_T / 3 + 16)     // resampler outputs per chunk (ratio >= 3)
+// FIR input image: pair i at i + i/8 (lanes 8 pairs apart land 9 apart:
+// conflict-free ds_read_b64)
+__device__ __forceinline__ int au_xi(int i) { return i + (i >> 3); }
+struct AuShared {
+  float2 x[(AU_HALO + AU2_T + 8) * 9 / 8 + 8]; // raw (L, R), 120 of history first
+  float2 f[AU_RHALO + AU2_T];                  // resampler input (L, R), 32 of history first
+  float2 o[AU2_MAXOUT];                        // resampler outputs of the chunk
+  float hT[FMX_AF_SUB][FMX_NPFB];              // resampler bank transposed: hT[n][b] = h_b[n]
+  float lt[136] __attribute__((aligned(16)));  // L/R FIR taps, lt[k + 7] = h[k], zeros around
+  float ws[3][4][2];                           // scan scratch (A, BL, BR per wave)
+  float iir[4];                                // de_L, de_R, dc_L, dc_R
+  int eb, ee, count;
+};
+
+// exclusive block scan (256 threads) of per-thread affine maps v -> A v + B
+// (B for L and R), applied to the carries: the state before this thread's
+// first element.
+__device__ __forceinline__ void au_scan_prev(float A, float BL, float BR, float cl, float cr, float (*ws)[4][2],
+                                             float &pl, float &pr) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float pA = __shfl_up(A, d), pL = __shfl_up(BL, d), pR = __shfl_up(BR, d);
+    if (lane >= d) {
+      BL = A * pL + BL;
+      BR = A * pR + BR;
+      A = A * pA;
+    }
+  }
+  if (lane == 63) {
+    ws[0][wave][0] = A;
+    ws[1][wave][0] = BL;
+    ws[2][wave][0] = BR;
+  }
+  float eA = __shfl_up(A, 1), eL = __shfl_up(BL, 1), eR = __shfl_up(BR, 1);
+  if (lane == 0) {
+    eA = 1.0f;
+    eL = 0.0f;
+    eR = 0.0f;
+  }
+  __syncthreads();
+  float vl = cl, vr = cr;
+  for (int w = 0; w < wave; ++w) {
+    vl = ws[0][w][0] * vl + ws[1][w][0];
+    vr = ws[0][w][0] * vr + ws[2][w][0];
+  }
+  pl = eA * vl + eL;
+  pr = eA * vr + eR;
+  __syncthreads(); // ws reusable
+}
+
 __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
-  __shared__ float li[AU_HALO + AU_T + 8], ri[AU_HALO + AU_T + 8];
-  __shared__ float lf[AU_RHALO + AU_T], rf[AU_RHALO + AU_T];
-  __shared__ float ol[AU_MAXOUT], orr[AU_MAXOUT];
-  __shared__ int s_eb, s_ee, s_count;
-  __shared__ float s_iir[4], s_ws[12];  // [de_L, de_R, dc_L, dc_R]; scan scratch
-  __shared__ float afh[FMX_NPFB * FMX_AF_SUB];  // resampler bank (per-lane branch -> LDS)
+  __shared__ AuShared S;
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
@@ -1455,32 +1517,22 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const float dc_alpha = mono ? 0.0008f : 0.005f;
   const float de_a1 = -(1.0f - dalpha);
   const float dc_a1 = -1.0f + dc_alpha;
-  for (int h = tid; h < AU_HALO + AU_T + 8; h += 256) {
-    li[h] = 0.0f;
-    ri[h] = 0.0f;
-  }
-  __syncthreads();
-  // halos
+  // ---- carried state ----
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
   if (lrfir)
-    for (int h = tid; h < AU_HALO; h += 256) {
-      li[h] = lrh[h];
-      ri[h] = lrh[(FMX_LR_LEN - 1) + h];
-    }
-  for (int h = tid; h < AU_RHALO; h += 256) {
-    lf[h] = win[h];
-    rf[h] = mono ? 0.0f : win[32 + h];
-  }
+    for (int h = tid; h < AU_HALO; h += 256) S.x[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
+  if (af)
+    for (int h = tid; h < AU_RHALO; h += 256) S.f[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
   if (af && tid == 0) {
     if (mono) {
-      s_iir[0] = iir[0];
-      s_iir[1] = 0.0f;
-      s_iir[2] = iir[1];
-      s_iir[3] = 0.0f;
+      S.iir[0] = iir[0];
+      S.iir[1] = 0.0f;
+      S.iir[2] = iir[1];
+      S.iir[3] = 0.0f;
     } else {
-      for (int k = 0; k < 4; ++k) s_iir[k] = iir[k];
+      for (int k = 0; k < 4; ++k) S.iir[k] = iir[k];
     }
   }
   const FmxSched *sched = nullptr;
@@ -1489,163 +1541,230 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     const int g = a.group[c];
     sched = a.sched + (size_t)g * a.sched_stride;
     sched_n = a.sched_n[g];
+    for (int k = tid; k < FMX_NPFB * FMX_AF_SUB; k += 256) {
+      const int b = k / FMX_AF_SUB, nn = k % FMX_AF_SUB;
+      S.hT[nn][b] = D->af_h[k];
+    }
   }
   if (tid == 0) {
-    s_eb = 0;
-    s_count = 0;
+    S.eb = 0;
+    S.count = 0;
   }
-  if (af)
-    for (int k = tid; k < FMX_NPFB * FMX_AF_SUB; k += 256) afh[k] = D->af_h[k];
+  if (lrfir)
+    for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
   const float *inl = a.in_l + (size_t)c * a.in_stride;
   const float *inr = mono ? nullptr : a.in_r + (size_t)c * a.in_stride;
+  const float sc = D->lr_scale;
   __syncthreads();
-  for (int n0 = 0; n0 < n; n0 += AU_T) {
-    const int cnt = min(AU_T, n - n0);
-    FmxSched en3[3];  // this chunk's resampler schedule entries (see k_frontend)
+  for (int n0 = 0; n0 < n; n0 += AU2_T) {
+    const int cnt = min(AU2_T, n - n0);
+    FmxSched en3[3];
     if (af) {
+      const int eb = S.eb;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const int e = s_eb + tid + 256 * k;
+        const int e = eb + tid + 256 * k;
         en3[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
       }
-      if (tid == 0) s_ee = s_eb;
     }
-    for (int j = tid; j < cnt; j += 256) {
-      if (lrfir) {
-        li[AU_HALO + j] = inl[n0 + j];
-        ri[AU_HALO + j] = inr[n0 + j];
-      } else {
-        lf[AU_RHALO + j] = inl[n0 + j];
-        if (!mono) rf[AU_RHALO + j] = inr[n0 + j];
+    // ---- chunk input (all loads issued before the first LDS write) ----
+    {
+      float vl[AU2_PT], vr[AU2_PT];
+#pragma unroll
+      for (int k = 0; k < AU2_PT; ++k) {
+        const int j = tid + 256 * k;
+        vl[k] = (j < cnt) ? inl[n0 + j] : 0.0f;
+        vr[k] = (j < cnt && !mono) ? inr[n0 + j] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < AU2_PT; ++k) {
+        const int j = tid + 256 * k;
+        if (lrfir) S.x[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
+        else if (j < cnt) S.f[AU_RHALO + j] = make_float2(vl[k], vr[k]);
       }
     }
+    if (tid == 0) S.ee = S.eb;
     __syncthreads();
+    // ---- L/R FIR: outputs j0 .. j0+7, inputs j0-120 .. j0+7 ----
     if (lrfir) {
-      float zl[3], zr[3];
-      fir_r3p(li, AU_HALO + 3 * tid, D->lr_pad, D->lr_pair, FMX_LR_LEN, zl);
-      fir_r3p(ri, AU_HALO + 3 * tid, D->lr_pad, D->lr_pair, FMX_LR_LEN, zr);
-      const float sc = D->lr_scale;
+      const int j0 = AU2_PT * tid;
+      f32x2 acc[AU2_PT];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int j = 3 * tid + r;
-        if (j < cnt) {
-          lf[AU_RHALO + j] = zl[r] * sc;
-          rf[AU_RHALO + j] = zr[r] * sc;
-          if (a.lr_out_l) {
-            a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = zl[r] * sc;
-            a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = zr[r] * sc;
+      for (int r = 0; r < AU2_PT; ++r) acc[r] = f32x2{0.0f, 0.0f};
+#pragma unroll 1
+      for (int m0 = 0; m0 < AU_HALO + AU2_PT; m0 += 8) {
+        // taps k = 113-m0 .. 128-m0 (zero outside 0..120): sample m0+u feeds
+        // output r with tap index 7 + r - u of this window
+        const float4 *tw = reinterpret_cast<const float4 *>(&S.lt[AU_HALO - m0]);
+        const float4 t0 = tw[0], t1 = tw[1], t2 = tw[2], t3 = tw[3];
+        const float t[16] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w,
+                             t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float2 v = S.x[au_xi(j0 + m0 + u)]; // input j0 - 120 + m0 + u
+          const f32x2 vv = f32x2{v.x, v.y};
+#pragma unroll
+          for (int r = 0; r < AU2_PT; ++r) {
+            const float h = t[7 + r - u];
+            acc[r] = __builtin_elementwise_fma(f32x2{h, h}, vv, acc[r]);
           }
         }
       }
-      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < AU2_PT; ++r) {
+        const int j = j0 + r;
+        if (j < cnt) {
+          const float2 y = make_float2(acc[r].x * sc, acc[r].y * sc);
+          if (af) S.f[AU_RHALO + j] = y;
+          if (a.lr_out_l) {
+            a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
+            a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
+          }
+        }
+      }
     }
+    __syncthreads();
     if (af) {
-      const int eb = s_eb;
+      // ---- resampler: one schedule entry per thread ----
+      const int eb = S.eb;
       int last = -1;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const int e = eb + tid + 256 * k;
         if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
-          auto gl = [&](int ii) -> float { return lf[AU_RHALO + ii - n0]; };
-          ol[e - eb] = resamp_out<FMX_AF_SUB>(afh, en3[k].packed, en3[k].mu, gl);
-          if (!mono) {
-            auto gr = [&](int ii) -> float { return rf[AU_RHALO + ii - n0]; };
-            orr[e - eb] = resamp_out<FMX_AF_SUB>(afh, en3[k].packed, en3[k].mu, gr);
+          const int i = (en3[k].packed & 0xFFFF) - n0;
+          const int b = (en3[k].packed >> 16) & 0xFF;
+          const bool boundary = (en3[k].packed >> 24) & 1;
+          const int b0 = boundary ? FMX_NPFB - 1 : b, b1 = boundary ? 0 : b + 1;
+          const int i0 = boundary ? i - 1 : i;
+          f32x2 y0 = f32x2{0.0f, 0.0f}, y1 = f32x2{0.0f, 0.0f};
+#pragma unroll
+          for (int m = 0; m < FMX_AF_SUB; ++m) {
+            const float2 v0 = S.f[AU_RHALO + i0 - (FMX_AF_SUB - 1) + m];
+            const float2 v1 = S.f[AU_RHALO + i - (FMX_AF_SUB - 1) + m];
+            const float h0 = S.hT[FMX_AF_SUB - 1 - m][b0], h1 = S.hT[FMX_AF_SUB - 1 - m][b1];
+            const f32x2 p0 = f32x2{h0, h0} * f32x2{v0.x, v0.y};
+            const f32x2 p1 = f32x2{h1, h1} * f32x2{v1.x, v1.y};
+            y0 = y0 + p0;
+            y1 = y1 + p1;
           }
+          const float mu = en3[k].mu, omu = 1.0f - mu;
+          const f32x2 w0 = f32x2{omu, omu} * y0;
+          const f32x2 w1 = f32x2{mu, mu} * y1;
+          const f32x2 y = w0 + w1;
+          S.o[e - eb] = make_float2(y.x, y.y);
           last = e;
         }
       }
-      if (last >= 0) atomicMax(&s_ee, last + 1);
+      if (last >= 0) atomicMax(&S.ee, last + 1);
       __syncthreads();
-      const int ee = s_ee;
-      // de-emphasis + DC block (DF-II, af_post_processor.cpp:66-75 /
-      // fm_demod.cpp:218-224): each IIR as a block affine scan for the
-      // state before output k, then output k in the reference's op order.
-      {
-        const int m = ee - eb;  // <= AU_MAXOUT
-        const bool on = tid < m;
-        float xl = on ? ol[tid] : 0.0f;
-        float xr = (on && !mono) ? orr[tid] : 0.0f;
-        if (de_on) {
-          float pl, pr;
-          block_affine_prev(on ? -de_a1 : 1.0f, xl, xr, s_iir[0], s_iir[1], s_ws, pl, pr);
-          const float vl = xl - de_a1 * pl, vr = xr - de_a1 * pr;
-          if (tid == m - 1) {
-            s_iir[0] = vl;
-            s_iir[1] = vr;
-          }
-          xl = dalpha * vl;
-          xr = dalpha * vr;
-        }
-        float ql, qr;
-        block_affine_prev(on ? -dc_a1 : 1.0f, xl, xr, s_iir[2], s_iir[3], s_ws, ql, qr);
-        const float vl = xl - dc_a1 * ql, vr = xr - dc_a1 * qr;
-        float yl = vl - ql, yr = vr - qr;
-        __syncthreads();
-        if (tid == m - 1) {
-          s_iir[2] = vl;
-          s_iir[3] = vr;
-        }
-        if (pipe_mono) yl = yl * 0.5f;
-        if (a.clamp) {
-          yl = d_clamp(yl, -1.0f, 1.0f);
-          yr = d_clamp(yr, -1.0f, 1.0f);
-        }
-        const int o = s_count + tid;
-        if (on && o < a.cap) {
-          a.out_l[(size_t)c * a.out_stride + o] = yl;
-          if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = yl;
-          else if (!mono) a.out_r[(size_t)c * a.out_stride + o] = yr;
-        }
+      // ---- de-emphasis + DC block over the m outputs, 3 per thread ----
+      const int m = S.ee - eb; // <= AU2_MAXOUT
+      float xl[3], xr[3];
+      bool on[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = 3 * tid + k;
+        on[k] = q < m;
+        const float2 v = on[k] ? S.o[q] : make_float2(0.0f, 0.0f);
+        xl[k] = v.x;
+        xr[k] = v.y;
       }
+      auto compose = [&](float a_, const float *bl, const float *br, float &A, float &BL, float &BR) {
+        A = 1.0f;
+        BL = 0.0f;
+        BR = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (on[k]) {
+            BL = a_ * BL + bl[k];
+            BR = a_ * BR + br[k];
+            A = a_ * A;
+          }
+      };
+      if (de_on) {
+        float A, BL, BR, pl, pr;
+        compose(-de_a1, xl, xr, A, BL, BR);
+        au_scan_prev(A, BL, BR, S.iir[0], S.iir[1], S.ws, pl, pr);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (on[k]) {
+            const float vl = xl[k] - de_a1 * pl, vr = xr[k] - de_a1 * pr;
+            if (3 * tid + k == m - 1) {
+              S.iir[0] = vl;
+              S.iir[1] = vr;
+            }
+            pl = vl;
+            pr = vr;
+            xl[k] = dalpha * vl;
+            xr[k] = dalpha * vr;
+          }
+      }
+      float A, BL, BR, ql, qr;
+      compose(-dc_a1, xl, xr, A, BL, BR);
+      au_scan_prev(A, BL, BR, S.iir[2], S.iir[3], S.ws, ql, qr);
+      const int o0 = S.count;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (on[k]) {
+          const float vl = xl[k] - dc_a1 * ql, vr = xr[k] - dc_a1 * qr;
+          float yl = vl - ql, yr = vr - qr;
+          if (3 * tid + k == m - 1) {
+            S.iir[2] = vl;
+            S.iir[3] = vr;
+          }
+          ql = vl;
+          qr = vr;
+          if (pipe_mono) yl = yl * 0.5f;
+          if (a.clamp) {
+            yl = d_clamp(yl, -1.0f, 1.0f);
+            yr = d_clamp(yr, -1.0f, 1.0f);
+          }
+          const int o = o0 + 3 * tid + k;
+          if (o < a.cap) {
+            a.out_l[(size_t)c * a.out_stride + o] = yl;
+            if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = yl;
+            else if (!mono) a.out_r[(size_t)c * a.out_stride + o] = yr;
+          }
+        }
       __syncthreads();
       if (tid == 0) {
-        s_count += ee - eb;
-        s_eb = ee;
+        S.count = o0 + m;
+        S.eb = eb + m;
       }
     }
-    // carry halos
+    // ---- carry halos ----
     {
-      float cl = 0.0f, cr = 0.0f, fl = 0.0f, fr = 0.0f;
-      if (lrfir && tid < AU_HALO) {
-        cl = li[tid + cnt];
-        cr = ri[tid + cnt];
-      }
-      if (tid < AU_RHALO) {
-        fl = lf[tid + cnt];
-        fr = rf[tid + cnt];
-      }
+      float2 cx = make_float2(0.0f, 0.0f), cf = make_float2(0.0f, 0.0f);
+      if (lrfir && tid < AU_HALO) cx = S.x[au_xi(tid + cnt)];
+      if (af && tid < AU_RHALO) cf = S.f[tid + cnt];
       __syncthreads();
-      if (lrfir && tid < AU_HALO) {
-        li[tid] = cl;
-        ri[tid] = cr;
-      }
-      if (tid < AU_RHALO) {
-        lf[tid] = fl;
-        rf[tid] = fr;
-      }
+      if (lrfir && tid < AU_HALO) S.x[au_xi(tid)] = cx;
+      if (af && tid < AU_RHALO) S.f[tid] = cf;
       __syncthreads();
     }
   }
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) {
-      lrh[h] = li[h];
-      lrh[(FMX_LR_LEN - 1) + h] = ri[h];
+      const float2 v = S.x[au_xi(h)];
+      lrh[h] = v.x;
+      lrh[(FMX_LR_LEN - 1) + h] = v.y;
     }
   if (af) {
     for (int h = tid; h < AU_RHALO; h += 256) {
-      win[h] = lf[h];
-      if (!mono) win[32 + h] = rf[h];
+      const float2 v = S.f[h];
+      win[h] = v.x;
+      if (!mono) win[32 + h] = v.y;
     }
     if (tid == 0) {
       if (mono) {
-        iir[0] = s_iir[0];
-        iir[1] = s_iir[2];
+        iir[0] = S.iir[0];
+        iir[1] = S.iir[2];
       } else {
-        for (int k = 0; k < 4; ++k) iir[k] = s_iir[k];
+        for (int k = 0; k < 4; ++k) iir[k] = S.iir[k];
       }
     }
-    if (tid == 0 && a.out_count) a.out_count[c] = s_count < a.cap ? s_count : a.cap;
+    if (tid == 0 && a.out_count) a.out_count[c] = S.count < a.cap ? S.count : a.cap;
   }
 }
 
