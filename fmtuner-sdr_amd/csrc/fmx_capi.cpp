@@ -99,6 +99,9 @@ struct Handle {
   TimingSet t_af, t_mono, t_rds;
   // kernel timing
   bool timing = false;
+  // diagnostic (FMX_DIAG_SKIP=rds,pll,audio): kernels left out of
+  // process_block to measure what the others cost together -- outputs invalid
+  bool skip_rds = false, skip_pll = false, skip_audio = false;
   struct Pending {
     int k;
     hipEvent_t a, b;
@@ -445,6 +448,12 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     return FMX_E_INVALID;
   }
   HIP_TRY(hipStreamCreateWithFlags(&h->sA, hipStreamNonBlocking));
+  if (const char *e = std::getenv("FMX_DIAG_SKIP")) {
+    const std::string v(e);
+    h->skip_rds = v.find("rds") != std::string::npos;
+    h->skip_pll = v.find("pll") != std::string::npos;
+    h->skip_audio = v.find("audio") != std::string::npos;
+  }
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
   } else {
@@ -701,7 +710,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
     KTimer t(h, FMX_K_RDS, h->sC);
-    if ((rc = launch_rds(a, h->sC)) != FMX_OK) {
+    if (!h->skip_rds && (rc = launch_rds(a, h->sC)) != FMX_OK) {
       h->err = "rds launch failed";
       return rc;
     }
@@ -719,7 +728,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.stereo_out = o->d_stereo;
     a.pilot_tenths_out = o->d_pilot_tenths;
     KTimer t(h, FMX_K_STEREO, h->sB);
-    if ((rc = launch_pll(a, h->sB)) != FMX_OK) {
+    if (!h->skip_pll && (rc = launch_pll(a, h->sB)) != FMX_OK) {
       h->err = "pll launch failed";
       return rc;
     }
@@ -742,7 +751,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.cap = h->cfg.block;
     a.clamp = 1;
     KTimer t(h, FMX_K_AUDIO, h->sD);
-    if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
+    if (!h->skip_audio && (rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
       return rc;
     }

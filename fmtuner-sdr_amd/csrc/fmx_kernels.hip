@@ -39,7 +39,7 @@ namespace fmx {
 #define AU_HALO 120
 #define AU_RHALO 32
 #define AU_MAXOUT 256
-#define PLL_T 16
+#define PLL_T 8
 
 static constexpr float kPiF = 3.14159265358979323846f;
 
@@ -244,39 +244,57 @@ __device__ __forceinline__ void fir_r3p(const float *x, int base, const float *_
   z[2] = a2;
 }
 
-// Resampler output from a window accessor; reference dot order (oldest first)
+// Resampler output from a window accessor; reference dot order (oldest first).
+// The boundary case (branch 31 of window i-1 blended with branch 0 of window
+// i) only swaps the branch / window indices, so both cases run the same
+// loop: no divergence in a wave that mixes them.
 template <int SUB, typename Get>
 __device__ __forceinline__ float resamp_out(const float *__restrict__ hb, int packed, float mu, Get get) {
   const int i = packed & 0xFFFF;
   const int b = (packed >> 16) & 0xFF;
-  const int boundary = (packed >> 24) & 1;
+  const bool boundary = (packed >> 24) & 1;
+  const float *h0 = hb + (boundary ? FMX_NPFB - 1 : b) * SUB;
+  const float *h1 = hb + (boundary ? 0 : b + 1) * SUB;
+  const int i0 = boundary ? i - 1 : i;
   float y0 = 0.0f, y1 = 0.0f;
-  if (!boundary) {
-    const float *h0 = hb + b * SUB;
-    const float *h1 = hb + (b + 1) * SUB;
 #pragma unroll
-    for (int m = 0; m < SUB; ++m) {
-      const float v = get(i - (SUB - 1) + m);
-      const float p0 = h0[SUB - 1 - m] * v;
-      const float p1 = h1[SUB - 1 - m] * v;
-      y0 = y0 + p0;
-      y1 = y1 + p1;
-    }
-  } else {
-    const float *h0 = hb + (FMX_NPFB - 1) * SUB;
-    const float *h1 = hb;
-#pragma unroll
-    for (int m = 0; m < SUB; ++m) {
-      const float v0 = get(i - 1 - (SUB - 1) + m);
-      const float v1 = get(i - (SUB - 1) + m);
-      const float p0 = h0[SUB - 1 - m] * v0;
-      const float p1 = h1[SUB - 1 - m] * v1;
-      y0 = y0 + p0;
-      y1 = y1 + p1;
-    }
+  for (int m = 0; m < SUB; ++m) {
+    const float v0 = get(i0 - (SUB - 1) + m);
+    const float v1 = get(i - (SUB - 1) + m);
+    const float p0 = h0[SUB - 1 - m] * v0;
+    const float p1 = h1[SUB - 1 - m] * v1;
+    y0 = y0 + p0;
+    y1 = y1 + p1;
   }
   const float w0 = (1.0f - mu) * y0;
   const float w1 = mu * y1;
+  return w0 + w1;
+}
+
+// resamp_out with the two branch dot products as one packed (y0, y1) chain:
+// hp[n][b] = {h_b[n], h_(b+1)%32[n]} (branch 31 pairs with branch 0, the
+// boundary case), the window pair {x[i0-25+m], x[i-25+m]} from one 8-byte
+// read (i0 = i - 1 at a boundary, else the same sample twice).  Products and
+// sums are the same IEEE operations in the same order as resamp_out.
+template <int SUB>
+__device__ __forceinline__ float resamp_out_pair(const float2 (*hp)[FMX_NPFB], int packed, float mu,
+                                                 const float *win) {
+  const int i = packed & 0xFFFF;
+  const int b = (packed >> 16) & 0xFF;
+  const bool boundary = (packed >> 24) & 1;
+  const int bb = boundary ? FMX_NPFB - 1 : b;
+  const float *w = win + (boundary ? i - 1 : i) - (SUB - 1);
+  f32x2 y = {0.0f, 0.0f};
+#pragma unroll
+  for (int m = 0; m < SUB; ++m) {
+    const float2 h = hp[SUB - 1 - m][bb];
+    const float va = w[m], vb = w[m + 1];
+    const f32x2 v = {va, boundary ? vb : va};
+    const f32x2 p = f32x2{h.x, h.y} * v;
+    y = y + p;
+  }
+  const float w0 = (1.0f - mu) * y.x;
+  const float w1 = mu * y.y;
   return w0 + w1;
 }
 
@@ -361,7 +379,7 @@ template <int M, int TPP, bool VEC> struct FeLayout {
   static constexpr int MX = XIN + (FE_HALO_IQ + FE_T + 8) * 8;
   static constexpr int RB = MX + (FMX_HIST + FE_T + 8) * 4;   // RDS resampler window: 32 history + chunk
   static constexpr int RSH = RB + (32 + FE_T + 8) * 4;           // RDS resampler filter bank (per-lane branch)
-  static constexpr int SG = RSH + FMX_NPFB * FMX_RDS_RS_SUB * 4;  // 4 waves x 6 u64 RF-level partials
+  static constexpr int SG = RSH + FMX_NPFB * FMX_RDS_RS_SUB * 8;  // 4 waves x 6 u64 RF-level partials
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (M > 1) ? (RAW_BYTES - 64 + 16 * 256 - 1) / (16 * 256) : 1;  // 16-B loads / thread
@@ -460,8 +478,13 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   }
   const float *rhist = a.rds_hist + (size_t)c * 32;
   if (rds && tid < 32) rb[tid] = rhist[tid];
+  // RDS resampler bank as (branch, next branch) pairs: rsp[n][b]
+  float2(*rsp)[FMX_NPFB] = reinterpret_cast<float2(*)[FMX_NPFB]>(rsh);
   if (rds)
-    for (int k = tid; k < FMX_NPFB * FMX_RDS_RS_SUB; k += 256) rsh[k] = D->rds_rs_h[k];
+    for (int k = tid; k < FMX_NPFB * FMX_RDS_RS_SUB; k += 256) {
+      const int b = k / FMX_RDS_RS_SUB, nn = k % FMX_RDS_RS_SUB;
+      rsp[nn][b] = make_float2(D->rds_rs_h[k], D->rds_rs_h[((b + 1) % FMX_NPFB) * FMX_RDS_RS_SUB + nn]);
+    }
   int e_pos = 0;
   // VEC: chunk bytes [2*n0*M - HB, 2*(n0+cnt)*M) are fetched with 16-B loads
   // one chunk ahead into registers (HBM latency hidden behind the previous
@@ -750,9 +773,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       for (int k = 0; k < 3; ++k) {
         const int e = e_pos + tid + 256 * k;
         if (e < sched_n && (en3[k].packed & 0xFFFF) < n0 + cnt) {
-          auto get = [&](int ii) -> float { return rb[32 + ii - n0]; };
           a.rds_out[(size_t)c * a.rds_stride + e] =
-              resamp_out<FMX_RDS_RS_SUB>(rsh, en3[k].packed, en3[k].mu, get);
+              resamp_out_pair<FMX_RDS_RS_SUB>(rsp, en3[k].packed, en3[k].mu, rb + 32 - n0);
           last = e;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -933,7 +955,7 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
  * LDS slots rotate.  Every value is computed with the reference's arithmetic
  * in the reference's order; only WHERE it runs moved. */
 #define PLL_CH 64
-#define PLL_TS (PLL_T + 4)                 // padded row (16-B aligned, conflict-free float4 rows)
+#define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
 #define PLL_WAVES 5
 struct PllShared {
   float inp[3][PLL_CH][PLL_TS];            // pilot tiles (k+1 loading, k in W0, k-1 in W1)
@@ -1810,16 +1832,81 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 // A wave reading one segment per lane (lane = row) then hits all 64 banks
 // once per 16 lanes (conflict-free ds_read_b128).
 #define RDS_PIECE 260
-#define RDS_SYMQ 48 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
+#define RDS_SYMQ 24 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
 // Per-lane state lives in LDS (odd dword stride: conflict-free across lanes);
 // only the per-sample quantities (NCO, FIR partial sums, AGC, symsync
 // scalars) are held in registers.  Block sync / biphase state is touched once
 // per symbol.
+// The bit-decoder state of FmxRdsState (biphase, delta, block sync) -- the
+// only state k_rds keeps in LDS; the per-sample state lives in registers.
+struct RdsBits {
+  float bi_prev_re, bi_prev_im, bi_even, bi_odd;
+  uint32_t bi_clock, bi_polarity;
+  int delta_prev;
+  uint32_t bs_bitcount, bs_until_next, bs_reg, bs_err_mask_lo, bs_err_mask_hi;
+  int bs_expected, bs_in_sync, bs_err_ptr;
+  uint32_t bs_pulse_pos[4];
+  int bs_pulse_off[4];
+  uint32_t bs_blk_raw[4];
+  uint16_t bs_blk_data[4];
+  uint8_t bs_blk_flags[4];
+  uint32_t bs_bits_since_lost;
+};
 struct RdsCold {
-  FmxRdsState s;
-  uint32_t pad_;
+  RdsBits s;
+  uint32_t pad_[(sizeof(RdsBits) / 4) % 2 == 0 ? 1 : 2];
 };
 static_assert((sizeof(RdsCold) / 4) % 2 == 1, "RdsCold must have an odd dword stride");
+__device__ __forceinline__ void rds_bits_load(RdsBits &b, const FmxRdsState &g) {
+  b.bi_prev_re = g.bi_prev_re;
+  b.bi_prev_im = g.bi_prev_im;
+  b.bi_even = g.bi_even;
+  b.bi_odd = g.bi_odd;
+  b.bi_clock = g.bi_clock;
+  b.bi_polarity = g.bi_polarity;
+  b.delta_prev = g.delta_prev;
+  b.bs_bitcount = g.bs_bitcount;
+  b.bs_until_next = g.bs_until_next;
+  b.bs_reg = g.bs_reg;
+  b.bs_err_mask_lo = g.bs_err_mask_lo;
+  b.bs_err_mask_hi = g.bs_err_mask_hi;
+  b.bs_expected = g.bs_expected;
+  b.bs_in_sync = g.bs_in_sync;
+  b.bs_err_ptr = g.bs_err_ptr;
+  for (int i = 0; i < 4; ++i) {
+    b.bs_pulse_pos[i] = g.bs_pulse_pos[i];
+    b.bs_pulse_off[i] = g.bs_pulse_off[i];
+    b.bs_blk_raw[i] = g.bs_blk_raw[i];
+    b.bs_blk_data[i] = g.bs_blk_data[i];
+    b.bs_blk_flags[i] = g.bs_blk_flags[i];
+  }
+  b.bs_bits_since_lost = g.bs_bits_since_lost;
+}
+__device__ __forceinline__ void rds_bits_store(FmxRdsState &g, const RdsBits &b) {
+  g.bi_prev_re = b.bi_prev_re;
+  g.bi_prev_im = b.bi_prev_im;
+  g.bi_even = b.bi_even;
+  g.bi_odd = b.bi_odd;
+  g.bi_clock = b.bi_clock;
+  g.bi_polarity = b.bi_polarity;
+  g.delta_prev = b.delta_prev;
+  g.bs_bitcount = b.bs_bitcount;
+  g.bs_until_next = b.bs_until_next;
+  g.bs_reg = b.bs_reg;
+  g.bs_err_mask_lo = b.bs_err_mask_lo;
+  g.bs_err_mask_hi = b.bs_err_mask_hi;
+  g.bs_expected = b.bs_expected;
+  g.bs_in_sync = b.bs_in_sync;
+  g.bs_err_ptr = b.bs_err_ptr;
+  for (int i = 0; i < 4; ++i) {
+    g.bs_pulse_pos[i] = b.bs_pulse_pos[i];
+    g.bs_pulse_off[i] = b.bs_pulse_off[i];
+    g.bs_blk_raw[i] = b.bs_blk_raw[i];
+    g.bs_blk_data[i] = b.bs_blk_data[i];
+    g.bs_blk_flags[i] = b.bs_blk_flags[i];
+  }
+  g.bs_bits_since_lost = b.bs_bits_since_lost;
+}
 struct RdsLds {
   float taps[24][12] __attribute__((aligned(16))); // row jp: h[jp + 24 i], i = 0..10, zero pad
   float mf[FMX_NPFB * FMX_SS_SUB];
@@ -1832,7 +1919,7 @@ struct RdsLds {
   RdsCold cold[64];
 };
 
-__device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a, int c, int &ng) {
+__device__ __forceinline__ void rds_emit_group(RdsBits &s, const RdsArgs &a, int c, int &ng) {
   fmx_rds_group g;
   uint8_t e[4];
   uint16_t d[4];
@@ -1855,7 +1942,7 @@ __device__ __forceinline__ void rds_emit_group(FmxRdsState &s, const RdsArgs &a,
 
 // BlockStream::pushBit / findBlockInInputRegister / acquireSync
 // (block_sync.cpp:235-313) and Group::setBlock (group.cpp:103-128)
-__device__ __forceinline__ void rds_push_bit(FmxRdsState &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
+__device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
   s.bs_reg = (s.bs_reg << 1u) + (uint32_t)bit;
   s.bs_until_next--;
   s.bs_bitcount++;
@@ -1998,36 +2085,32 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
         idx++;
       }
   }
-  FmxRdsState &S = L.cold[lane].s;
-  int count = 0;
-  if (act) {
-    S = a.st[c];
-    count = a.in_count[c];
-  } else {
-    S = FmxRdsState{};
-  }
+  RdsBits &S = L.cold[lane].s;
+  const FmxRdsState G = act ? a.st[c] : FmxRdsState{}; // the compiler loads only the fields used
+  const int count = act ? a.in_count[c] : 0;
+  rds_bits_load(S, G);
   float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
   // ---- hot state -> registers ----
-  uint32_t theta = S.theta, dtheta = S.dtheta, ssr = S.sample_since_reset;
-  float prev_f0 = S.prev_f0, phase0 = S.phase0;
+  uint32_t theta = G.theta, dtheta = G.dtheta, ssr = G.sample_since_reset;
+  float prev_f0 = G.prev_f0, phase0 = G.phase0;
   f32x2 acc[FMX_RDS_NACC];
-  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{S.acc_re[i], S.acc_im[i]};
-  float agc_g = S.agc_g, agc_y2p = S.agc_y2p;
-  float ss_rate = S.ss_rate, ss_del = S.ss_del, ss_tau = S.ss_tau, ss_q_hat = S.ss_q_hat, ss_v1 = S.ss_v1;
-  int ss_b = S.ss_b, ss_decim = S.ss_decim, ss_valid = S.ss_mf_valid;
+  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{G.acc_re[i], G.acc_im[i]};
+  float agc_g = G.agc_g, agc_y2p = G.agc_y2p;
+  float ss_rate = G.ss_rate, ss_del = G.ss_del, ss_tau = G.ss_tau, ss_q_hat = G.ss_q_hat, ss_v1 = G.ss_v1;
+  int ss_b = G.ss_b, ss_decim = G.ss_decim, ss_valid = G.ss_mf_valid;
   for (int m = 0; m < FMX_SS_SUB; ++m) {
-    const f32x2 w = f32x2{S.ss_win_re[m], S.ss_win_im[m]};
+    const f32x2 w = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
     L.win[m][lane] = w;
     L.win[m + FMX_SS_SUB][lane] = w;
   }
   int wp = FMX_SS_SUB - 1; // newest window sample at wp (and wp + 18)
-  if (act && S.rebuild) {
+  if (act && G.rebuild) {
     // decimation phase changed by a reset: rebuild the partial sums from the
     // last mixed samples (the reference's FIR window survives the reset)
     for (int i = 0; i < FMX_RDS_NACC; ++i) {
       float ar = 0.0f, ai = 0.0f;
       for (int kp = FMX_RDS_FIR - 1 - 24 * i; kp >= 1; --kp) {
-        const uint32_t idx = (S.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
+        const uint32_t idx = (G.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
         const float h = D->rds_fir[24 * i + kp];
         const float pr = h * ring[2 * idx];
         const float pi = h * ring[2 * idx + 1];
@@ -2036,7 +2119,6 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
       }
       acc[i] = f32x2{ar, ai};
     }
-    S.rebuild = 0;
   }
   int ng = 0;
   const f32x2 fscale2 = f32x2{D->rds_fir_scale, D->rds_fir_scale};
@@ -2045,7 +2127,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   const float psk_xr1 = D->psk_xr1, psk_xi1 = D->psk_xi1;
   const float alpha = D->rds_alpha, beta = D->rds_beta;
   const float dphi_psk = (float)(3.14159265358979323846 * (1.0 - 1.0 / 2));
-  const uint32_t ring0 = S.ring_pos;
+  const uint32_t ring0 = G.ring_pos;
   int nmax = count, cmin = act ? count : 0x7fffffff;
   for (int d = 32; d >= 1; d >>= 1) {
     nmax = max(nmax, __shfl_xor(nmax, d));
@@ -2365,32 +2447,35 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   }
   if (!act) return;
   // ---- registers -> state ----
-  S.theta = theta;
-  S.dtheta = dtheta;
-  S.sample_since_reset = ssr;
-  S.prev_f0 = prev_f0;
-  S.phase0 = phase0;
+  FmxRdsState *out = a.st + c;
+  out->theta = theta;
+  out->dtheta = dtheta;
+  out->prev_f0 = prev_f0;
+  out->phase0 = phase0;
+  out->sample_since_reset = ssr;
+  out->ring_pos = ring0 + (uint32_t)count;
+  out->rebuild = 0;
   for (int i = 0; i < FMX_RDS_NACC; ++i) {
-    S.acc_re[i] = acc[i].x;
-    S.acc_im[i] = acc[i].y;
+    out->acc_re[i] = acc[i].x;
+    out->acc_im[i] = acc[i].y;
   }
-  S.agc_g = agc_g;
-  S.agc_y2p = agc_y2p;
-  S.ss_rate = ss_rate;
-  S.ss_del = ss_del;
-  S.ss_tau = ss_tau;
-  S.ss_q_hat = ss_q_hat;
-  S.ss_v1 = ss_v1;
-  S.ss_b = ss_b;
-  S.ss_decim = ss_decim;
-  S.ss_mf_valid = ss_valid;
+  out->agc_g = agc_g;
+  out->agc_y2p = agc_y2p;
   for (int m = 0; m < FMX_SS_SUB; ++m) {
     const f32x2 w = L.win[wp + 1 + m][lane];
-    S.ss_win_re[m] = w.x;
-    S.ss_win_im[m] = w.y;
+    out->ss_win_re[m] = w.x;
+    out->ss_win_im[m] = w.y;
   }
-  S.ring_pos = ring0 + (uint32_t)count;
-  a.st[c] = S;
+  out->ss_mf_valid = ss_valid;
+  out->ss_rate = ss_rate;
+  out->ss_del = ss_del;
+  out->ss_tau = ss_tau;
+  out->ss_q_hat = ss_q_hat;
+  out->ss_v1 = ss_v1;
+  out->ss_v2 = G.ss_v2;
+  out->ss_b = ss_b;
+  out->ss_decim = ss_decim;
+  rds_bits_store(*out, S);
   if (a.group_count) a.group_count[c] = ng;
   RDS_STAMP(6)
 #ifdef FMX_STAMPS
