@@ -557,6 +557,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
 static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   FeArgs a{};
   a.des = h->ddes;
+  a.des_fs = h->hdes->fs;
   a.par = h->dpar;
   a.C = h->C;
   a.n = n;
@@ -662,7 +663,11 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
   const int buf = static_cast<int>(h->step & 1);
-  // buffers of parity `buf` were last read by step k-2 on sB / sC / sD
+  // buffers of parity `buf` were last read by step k-2 on sB / sC, and by its
+  // audio on sD in mono mode.  In stereo mode the audio of step k-2 only
+  // reads raw L/R, but waiting for it anyway throttles the frontend: measured,
+  // letting the frontends run ahead starves the PLL / audio chain (2.25 vs
+  // 1.61 ms per step, tools/gpu_timeline.sh)
   if (h->evB_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf], 0));
   if (h->evC_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf], 0));
   if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));

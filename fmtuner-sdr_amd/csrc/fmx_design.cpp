@@ -315,6 +315,9 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
   }
   for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
     for (int k = 0; k < d->iq_len[i]; ++k) d->iq_pad[i][k + 5] = d->iq_taps[i][k];
+  for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
+    for (int k = 0; k < d->iq_len[i]; ++k) d->iq_z16[i][k + 16] = d->iq_taps[i][k];
+  for (int k = 0; k < d->pilot_len; ++k) d->pilot_z16[k + 16] = d->pilot_taps[k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
   for (int k = 0; k + 1 < FMX_PILOT_MAX + FMX_PAD; ++k) {
     d->pilot_pair[k][0] = d->pilot_pad[k];

@@ -47,12 +47,14 @@ typedef struct {
   float iq_scale[FMX_IQ_DESIGNS];
   float iq_taps[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN];
   float iq_pad[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN + FMX_PAD]; // [k + 5] = taps[k], zeros around
+  float iq_z16[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN + 32]; // [k + 16] = taps[k], 16 zeros each side (k_fe8)
   float fd_ref;          // 1 / (2 pi kf), kf = 75 kHz / Fs
   float deemph_alpha[2]; // 50 us, 75 us at out_rate (fm_demod.cpp:119-131)
   // StereoDecoder (stereo_decoder.cpp:25-63)
   int pilot_len, delay_len; // delay_len = delaySamples + 1 (ring size)
   float pilot_taps[FMX_PILOT_MAX];
   float pilot_pad[FMX_PILOT_MAX + FMX_PAD];
+  float pilot_z16[FMX_PILOT_MAX + 32]; // [k + 16] = taps[k], 16 zeros each side (k_fe8)
   float pilot_pair[FMX_PILOT_MAX + FMX_PAD][2] __attribute__((aligned(8))); // {pad[k], pad[k+1]}: packed-FMA tap pairs
   float lr_scale;
   float lr_taps[FMX_LR_LEN];

@@ -37,6 +37,7 @@ enum FeInMode { FE_IN_U8_DECIM = 0, FE_IN_CF = 1, FE_IN_U8_DIRECT = 2, FE_IN_MPX
 
 struct FeArgs {
   const FmxDesign *des;
+  int des_fs;        // DSP rate (host copy of des->fs, for the launcher)
   const FmxChanParam *par;
   int C, n, in_mode;
   // inputs

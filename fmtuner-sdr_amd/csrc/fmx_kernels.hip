@@ -27,6 +27,8 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fmx_internal.h"
 #include "fmx_math.h"
 #include "fmx_synth.h"
@@ -363,6 +365,60 @@ struct SigAcc {
     sample((w >> 16) & 255u, w >> 24);
   }
 };
+
+// RF-level epilogue of a frontend workgroup (computeSignalLevel +
+// smoothSignalLevel, signal_level.cpp:145-214): block-reduce the exact byte
+// sums, then thread 0 evaluates the reference's formulas in double.
+__device__ __forceinline__ void fe_signal_level(const FeArgs &a, const SigAcc &sig, unsigned long long *sgp, int c,
+                                                long samples, int lane, int wave, int tid) {
+  unsigned long long v[6] = {sig.sI, sig.sQ, sig.sII, sig.sQQ, sig.hard, sig.nearc};
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    for (int d = 32; d >= 1; d >>= 1) v[k] += __shfl_xor(v[k], d);
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) sgp[wave * 6 + k] = v[k];
+  __syncthreads();
+  if (tid != 0) return;
+  double t[6];
+  for (int k = 0; k < 6; ++k) t[k] = (double)(sgp[k] + sgp[6 + k] + sgp[12 + k] + sgp[18 + k]);
+  fmx_signal_level r;
+  r.level120 = 0.0f;
+  r.dbfs = -120.0;
+  r.compensated_dbfs = -120.0;
+  r.hard_clip_ratio = 0.0;
+  r.near_clip_ratio = 0.0;
+  if (samples > 0) {
+    // sums of (b - 127.5) / 127.5 and its square from the exact byte sums
+    const double nn = (double)samples, k1 = 1.0 / 127.5;
+    const double sumI = (t[0] - 127.5 * nn) * k1, sumQ = (t[1] - 127.5 * nn) * k1;
+    const double sumII = (t[2] - 255.0 * t[0] + 16256.25 * nn) * (k1 * k1);
+    const double sumQQ = (t[3] - 255.0 * t[1] + 16256.25 * nn) * (k1 * k1);
+    const double meanI = sumI / nn, meanQ = sumQ / nn;
+    const double varI = fmax(0.0, (sumII / nn) - (meanI * meanI));
+    const double varQ = fmax(0.0, (sumQQ / nn) - (meanQ * meanQ));
+    const double rms = sqrt(fmax(1e-15, 0.5 * (varI + varQ)));
+    const double *sp = a.sig_par + 4 * (size_t)c;  // gain*factor, bias, floor, ceil
+    r.dbfs = 20.0 * log10(rms + 1e-12);
+    r.compensated_dbfs = r.dbfs - sp[0] + sp[1];
+    const double safeCeil = fmax(sp[3], sp[2] + 1.0);
+    const double norm = (r.compensated_dbfs - sp[2]) / (safeCeil - sp[2]);
+    const float l = (float)(norm * 120.0);
+    r.level120 = l < 0.0f ? 0.0f : (l > 120.0f ? 120.0f : l);
+    r.hard_clip_ratio = t[4] / nn;
+    r.near_clip_ratio = t[5] / nn;
+  }
+  // smoothSignalLevel (signal_level.cpp:206-214)
+  float *sm = a.sig_smooth + 2 * (size_t)c;
+  if (sm[1] == 0.0f) {
+    sm[0] = r.level120;
+    sm[1] = 1.0f;
+  } else {
+    const float alpha = (r.level120 > sm[0]) ? 0.42f : 0.18f;
+    sm[0] += (r.level120 - sm[0]) * alpha;
+  }
+  r.level120_smoothed = sm[0];
+  a.sig_out[c] = r;
+}
 
 // LDS layout of k_frontend (shared with the launcher's size computation).
 // VEC: the decimator input is natural-order u8 IQ (HB halo bytes + the
@@ -868,57 +924,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 #undef FE_STAMP
   if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
     a.clip_out[c] = (n > 0) ? (float)sh->clip / (float)n : 0.0f;
-  if (want_sig) {
-    unsigned long long v[6] = {sig.sI, sig.sQ, sig.sII, sig.sQQ, sig.hard, sig.nearc};
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      for (int d = 32; d >= 1; d >>= 1) v[k] += __shfl_xor(v[k], d);
-    if (lane == 0)
-      for (int k = 0; k < 6; ++k) sgp[wave * 6 + k] = v[k];
-    __syncthreads();
-    if (tid == 0) {
-      double t[6];
-      for (int k = 0; k < 6; ++k) t[k] = (double)(sgp[k] + sgp[6 + k] + sgp[12 + k] + sgp[18 + k]);
-      fmx_signal_level r;
-      r.level120 = 0.0f;
-      r.dbfs = -120.0;
-      r.compensated_dbfs = -120.0;
-      r.hard_clip_ratio = 0.0;
-      r.near_clip_ratio = 0.0;
-      const long samples = (long)n * ((a.in_mode == FE_IN_U8_DECIM) ? M : 1);
-      if (samples > 0) {
-        // sums of (b - 127.5) / 127.5 and its square from the exact byte sums
-        const double nn = (double)samples, k1 = 1.0 / 127.5;
-        const double sumI = (t[0] - 127.5 * nn) * k1, sumQ = (t[1] - 127.5 * nn) * k1;
-        const double sumII = (t[2] - 255.0 * t[0] + 16256.25 * nn) * (k1 * k1);
-        const double sumQQ = (t[3] - 255.0 * t[1] + 16256.25 * nn) * (k1 * k1);
-        const double meanI = sumI / nn, meanQ = sumQ / nn;
-        const double varI = fmax(0.0, (sumII / nn) - (meanI * meanI));
-        const double varQ = fmax(0.0, (sumQQ / nn) - (meanQ * meanQ));
-        const double rms = sqrt(fmax(1e-15, 0.5 * (varI + varQ)));
-        const double *sp = a.sig_par + 4 * (size_t)c;  // gain*factor, bias, floor, ceil
-        r.dbfs = 20.0 * log10(rms + 1e-12);
-        r.compensated_dbfs = r.dbfs - sp[0] + sp[1];
-        const double safeCeil = fmax(sp[3], sp[2] + 1.0);
-        const double norm = (r.compensated_dbfs - sp[2]) / (safeCeil - sp[2]);
-        const float l = (float)(norm * 120.0);
-        r.level120 = l < 0.0f ? 0.0f : (l > 120.0f ? 120.0f : l);
-        r.hard_clip_ratio = t[4] / nn;
-        r.near_clip_ratio = t[5] / nn;
-      }
-      // smoothSignalLevel (signal_level.cpp:206-214)
-      float *sm = a.sig_smooth + 2 * (size_t)c;
-      if (sm[1] == 0.0f) {
-        sm[0] = r.level120;
-        sm[1] = 1.0f;
-      } else {
-        const float alpha = (r.level120 > sm[0]) ? 0.42f : 0.18f;
-        sm[0] += (r.level120 - sm[0]) * alpha;
-      }
-      r.level120_smoothed = sm[0];
-      a.sig_out[c] = r;
-    }
-  }
+  if (want_sig) fe_signal_level(a, sig, sgp, c, (long)n * ((a.in_mode == FE_IN_U8_DECIM) ? M : 1), lane, wave, tid);
 }
 
 /* ================================================================== */
@@ -2612,6 +2618,513 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
 }
 
 /* ================================================================== */
+/* k_fe8: the steady-state frontend, 8 consecutive outputs per thread  */
+/* ================================================================== */
+/* The VEC path of k_frontend (u8 IQ, full decimator history) for calls of
+ * whole FE8_T-sample chunks -- every fmx_process_block call of a running
+ * receiver and of the bench.  Same stages and per-output arithmetic; each
+ * thread owns 8 consecutive DSP samples, so every input sample it reads
+ * feeds 8 outputs:
+ *   decimator     one 16-B LDS read = 8 IQ samples -> up to 64 packed (I,Q)
+ *                 FMAs; the window is fully unrolled, zero taps never issued
+ *   DC blockers   8-element affine maps per thread, block scan, recompute
+ *   IQ FIR        complex: 1 ds_read_b64 per input -> 8 packed FMAs
+ *   pilot BPF     1 ds_read_b32 per input -> 4 packed FMAs (output pairs)
+ *   RDS resampler packed (branch, next branch) chain on the MPX image
+ * The IQ and MPX images in LDS are padded (element i at i + i/8): lanes 8
+ * elements apart read distinct banks.  ~76 KB of LDS per workgroup, two
+ * workgroups (8 waves) per CU. */
+#define FE8_T 2048
+__device__ __forceinline__ int fe8_i(int i) { return i + (i >> 3); }
+
+template <int M, int TPP> struct Fe8Layout {
+  static constexpr int L = M * TPP;
+  static constexpr int G = (7 * M + L + 1 + 7) / 8;                 // 8-sample groups per thread window
+  static constexpr int HB = 2 * L;                                   // halo bytes (L samples)
+  static constexpr int RAW_BYTES = HB + 2 * FE8_T * M + 16;
+  static constexpr int YB_BYTES = (FE8_T + 1) * 8;
+  static constexpr int R0 = ((RAW_BYTES > YB_BYTES ? RAW_BYTES : YB_BYTES) + 15) & ~15;
+  static constexpr int XN = (FE_HALO_IQ + FE8_T + 16) * 9 / 8 + 8;   // padded complex image
+  static constexpr int MN = (FMX_HIST + FE8_T + 16) * 9 / 8 + 8;     // padded MPX image
+  static constexpr int XIN = R0;
+  static constexpr int MX = XIN + XN * 8;
+  static constexpr int RST = (MX + MN * 4 + 15) & ~15;               // RDS resampler bank [26][33]
+  static constexpr int SG = (RST + FMX_RDS_RS_SUB * (FMX_NPFB + 1) * 4 + 15) & ~15;
+  static constexpr int SH = SG + 4 * 6 * 8;
+  static constexpr int BYTES = SH + (int)sizeof(FeShared);
+  static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256);
+};
+
+// 8 outputs j0..j0+7 of a real-tap FIR of runtime length P on a padded LDS
+// image x (input i at x[fe8_i(i)]); hz = taps with 16 zeros on each side
+// (hz[16 + k] = h[k]).  Per output the FMA chain runs oldest input first, as
+// fir_r3; outputs (2q, 2q+1) share one packed FMA.
+__device__ __forceinline__ void fir8_r(const float *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x2{0.0f, 0.0f};
+#pragma unroll 2
+  for (int m0 = 0; m0 < P + 7; m0 += 8) {
+    // input j0-(P-1)+m0+u feeds output r with tap (P-1)-m0+r-u = tw[7+r-u]
+    const FMX_CONST float *tw = cptr(hz) + 16 + (P - 1) - m0 - 7;
+    float t[16];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) t[k] = tw[k];
+    t[15] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float v = x[fe8_i(j0 - (P - 1) + m0 + u)];
+      const f32x2 vv = {v, v};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_elementwise_fma(f32x2{t[7 + 2 * q - u], t[8 + 2 * q - u]}, vv, acc[q]);
+    }
+  }
+}
+// Complex input (float2 image), real taps: 8 outputs as packed (re, im).
+__device__ __forceinline__ void fir8_c(const float2 *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[8]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
+#pragma unroll 2
+  for (int m0 = 0; m0 < P + 7; m0 += 8) {
+    const FMX_CONST float *tw = cptr(hz) + 16 + (P - 1) - m0 - 7;
+    float t[16];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) t[k] = tw[k];
+    t[15] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float2 v = x[fe8_i(j0 - (P - 1) + m0 + u)];
+      const f32x2 vv = {v.x, v.y};
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float h = t[7 + r - u];
+        acc[r] = __builtin_elementwise_fma(f32x2{h, h}, vv, acc[r]);
+      }
+    }
+  }
+}
+
+template <int M, int TPP>
+__global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  using LY = Fe8Layout<M, TPP>;
+  constexpr int L = LY::L;
+  uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
+  float2 *yb = reinterpret_cast<float2 *>(smem);
+  float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
+  float *mx = reinterpret_cast<float *>(smem + LY::MX);
+  float(*rst)[FMX_NPFB + 1] = reinterpret_cast<float(*)[FMX_NPFB + 1]>(smem + LY::RST);
+  unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
+  FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const bool want_sig = a.sig_out != nullptr;
+#ifdef FMX_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
+#define FE_STAMP(k)                                              \
+  if (a.dbg && threadIdx.x == 0) {                               \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+    st_acc[k] += t_ - st_last;                                   \
+    st_last = t_;                                                \
+  }
+#else
+#define FE_STAMP(k)
+#endif
+  SigAcc sig;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int j0 = 8 * tid;
+  const FmxDesign *__restrict__ D = a.des;
+  const int n = a.n;
+  const FmxChanParam par = a.par[c];
+  const int iqL = D->iq_len[par.iqsel];
+  const float *__restrict__ iqz = D->iq_z16[par.iqsel];
+  const float iqscale = D->iq_scale[par.iqsel];
+  const bool pilot = a.pilot_out != nullptr;
+  const bool rds = a.rds_out != nullptr;
+  const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
+  const float dc_c = -dc_a1;
+
+  // ---- zeroed images, carried state ----
+  for (int h = tid; h < LY::XN; h += 256) xin[h] = make_float2(0.0f, 0.0f);
+  for (int h = tid; h < LY::MN; h += 256) mx[h] = 0.0f;
+  __syncthreads();
+  for (int h = tid; h < FE_HALO_IQ; h += 256) {
+    const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
+    xin[fe8_i(h)] = make_float2(v.x, v.y);
+  }
+  if (tid == 0) {
+    sh->carry_i = a.dc_v[2 * c];
+    sh->carry_q = a.dc_v[2 * c + 1];
+    sh->fd_re = a.fd_prev[2 * c];
+    sh->fd_im = a.fd_prev[2 * c + 1];
+    sh->clip = 0;
+  }
+  {
+    const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
+    for (int h = tid; h < FMX_HIST; h += 256) mx[fe8_i(h)] = pilot ? hist[h] : 0.0f;
+  }
+  float agc_g = 1.0f, agc_y2p = 1.0f;
+  if (par.agc != 0 && tid == 0) {
+    agc_g = a.agc[2 * c];
+    agc_y2p = a.agc[2 * c + 1];
+  }
+  const float agc_bw = (par.agc == 1) ? 0.01f : 0.001f;
+  const uint16_t *iq16 = reinterpret_cast<const uint16_t *>(a.iq + (size_t)c * a.iq_stride);
+  const uint8_t *dhist = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
+  const FmxSched *sched = nullptr;
+  int sched_n = 0;
+  float rds_keep = 0.0f; // the RDS resampler's own window of the previous call (32 samples)
+  if (rds) {
+    const int g = a.rds_group[c];
+    sched = a.rds_sched + (size_t)g * a.rds_sched_stride;
+    sched_n = a.rds_sched_n[g];
+    if (tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
+    for (int k = tid; k < FMX_NPFB * FMX_RDS_RS_SUB; k += 256) {
+      const int b = k / FMX_RDS_RS_SUB, nn = k % FMX_RDS_RS_SUB;
+      rst[nn][b] = D->rds_rs_h[k];
+      if (b == 0) rst[nn][FMX_NPFB] = D->rds_rs_h[k]; // column 32 = branch 0 (a boundary pairs 31 with 0)
+    }
+  }
+  int e_pos = 0;
+  u32x4 pf[LY::NPF];
+  auto prefetch = [&](int n0p) {
+    const uint8_t *base = a.iq + (size_t)c * a.iq_stride + 2L * n0p * M - LY::HB;
+#pragma unroll
+    for (int j = 0; j < LY::NPF; ++j) {
+      const int off = 16 * (tid + 256 * j);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (off < LY::HB + 2 * FE8_T * M && (n0p > 0 || off >= LY::HB))
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off));
+      pf[j] = v;
+    }
+  };
+  prefetch(0);
+  __syncthreads();
+
+  for (int n0 = 0; n0 < n; n0 += FE8_T) {
+    if (rds && tid == 0) sh->e_end = e_pos;
+    FE_STAMP(7)
+    // ================= decimator =================
+#pragma unroll
+    for (int j = 0; j < LY::NPF; ++j) {
+      const int off = 16 * (tid + 256 * j);
+      if (off < LY::HB + 2 * FE8_T * M && (n0 > 0 || off >= LY::HB)) *reinterpret_cast<u32x4 *>(raw + off) = pf[j];
+      if (want_sig && off >= LY::HB && off < LY::HB + 2 * FE8_T * M) {
+        sig.word(pf[j].x);
+        sig.word(pf[j].y);
+        sig.word(pf[j].z);
+        sig.word(pf[j].w);
+      }
+    }
+    if (n0 == 0) // halo: a zero lead sample, then the carried L-1 samples (full history)
+      for (int h = tid; h < L; h += 256) {
+        const int hh = h - 1;
+        uint16_t v = 0;
+        if (hh >= 0) v = (uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8);
+        reinterpret_cast<uint16_t *>(raw)[h] = v;
+      }
+    if (n0 + FE8_T < n) prefetch(n0 + FE8_T);
+    __syncthreads();
+    {
+      // thread window: samples s = 0 .. 8G-1 from raw sample 8*M*tid; output
+      // r uses s in [r*M + 1, r*M + L] with tap L + r*M - s
+      f32x2 acc[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
+      const u32x4 *rw = reinterpret_cast<const u32x4 *>(raw) + M * tid;
+      const FMX_CONST float *hd = cptr(D->dec_taps);
+      const f32x2 off = {-127.5f, -127.5f};
+      // one group of 8 samples: live (s, r) pairs known at compile time
+      // (head / tail of the window), or all live (middle, runtime loop with
+      // the tap base in SGPRs)
+      auto group = [&](int g, auto live_known) __attribute__((always_inline)) {
+        const u32x4 w = rw[g];
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+        // tap of (u, r) = hb[r*M - u]; the opaque zero keeps the compiler from
+        // hoisting every group's tap loads into SGPRs at once (spills)
+        int z;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        const FMX_CONST float *hb = hd + (L - 8 * g + z);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          constexpr bool known = decltype(live_known)::value;
+          if (known) {
+            bool live = false;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) live = live || (8 * g + u >= r * M + 1 && 8 * g + u <= r * M + L);
+            if (!live) continue;
+          }
+          const uint32_t wd = ww[u >> 1];
+          const int sh0 = (u & 1) ? 16 : 0;
+          f32x2 x;
+          x.x = (float)((wd >> sh0) & 255u);
+          x.y = (float)((wd >> (sh0 + 8)) & 255u);
+          x = x + off;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            if (known) {
+              const int k = L + r * M - (8 * g + u);
+              if (k < 0 || k >= L) continue;
+            }
+            const float h = hb[r * M - u];
+            acc[r] = __builtin_elementwise_fma(f32x2{h, h}, x, acc[r]);
+          }
+        }
+      };
+      constexpr int GH = (7 * M + 1 + 7) / 8;  // first group where every output is live
+      constexpr int GT = (L - 7) / 8;          // last such group
+#pragma unroll
+      for (int g = 0; g < GH; ++g) group(g, std::true_type{});
+#pragma unroll 2
+      for (int g = GH; g <= GT; ++g) group(g, std::false_type{});
+#pragma unroll
+      for (int g = GT + 1; g < LY::G; ++g) group(g, std::true_type{});
+      int myclip = 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float yr = acc[r].x * D->dec_scale;
+        const float yi = acc[r].y * D->dec_scale;
+        if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
+        xin[fe8_i(FE_HALO_IQ + j0 + r)] = make_float2(yr, yi);
+      }
+      if (myclip) atomicAdd(&sh->clip, myclip);
+    }
+    __syncthreads(); // raw aliases yb
+    FE_STAMP(0)
+    // ================= DC blockers: affine scan, 8 per thread =================
+    {
+      float2 xv[8];
+      float A = 1.0f, BI = 0.0f, BQ = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        xv[r] = xin[fe8_i(FE_HALO_IQ + j0 + r)];
+        BI = xv[r].x + dc_c * BI;
+        BQ = xv[r].y + dc_c * BQ;
+        A = dc_c * A;
+      }
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float pA = __shfl_up(A, d), pI = __shfl_up(BI, d), pQ = __shfl_up(BQ, d);
+        if (lane >= d) {
+          BI = A * pI + BI;
+          BQ = A * pQ + BQ;
+          A = A * pA;
+        }
+      }
+      if (lane == 63) {
+        sh->wave_a[wave] = A;
+        sh->wave_bi[wave] = BI;
+        sh->wave_bq[wave] = BQ;
+      }
+      float eA = __shfl_up(A, 1), eI = __shfl_up(BI, 1), eQ = __shfl_up(BQ, 1);
+      if (lane == 0) {
+        eA = 1.0f;
+        eI = 0.0f;
+        eQ = 0.0f;
+      }
+      __syncthreads();
+      float vI = sh->carry_i, vQ = sh->carry_q;
+      for (int w = 0; w < wave; ++w) {
+        vI = sh->wave_a[w] * vI + sh->wave_bi[w];
+        vQ = sh->wave_a[w] * vQ + sh->wave_bq[w];
+      }
+      vI = eA * vI + eI;
+      vQ = eA * vQ + eQ;
+      // the state before this thread's first element, then the reference's op order
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float tI = dc_a1 * vI, tQ = dc_a1 * vQ;
+        const float nI = xv[r].x - tI, nQ = xv[r].y - tQ;
+        xin[fe8_i(FE_HALO_IQ + j0 + r)] = make_float2(nI - vI, nQ - vQ);
+        vI = nI;
+        vQ = nQ;
+      }
+      __syncthreads();
+      if (tid == 255) {
+        sh->carry_i = vI;
+        sh->carry_q = vQ;
+      }
+    }
+    __syncthreads();
+    FE_STAMP(1)
+    // ================= IQ FIR =================
+    {
+      f32x2 z[8];
+      fir8_c(xin, FE_HALO_IQ + j0, iqz, iqL, z);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) yb[1 + j0 + r] = make_float2(z[r].x * iqscale, z[r].y * iqscale);
+      if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
+    }
+    __syncthreads();
+    // ================= AGC (serial, only when enabled) =================
+    if (par.agc != 0) {
+      if (tid == 0) {
+        for (int j = 0; j < FE8_T; ++j) {
+          const float2 x = yb[1 + j];
+          const float yr = x.x * agc_g, yi = x.y * agc_g;
+          const float y2 = yr * yr + yi * yi;
+          agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
+          if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
+          if (agc_g > 1e6f) agc_g = 1e6f;
+          yb[1 + j] = make_float2(yr, yi);
+        }
+      }
+      __syncthreads();
+    }
+    FE_STAMP(2)
+    // ================= discriminator =================
+    {
+      const float ref = D->fd_ref;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = tid + 256 * k;
+        const float2 p = yb[j], r = yb[1 + j];
+        const float re = p.x * r.x + p.y * r.y;
+        const float im = p.x * r.y - p.y * r.x;
+        const float m = atan2f(im, re) * ref;
+        mx[fe8_i(FMX_HIST + j)] = m;
+        if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
+      }
+      if (tid == 0) {
+        sh->fd_re = yb[FE8_T].x;
+        sh->fd_im = yb[FE8_T].y;
+      }
+    }
+    __syncthreads();
+    FE_STAMP(3)
+    // RDS schedule entries of this chunk, fetched before the pilot FIR
+    FmxSched en[8];
+    if (rds) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e_pos + tid + 256 * k;
+        en[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
+      }
+    }
+    // ================= 19 kHz pilot band-pass =================
+    if (pilot) {
+      f32x2 z[4];
+      fir8_r(mx, FMX_HIST + j0, D->pilot_z16, D->pilot_len, z);
+      float4 *po = reinterpret_cast<float4 *>(a.pilot_out + (size_t)c * a.pilot_stride + n0 + j0);
+      po[0] = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
+      po[1] = make_float4(z[2].x, z[2].y, z[3].x, z[3].y);
+    }
+    FE_STAMP(4)
+    // ================= RDS resampler 240k -> 171k =================
+    if (rds) {
+      if (n0 == 0) { // first chunk: the resampler's own window before this call
+        __syncthreads();
+        if (tid < 32) mx[fe8_i(FMX_HIST - 32 + tid)] = rds_keep;
+        __syncthreads();
+      }
+      int last = -1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e_pos + tid + 256 * k;
+        if (e < sched_n && (en[k].packed & 0xFFFF) < n0 + FE8_T) {
+          const int i = (en[k].packed & 0xFFFF) - n0;
+          const int b = (en[k].packed >> 16) & 0xFF;
+          const bool boundary = (en[k].packed >> 24) & 1;
+          const int bb = boundary ? FMX_NPFB - 1 : b;
+          const int w0 = FMX_HIST + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1);
+          f32x2 y = {0.0f, 0.0f};
+#pragma unroll
+          for (int m = 0; m < FMX_RDS_RS_SUB; ++m) {
+            const float h0 = rst[FMX_RDS_RS_SUB - 1 - m][bb], h1 = rst[FMX_RDS_RS_SUB - 1 - m][bb + 1];
+            const float va = mx[fe8_i(w0 + m)], vb = mx[fe8_i(w0 + m + 1)];
+            const f32x2 p = f32x2{h0, h1} * f32x2{va, boundary ? vb : va};
+            y = y + p;
+          }
+          const float w0f = (1.0f - en[k].mu) * y.x;
+          const float w1f = en[k].mu * y.y;
+          a.rds_out[(size_t)c * a.rds_stride + e] = w0f + w1f;
+          last = e;
+        }
+      }
+      if (last >= 0) atomicMax(&sh->e_end, last + 1);
+    }
+    __syncthreads();
+    if (rds) e_pos = sh->e_end;
+    FE_STAMP(5)
+    // ================= carry halos to the next chunk =================
+    {
+      float2 cx = make_float2(0.0f, 0.0f);
+      if (tid < FE_HALO_IQ) cx = xin[fe8_i(tid + FE8_T)];
+      const float cm0 = mx[fe8_i(tid + FE8_T)], cm1 = mx[fe8_i(tid + 256 + FE8_T)];
+      __syncthreads();
+      if (tid < FE_HALO_IQ) xin[fe8_i(tid)] = cx;
+      mx[fe8_i(tid)] = cm0;
+      mx[fe8_i(tid + 256)] = cm1;
+      __syncthreads();
+    }
+  }
+
+  // ---- write back state ----
+  {
+    const long total = (long)n * M;
+    uint16_t keep[2];
+    int cntk = 0;
+    for (int h = tid; h < L - 1; h += 256) keep[cntk++] = iq16[total - (L - 1) + h];
+    __syncthreads();
+    cntk = 0;
+    uint8_t *dh = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
+    for (int h = tid; h < L - 1; h += 256) {
+      const uint16_t v = keep[cntk++];
+      dh[2 * h] = (uint8_t)(v & 255);
+      dh[2 * h + 1] = (uint8_t)(v >> 8);
+    }
+    if (tid == 0) a.dec_valid[c] = L - 1;
+  }
+  for (int h = tid; h < FE_HALO_IQ; h += 256) {
+    const float2 v = xin[fe8_i(h)];
+    a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{v.x, v.y};
+  }
+  if (tid == 0) {
+    a.dc_v[2 * c] = sh->carry_i;
+    a.dc_v[2 * c + 1] = sh->carry_q;
+    a.fd_prev[2 * c] = sh->fd_re;
+    a.fd_prev[2 * c + 1] = sh->fd_im;
+    if (par.agc != 0) {
+      a.agc[2 * c] = agc_g;
+      a.agc[2 * c + 1] = agc_y2p;
+    }
+  }
+  if (pilot) {
+    float *hist = a.st_hist_wr + (size_t)c * FMX_HIST;
+    for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[fe8_i(h)];
+  }
+  if (rds) {
+    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = mx[fe8_i(FMX_HIST - 32 + tid)];
+    if (tid == 0) a.rds_count[c] = sched_n;
+  }
+  if (tid == 0 && a.clip_out) a.clip_out[c] = (float)sh->clip / (float)n;
+  FE_STAMP(6)
+#ifdef FMX_STAMPS
+  if (a.dbg && tid == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, st_acc[k]);
+#endif
+#undef FE_STAMP
+  if (want_sig) fe_signal_level(a, sig, sgp, c, (long)n * M, lane, wave, tid);
+}
+
+template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
+  static_assert(Fe8Layout<M, TPP>::BYTES <= 80 * 1024, "k_fe8 must fit two workgroups per CU");
+  const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
+  static bool configured = false;
+  if (!configured) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fe8<M, TPP>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+      return FMX_E_HIP;
+    configured = true;
+  }
+  hipLaunchKernelGGL((k_fe8<M, TPP>), dim3(a.C), dim3(256), smem, st, a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+
+/* ================================================================== */
 /* launchers                                                           */
 /* ================================================================== */
 template <int M, int TPP, bool VEC> static int fe_launch(const FeArgs &a, hipStream_t st) {
@@ -2636,6 +3149,18 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1, false>(a, st);
   vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
+  // steady state: whole 2048-sample chunks, full history, no complex
+  // decimator output, 16-B pilot rows, RDS rate ratio < 0.9 (<= 8 resampler
+  // outputs per thread and chunk) -> k_fe8
+  const bool fe8 = vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
+                   (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
+                   a.des_fs >= 190000;
+  if (fe8) {
+    if (M == 10 && tpp == 28) return fe8_launch<10, 28>(a, st);
+    if (M == 8 && tpp == 28) return fe8_launch<8, 28>(a, st);
+    if (M == 4 && tpp == 20) return fe8_launch<4, 20>(a, st);
+    if (M == 2 && tpp == 12) return fe8_launch<2, 12>(a, st);
+  }
   if (M == 10 && tpp == 28) return vec ? fe_launch<10, 28, true>(a, st) : fe_launch<10, 28, false>(a, st);
   if (M == 8 && tpp == 28) return vec ? fe_launch<8, 28, true>(a, st) : fe_launch<8, 28, false>(a, st);
   if (M == 4 && tpp == 20) return vec ? fe_launch<4, 20, true>(a, st) : fe_launch<4, 20, false>(a, st);
