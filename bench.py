@@ -25,9 +25,16 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fmtuner-sdr_amd"))
 
-# per-unit algorithmic figures
+# per-unit algorithmic figures: bytes and FLOP per input
+# IQ sample at M = 10 (stereo + RDS)
 BYTES_PER_IQ_FRONTEND = 2.0 + 0.4 + 0.4 + 4.0 * 0.7125 / 10.0   # u8 IQ in; MPX, pilot, RDS-rate out
 FLOP_PER_IQ_FRONTEND = 112.0 + 32.4 + 61.0 + 7.4                 # decim, IQ FIR, pilot BPF, RDS resampler
+PER_IQ = {  # kernel: (algorithmic HBM bytes, FLOP) per IQ sample
+    "frontend": (BYTES_PER_IQ_FRONTEND, FLOP_PER_IQ_FRONTEND),
+    "stereo": (0.4 + 0.8 + 0.8, 20.0),      # pilot + MPX + delayed MPX in, raw L/R out
+    "audio": (0.8 + 0.107, 48.0 + 3.0),     # raw L/R in, 32 kHz PCM out; L/R FIRs + AF
+    "rds": (4.0 * 0.7125 / 10.0, 15.0),     # 171 kHz samples in (groups out ~0)
+}
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3
 
@@ -152,15 +159,21 @@ def main():
         except Exception:
             traffic = None
     achieved_gbs = fe_bytes / fe_avg_s / 1e9
-    roof = {"bound": "hbm", "kernel": "k_frontend", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+    roof = {"bound": "hbm", "kernel": "k_fe8 (frontend)", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
             # the roof that binds this path (no MFMA: FIR/IIR/PLL work is FP32 VALU)
             "valu_view": {"achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                           "algorithmic_flop_per_launch": fe_flops}}
-    kern = {k: {"ms_total": round(v[0], 3), "launches": v[1], "avg_ms": round(v[0] / max(v[1], 1), 4)}
-            for k, v in ktimes.items()}
+    kern = {}
+    for k, v in ktimes.items():
+        avg_s = v[0] / max(v[1], 1) * 1e-3
+        bpi, fpi = PER_IQ[k]
+        kern[k] = {"ms_total": round(v[0], 3), "launches": v[1], "avg_ms": round(avg_s * 1e3, 4),
+                   # live in the pipelined timed region (co-running kernels included)
+                   "hbm_gbs": round(bpi * units / max(avg_s, 1e-12) / 1e9, 1),
+                   "fp32_tflops": round(fpi * units / max(avg_s, 1e-12) / 1e12, 3)}
 
     # ---- CPU baseline: the oracle on this box's host cores (rank 0, N=1) ----
     cpu = None
