@@ -50,6 +50,12 @@ class BlockOut(C.Structure):
                 ("d_signal", C.c_void_p)]
 
 
+class XdrPiState(C.Structure):
+    _fields_ = [("pi_buf", C.c_uint16 * 64), ("pi_err", C.c_uint8 * 8), ("fill", C.c_uint8),
+                ("pos", C.c_uint8), ("last_state", C.c_uint8), ("pad", C.c_uint8),
+                ("last_value", C.c_uint16), ("pad2", C.c_uint16)]
+
+
 class SynthConfig(C.Structure):
     _fields_ = [("iq_rate", C.c_int), ("kind", C.c_int), ("amplitude", C.c_float),
                 ("noise_std", C.c_float), ("seed_base", C.c_uint32),
@@ -97,6 +103,13 @@ def lib():
         "fmx_synth_device": (i, [vp, C.POINTER(SynthConfig), C.c_uint32, i, C.c_int64, i, vp, vp, sz]),
         "fmx_design_taps": (i, [C.POINTER(Config), i, fp, i]),
         "fmx_resamp_schedule": (i, [C.c_float, i, C.POINTER(C.c_int), fp, i]),
+        "fmx_xdr_pi_reset": (None, [C.POINTER(XdrPiState)]),
+        "fmx_xdr_rds_lines": (i, [C.POINTER(XdrPiState), vp, i, C.c_char_p, i]),
+        "fmx_xdr_scan_line": (i, [vp, vp, vp, i, C.c_char_p, i]),
+        "fmx_wav_header": (i, [C.c_uint32, vp]),
+        "fmx_pcm_to_s16": (i, [vp, vp, i, i, C.POINTER(C.c_float), vp]),
+        "fmx_iq_capture": (i, [C.c_char_p, vp, i, i]),
+        "fmx_iq_replay": (i, [C.c_char_p, C.c_longlong, i, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -253,3 +266,78 @@ def resamp_schedule(del_, n_in):
                                   packed.ctypes.data_as(C.POINTER(C.c_int)),
                                   mu.ctypes.data_as(C.POINTER(C.c_float)), cap)
     return packed[:k], mu[:k]
+
+
+# ---- host-side formats (fmx_host.cpp): XDR RDS / scan lines, WAV, IQ files ----
+class XdrRds:
+    """Per-channel XDRServer RDS state (PI debounce) turning fmx_rds_group
+    records into the server's "P"/"R" lines."""
+
+    def __init__(self):
+        self.st = XdrPiState()
+        lib().fmx_xdr_pi_reset(C.byref(self.st))
+
+    def lines(self, groups):
+        """groups: list of (a, b, c, d, errors) -> list of lines (no newline)."""
+        import numpy as np
+        n = len(groups)
+        arr = (RdsGroup * max(n, 1))()
+        for k, (a, b, c, d, e) in enumerate(groups):
+            arr[k] = RdsGroup(a, b, c, d, e, 0, 0)
+        cap = 32 * max(n, 1) + 1
+        buf = C.create_string_buffer(cap)
+        rc = lib().fmx_xdr_rds_lines(C.byref(self.st), C.cast(arr, C.c_void_p), n, buf, cap)
+        if rc < 0:
+            raise FmxError(f"fmx_xdr_rds_lines failed ({rc})")
+        return buf.value.decode().splitlines()
+
+
+def xdr_scan_line(freq_khz, level_sum, reads):
+    import numpy as np
+    f = np.ascontiguousarray(freq_khz, dtype=np.int32)
+    s = np.ascontiguousarray(level_sum, dtype=np.float64)
+    r = np.ascontiguousarray(reads, dtype=np.int32)
+    cap = 24 * len(f) + 2
+    buf = C.create_string_buffer(cap)
+    rc = lib().fmx_xdr_scan_line(f.ctypes.data, s.ctypes.data, r.ctypes.data, len(f), buf, cap)
+    if rc < 0:
+        raise FmxError(f"fmx_xdr_scan_line failed ({rc})")
+    return buf.value.decode()
+
+
+def wav_header(data_bytes):
+    import numpy as np
+    h = np.zeros(44, dtype=np.uint8)
+    lib().fmx_wav_header(data_bytes, h.ctypes.data)
+    return h.tobytes()
+
+
+def pcm_to_s16(left, right, volume_percent=100, volume_scale=0.85):
+    """Returns (interleaved int16 array, new volume_scale)."""
+    import numpy as np
+    l = np.ascontiguousarray(left, dtype=np.float32)
+    r = np.ascontiguousarray(right, dtype=np.float32)
+    out = np.zeros(2 * len(l), dtype=np.int16)
+    vs = C.c_float(volume_scale)
+    rc = lib().fmx_pcm_to_s16(l.ctypes.data, r.ctypes.data, len(l), volume_percent, C.byref(vs), out.ctypes.data)
+    if rc < 0:
+        raise FmxError("fmx_pcm_to_s16 failed")
+    return out, vs.value
+
+
+def iq_capture(path, iq, append=True):
+    import numpy as np
+    a = np.ascontiguousarray(iq, dtype=np.uint8)
+    rc = lib().fmx_iq_capture(path.encode(), a.ctypes.data, a.size // 2, 1 if append else 0)
+    if rc < 0:
+        raise FmxError("fmx_iq_capture failed")
+    return rc
+
+
+def iq_replay(path, sample_offset, n_samples):
+    import numpy as np
+    out = np.zeros(2 * n_samples, dtype=np.uint8)
+    k = lib().fmx_iq_replay(path.encode(), sample_offset, n_samples, out.ctypes.data)
+    if k < 0:
+        raise FmxError("fmx_iq_replay failed")
+    return out[:2 * k]

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 2
+#define FMX_ABI_VERSION 3
 
 enum {
   FMX_OK = 0,
@@ -230,6 +230,43 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap);
 /* liquid resamp_rrrf output schedule for rate 1/del over n_in inputs from
  * the reset state: packed = i | (branch << 16) | (boundary << 24). */
 int fmx_resamp_schedule(float del, int n_in, int *packed, float *mu, int cap);
+
+/* ---- host-side consumers of the GPU outputs ----
+ * The reference's wire and file formats, fed from fmx_process_block's
+ * outputs (copied to the host).  No GPU needed. */
+/* Per-channel PI debounce state of the XDR server (xdr_server.h:151-156). */
+typedef struct {
+  uint16_t pi_buf[64];
+  uint8_t pi_err[8];
+  uint8_t fill, pos, last_state, pad;
+  uint16_t last_value, pad2;
+} fmx_xdr_pi_state;
+/* XDRServer ctor / setFrequencyState reset (xdr_server.cpp:261-266, 465-470). */
+void fmx_xdr_pi_reset(fmx_xdr_pi_state *s);
+/* XDRServer::updateRDS for n groups of one channel (xdr_server.cpp:189-213,
+ * 403-457): writes the queued lines ("P%04X" + '?' per block-A error level,
+ * "R%04X%04X%04X%02X"), each ending in '\n', NUL-terminated.  Returns the bytes
+ * written, or -(bytes needed + 1) when cap is too small (then nothing is
+ * written and the state is unchanged). */
+int fmx_xdr_rds_lines(fmx_xdr_pi_state *s, const fmx_rds_group *groups, int n, char *out, int cap);
+/* Scan line of main.cpp:1069-1113 as XDRServer::pushScanLine queues it
+ * ("U" + "f=level,..." with level = (float)(level_sum / reads) at one
+ * decimal; points with reads == 0 skipped; empty when no point).  level_sum
+ * holds summed fmx_signal_level.level120 values.  Same return convention. */
+int fmx_xdr_scan_line(const int *freq_khz, const double *level_sum, const int *reads, int n, char *out, int cap);
+/* AudioOutput::writeWAVHeader (audio_output.cpp:1346-1377): 44 bytes for
+ * data_bytes of S16LE 32 kHz stereo.  Returns 44. */
+int fmx_wav_header(uint32_t data_bytes, uint8_t *out44);
+/* AudioOutput::write volume ramp (:1432-1467) + writeWAVData (:1379-1398):
+ * n stereo frames -> 2n interleaved int16; *volume_scale carries the sink's
+ * m_currentVolumeScale (initially 0.85).  Returns n. */
+int fmx_pcm_to_s16(const float *left, const float *right, int n, int volume_percent, float *volume_scale,
+                   int16_t *out);
+/* writeIqCapture (main.cpp:742-747): n raw I/Q byte pairs to path
+ * (append != 0 appends).  fmx_iq_replay reads n pairs at a sample offset
+ * back (returns the pairs read). */
+int fmx_iq_capture(const char *path, const uint8_t *iq, int n_samples, int append);
+int fmx_iq_replay(const char *path, long long sample_offset, int n_samples, uint8_t *out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,21 @@
+"""fmx_sincos (fmtuner-sdr_amd/csrc/fmx_math.h), the sin/cos every kernel's
+NCOs and PLL phase rotations use in place of the reference's float sin/cos
+(std::cos/std::sin at stereo_decoder.cpp:179-180, 219-220; std::polar
+at redsea_port/dsp/liquid_wrappers.cpp:122 and liquid_wrappers.hh:104): built for the host
+from the same header and checked against double-precision sin/cos over the
+phase range the kernels feed it.  The bound is < 1 ulp (faithful rounding)."""
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_sincos_within_one_ulp(tmp_path):
+    exe = str(tmp_path / "math_test")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(ROOT, "tests", "cpp", "math_test.cpp")],
+                   check=True, timeout=120)
+    out = subprocess.run([exe, "2000000"], check=True, capture_output=True, text=True, timeout=120).stdout
+    r = json.loads(out)
+    assert r["max_ulp"] < 1.0, r
+    assert r["max_abs"] < 1.2e-7, r
