@@ -41,10 +41,20 @@ def sum_counters(values, device="cpu"):
 
 
 def gather_levels(levels):
-    """levels: this rank's per-channel float tensor (equal length on every
-    rank).  Returns the concatenation over ranks in rank order."""
+    """levels: this rank's per-channel float tensor (shard lengths may differ
+    by one when C % world != 0).  Returns the concatenation over ranks in rank
+    order: lengths are exchanged first, shards padded to the longest for the
+    all_gather, and the padding dropped."""
     if not _ready():
         return levels
-    parts = [torch.empty_like(levels) for _ in range(dist.get_world_size())]
-    dist.all_gather(parts, levels)
-    return torch.cat(parts)
+    world = dist.get_world_size()
+    n = torch.tensor([levels.numel()], dtype=torch.int64, device=levels.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    lens = [int(x.item()) for x in ns]
+    width = max(lens)
+    padded = torch.zeros(width, dtype=levels.dtype, device=levels.device)
+    padded[:levels.numel()] = levels.reshape(-1)
+    parts = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(parts, padded)
+    return torch.cat([p[:k] for p, k in zip(parts, lens)])

@@ -50,8 +50,8 @@ def test_shard_covers_all_channels_balanced():
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_gloo_world2_gather_and_reduce():
-    world, total = 2, 16
+@pytest.mark.parametrize("world,total", [(2, 16), (2, 17), (3, 10)])
+def test_gloo_gather_and_reduce(world, total):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -64,5 +64,5 @@ def test_gloo_world2_gather_and_reduce():
         assert p.exitcode == 0
     for rank, b, e, allv, tmax, sums in res:
         assert allv == [0.5 * i for i in range(total)]
-        assert tmax == 2.0
-        assert sums == [total, 2.0]
+        assert tmax == float(world)
+        assert sums == [total, float(world)]
