@@ -457,9 +457,38 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
   } else {
-    HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
+    const char *cu = std::getenv("FMX_CU_SERIAL");
+    if (cu && cu[0]) {
+      // Experiment: pin the serial kernels (sB k_pll, sC k_rds) to every s-th
+      // CU ("s": both on CUs i % s == 0; "s,d": k_pll on i % s == 0, k_rds on
+      // i % s == s/2) and the data-parallel ones (sA, sD) to the rest
+      // (FMX_CU_PAR_ALL=1: everywhere).
+      const int s = std::max(2, std::atoi(cu));
+      const bool disjoint = std::strchr(cu, ',') != nullptr;
+      const bool par_all = std::getenv("FMX_CU_PAR_ALL") && std::getenv("FMX_CU_PAR_ALL")[0] == '1';
+      hipDeviceProp_t prop;
+      HIP_TRY(hipGetDeviceProperties(&prop, h->device));
+      const int ncu = prop.multiProcessorCount;
+      const int words = (ncu + 31) / 32;
+      std::vector<uint32_t> mb(words, 0), mc(words, 0), ma(words, 0);
+      for (int i = 0; i < ncu; ++i) {
+        const bool b = i % s == 0, c = disjoint ? i % s == s / 2 : b;
+        if (b) mb[i / 32] |= 1u << (i % 32);
+        if (c) mc[i / 32] |= 1u << (i % 32);
+        if (par_all || !(b || c)) ma[i / 32] |= 1u << (i % 32);
+      }
+      hipStream_t a2 = nullptr;
+      HIP_TRY(hipExtStreamCreateWithCUMask(&a2, words, ma.data()));
+      HIP_TRY(hipStreamDestroy(h->sA));
+      h->sA = a2;
+      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sB, words, mb.data()));
+      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sC, words, mc.data()));
+      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sD, words, ma.data()));
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+      HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+      HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
+    }
   }
   for (int b = 0; b < 2; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));

@@ -2632,8 +2632,11 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  *   pilot BPF     1 ds_read_b32 per input -> 4 packed FMAs (output pairs)
  *   RDS resampler packed (branch, next branch) chain on the MPX image
  * The IQ and MPX images in LDS are padded (element i at i + i/8): lanes 8
- * elements apart read distinct banks.  ~76 KB of LDS per workgroup, two
- * workgroups (8 waves) per CU. */
+ * elements apart read distinct banks.  The complex IQ image and the IQ FIR
+ * output alias the u8 input chunk (dead once the decimator's outputs are in
+ * registers); only the 120-sample IQ FIR history is carried separately.
+ * ~58 KB of LDS per workgroup: two workgroups (8 waves) per CU leave room
+ * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
 __device__ __forceinline__ int fe8_i(int i) { return i + (i >> 3); }
 
@@ -2643,16 +2646,20 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int HB = 2 * L;                                   // halo bytes (L samples)
   static constexpr int RAW_BYTES = HB + 2 * FE8_T * M + 16;
   static constexpr int YB_BYTES = (FE8_T + 1) * 8;
-  static constexpr int R0 = ((RAW_BYTES > YB_BYTES ? RAW_BYTES : YB_BYTES) + 15) & ~15;
   static constexpr int XN = (FE_HALO_IQ + FE8_T + 16) * 9 / 8 + 8;   // padded complex image
   static constexpr int MN = (FMX_HIST + FE8_T + 16) * 9 / 8 + 8;     // padded MPX image
-  static constexpr int XIN = R0;
-  static constexpr int MX = XIN + XN * 8;
+  static constexpr int XIN = 0;                                      // aliases raw
+  static constexpr int YB = XN * 8;                                  // aliases raw
+  static constexpr int NPC = (HB + 2 * FE8_T * M + 1023) / 1024;     // 1-KiB LDS-DMA pieces per chunk
+  static constexpr int RAW_ALLOC = NPC * 1024 > RAW_BYTES ? NPC * 1024 : RAW_BYTES;
+  static constexpr int R0 = ((RAW_ALLOC > YB + YB_BYTES ? RAW_ALLOC : YB + YB_BYTES) + 15) & ~15;
+  static constexpr int HX = R0;                                      // IQ FIR history (FE_HALO_IQ)
+  static constexpr int MX = HX + FE_HALO_IQ * 8;
   static constexpr int RST = (MX + MN * 4 + 15) & ~15;               // RDS resampler bank [26][33]
   static constexpr int SG = (RST + FMX_RDS_RS_SUB * (FMX_NPFB + 1) * 4 + 15) & ~15;
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
-  static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256);
+  static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
 };
 
 // 8 outputs j0..j0+7 of a real-tap FIR of runtime length P on a padded LDS
@@ -2710,8 +2717,9 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   using LY = Fe8Layout<M, TPP>;
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
-  float2 *yb = reinterpret_cast<float2 *>(smem);
+  float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
   float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
+  float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
   float *mx = reinterpret_cast<float *>(smem + LY::MX);
   float(*rst)[FMX_NPFB + 1] = reinterpret_cast<float(*)[FMX_NPFB + 1]>(smem + LY::RST);
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
@@ -2748,12 +2756,11 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   const float dc_c = -dc_a1;
 
   // ---- zeroed images, carried state ----
-  for (int h = tid; h < LY::XN; h += 256) xin[h] = make_float2(0.0f, 0.0f);
   for (int h = tid; h < LY::MN; h += 256) mx[h] = 0.0f;
   __syncthreads();
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
     const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
-    xin[fe8_i(h)] = make_float2(v.x, v.y);
+    hx[h] = make_float2(v.x, v.y);
   }
   if (tid == 0) {
     sh->carry_i = a.dc_v[2 * c];
@@ -2789,45 +2796,55 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     }
   }
   int e_pos = 0;
-  u32x4 pf[LY::NPF];
-  auto prefetch = [&](int n0p) {
-    const uint8_t *base = a.iq + (size_t)c * a.iq_stride + 2L * n0p * M - LY::HB;
+  // u8 IQ chunks arrive by LDS-DMA (16 B per lane, 1-KiB pieces, wave w
+  // moving pieces w, w+4, ...): the chunk [n0p*M - L, (n0p + FE8_T)*M) lands
+  // in raw while the previous chunk's pilot FIR and RDS resampler run.
+  // Bytes before the row (the first chunk's halo) read 0 (out of range) and
+  // are replaced by the carried decimator history.
+  const __amdgpu_buffer_rsrc_t riq = make_rsrc(a.iq + (size_t)c * a.iq_stride, (uint32_t)(2L * n * M));
+  auto dma_chunk = [&](int n0p) __attribute__((always_inline)) {
+    uint32_t off = (uint32_t)(2 * n0p * M - LY::HB + 1024 * wave) + 16u * (uint32_t)lane;
 #pragma unroll
-    for (int j = 0; j < LY::NPF; ++j) {
-      const int off = 16 * (tid + 256 * j);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (off < LY::HB + 2 * FE8_T * M && (n0p > 0 || off >= LY::HB))
-        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off));
-      pf[j] = v;
+    for (int j = 0; j < (LY::NPC + 3) / 4; ++j) {
+      const int pc = wave + 4 * j;
+      if (pc < LY::NPC)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, 0);
+      off += 4096u;
+      asm volatile("" : "+v"(off));
     }
   };
-  prefetch(0);
-  __syncthreads();
+  dma_chunk(0);
 
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
     FE_STAMP(7)
     // ================= decimator =================
-#pragma unroll
-    for (int j = 0; j < LY::NPF; ++j) {
-      const int off = 16 * (tid + 256 * j);
-      if (off < LY::HB + 2 * FE8_T * M && (n0 > 0 || off >= LY::HB)) *reinterpret_cast<u32x4 *>(raw + off) = pf[j];
-      if (want_sig && off >= LY::HB && off < LY::HB + 2 * FE8_T * M) {
-        sig.word(pf[j].x);
-        sig.word(pf[j].y);
-        sig.word(pf[j].z);
-        sig.word(pf[j].w);
-      }
-    }
-    if (n0 == 0) // halo: a zero lead sample, then the carried L-1 samples (full history)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads(); // this chunk's DMA has landed (every wave)
+    if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (full history)
       for (int h = tid; h < L; h += 256) {
         const int hh = h - 1;
         uint16_t v = 0;
         if (hh >= 0) v = (uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8);
         reinterpret_cast<uint16_t *>(raw)[h] = v;
       }
-    if (n0 + FE8_T < n) prefetch(n0 + FE8_T);
-    __syncthreads();
+      __syncthreads();
+    }
+    if (want_sig) {
+#pragma unroll
+      for (int j = 0; j < LY::NPF; ++j) {
+        const int off = 16 * (tid + 256 * j);
+        if (off >= LY::HB && off < LY::HB + 2 * FE8_T * M) {
+          const u32x4 w = *reinterpret_cast<const u32x4 *>(raw + off);
+          sig.word(w.x);
+          sig.word(w.y);
+          sig.word(w.z);
+          sig.word(w.w);
+        }
+      }
+    }
+    float2 xv[8]; // decimator outputs of this thread
     {
       // thread window: samples s = 0 .. 8G-1 from raw sample 8*M*tid; output
       // r uses s in [r*M + 1, r*M + L] with tap L + r*M - s
@@ -2888,19 +2905,20 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         const float yr = acc[r].x * D->dec_scale;
         const float yi = acc[r].y * D->dec_scale;
         if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
-        xin[fe8_i(FE_HALO_IQ + j0 + r)] = make_float2(yr, yi);
+        xv[r] = make_float2(yr, yi);
       }
       if (myclip) atomicAdd(&sh->clip, myclip);
     }
-    __syncthreads(); // raw aliases yb
+    __syncthreads(); // raw is dead: xin / yb alias it from here on
     FE_STAMP(0)
+    // IQ FIR history and the zero slack past the chunk (read with zero taps)
+    if (tid < FE_HALO_IQ) xin[fe8_i(tid)] = hx[tid];
+    if (tid < 16) xin[fe8_i(FE_HALO_IQ + FE8_T + tid)] = make_float2(0.0f, 0.0f);
     // ================= DC blockers: affine scan, 8 per thread =================
     {
-      float2 xv[8];
       float A = 1.0f, BI = 0.0f, BQ = 0.0f;
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        xv[r] = xin[fe8_i(FE_HALO_IQ + j0 + r)];
         BI = xv[r].x + dc_c * BI;
         BQ = xv[r].y + dc_c * BQ;
         A = dc_c * A;
@@ -2992,8 +3010,10 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         sh->fd_re = yb[FE8_T].x;
         sh->fd_im = yb[FE8_T].y;
       }
+      if (tid < FE_HALO_IQ) hx[tid] = xin[fe8_i(tid + FE8_T)]; // IQ FIR history for the next chunk
     }
-    __syncthreads();
+    __syncthreads(); // xin / yb are dead: the next chunk may land in raw
+    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T);
     FE_STAMP(3)
     // RDS schedule entries of this chunk, fetched before the pilot FIR
     FmxSched en[8];
@@ -3051,11 +3071,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     FE_STAMP(5)
     // ================= carry halos to the next chunk =================
     {
-      float2 cx = make_float2(0.0f, 0.0f);
-      if (tid < FE_HALO_IQ) cx = xin[fe8_i(tid + FE8_T)];
       const float cm0 = mx[fe8_i(tid + FE8_T)], cm1 = mx[fe8_i(tid + 256 + FE8_T)];
       __syncthreads();
-      if (tid < FE_HALO_IQ) xin[fe8_i(tid)] = cx;
       mx[fe8_i(tid)] = cm0;
       mx[fe8_i(tid + 256)] = cm1;
       __syncthreads();
@@ -3079,7 +3096,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     if (tid == 0) a.dec_valid[c] = L - 1;
   }
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
-    const float2 v = xin[fe8_i(h)];
+    const float2 v = hx[h];
     a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{v.x, v.y};
   }
   if (tid == 0) {
@@ -3111,7 +3128,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 }
 
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
-  static_assert(Fe8Layout<M, TPP>::BYTES <= 80 * 1024, "k_fe8 must fit two workgroups per CU");
+  static_assert(Fe8Layout<M, TPP>::BYTES <= 60 * 1024, "k_fe8: two workgroups per CU plus a serial-kernel workgroup");
   const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
   static bool configured = false;
   if (!configured) {
