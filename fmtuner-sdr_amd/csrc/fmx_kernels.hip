@@ -41,7 +41,7 @@ namespace fmx {
 #define AU_HALO 120
 #define AU_RHALO 32
 #define AU_MAXOUT 256
-#define PLL_T 8
+#define PLL_T 4
 
 static constexpr float kPiF = 3.14159265358979323846f;
 
