@@ -40,9 +40,9 @@ struct TimingSet {
   std::vector<int> hcount;
   // device copies, double-buffered by step parity: step k+1 uploads while
   // the consumers of step k may still run on another stream
-  FmxSched *d_sched[2] = {nullptr, nullptr};
-  int *d_count[2] = {nullptr, nullptr};
-  int *d_group[2] = {nullptr, nullptr};
+  FmxSched *d_sched[FMX_NBUF] = {};
+  int *d_count[FMX_NBUF] = {};
+  int *d_group[FMX_NBUF] = {};
   int stride = 0, cap_groups = 0;
   int cur = 0; // buffer holding the latest upload
 };
@@ -59,10 +59,9 @@ struct Handle {
   // one lane per channel, a few SIMDs) and step k-1's audio still run; the
   // audio of step k overlaps the PLL of step k+1 (raw L/R double-buffered).
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
-  hipEvent_t evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr}, evC[2] = {nullptr, nullptr},
-             evD[2] = {nullptr, nullptr};
+  hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
   hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr;
-  bool evB_set[2] = {false, false}, evC_set[2] = {false, false}, evD_set[2] = {false, false};
+  bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -91,9 +90,9 @@ struct Handle {
   int *reset_mask = nullptr;
   std::vector<int> hmask;
   // intermediates (double-buffered by step parity)
-  float *mpx[2] = {nullptr, nullptr}, *pilot[2] = {nullptr, nullptr}, *rds_in[2] = {nullptr, nullptr};
-  int *rds_count[2] = {nullptr, nullptr};
-  float *lraw[2] = {nullptr, nullptr}, *rraw[2] = {nullptr, nullptr};
+  float *mpx[FMX_NBUF] = {}, *pilot[FMX_NBUF] = {}, *rds_in[FMX_NBUF] = {};
+  int *rds_count[FMX_NBUF] = {};
+  float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
   uint32_t block_index = 0;
   TimingSet t_af, t_mono, t_rds;
@@ -185,7 +184,7 @@ static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
   t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
   int rc;
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &t.d_group[b], static_cast<size_t>(h->C))) != FMX_OK) return rc;
@@ -246,7 +245,7 @@ static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count)
   const int G = static_cast<int>(t.groups.size());
   if (G > t.cap_groups) {
     HIP_TRY(hipDeviceSynchronize());
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < FMX_NBUF; ++b) {
       for (void *p : {static_cast<void *>(t.d_sched[b]), static_cast<void *>(t.d_count[b])}) {
         h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), p), h->allocs.end());
         HIP_TRY(hipFree(p));
@@ -256,7 +255,7 @@ static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count)
     t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
     t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
     int rc;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < FMX_NBUF; ++b) {
       if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
       if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
     }
@@ -399,7 +398,7 @@ static void destroy(Handle *h) {
   }
   for (auto e : h->pool) hipEventDestroy(e);
   for (void *p : h->allocs) hipFree(p);
-  for (int b = 0; b < 2; ++b)
+  for (int b = 0; b < FMX_NBUF; ++b)
     for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
@@ -490,7 +489,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
       HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
     }
   }
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->evB[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->evC[b], hipEventDisableTiming));
@@ -553,11 +552,11 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->rds, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->reset_mask, C)) != FMX_OK) return rc;
   // intermediates
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->mpx[b], C * B)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->pilot[b], C * B)) != FMX_OK) return rc;
   }
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->lraw[b], C * B)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rraw[b], C * B)) != FMX_OK) return rc;
   }
@@ -565,7 +564,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
   h->rds_stride = (h->t_rds.stride + 63) & ~63; // 256-B rows: k_rds stages 16-B aligned pieces
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
   }
@@ -691,9 +690,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if ((rc = prepare(h)) != FMX_OK) return rc;
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
-  const int buf = static_cast<int>(h->step & 1);
-  // buffers of parity `buf` were last read by step k-2 on sB / sC, and by its
-  // audio on sD in mono mode.  In stereo mode the audio of step k-2 only
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
+  // buffers `buf` (step k mod FMX_NBUF) were last read by step k-FMX_NBUF on
+  // sB / sC, and by its audio on sD in mono mode.  In stereo mode the audio of step k-2 only
   // reads raw L/R, but waiting for it anyway throttles the frontend: measured,
   // letting the frontends run ahead starves the PLL / audio chain (2.25 vs
   // 1.61 ms per step, tools/gpu_timeline.sh)
@@ -701,9 +700,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if (h->evC_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf], 0));
   if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
   if (o->d_mpx) { // a caller-owned MPX buffer is read by step k-1's stereo/RDS/audio kernels
-    if (h->evB_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf ^ 1], 0));
-    if (h->evC_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf ^ 1], 0));
-    if (h->evD_set[buf ^ 1]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf ^ 1], 0));
+    if (h->evB_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
+    if (h->evC_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
+    if (h->evD_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
   }
   if (rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
@@ -756,7 +755,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   // ---- stereo PLL (sB), audio (sD) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   if (stereo) {
-    // raw L/R of parity buf were last read by step k-2's audio
+    // raw L/R `buf` were last read by step k-FMX_NBUF's audio
     if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[buf], 0));
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;
@@ -823,7 +822,7 @@ static int stage_begin(Handle *h, int n) {
 }
 // later pipelined work on sB / sC / sD must see the stage's results
 static int stage_end(Handle *h) {
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
@@ -991,7 +990,7 @@ static int demod_common(Handle *h, int mode, const void *d_in, size_t in_stride,
   int rc;
   if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   float *mpx = d_mpx ? d_mpx : h->mpx[buf];
   const int ms = d_mpx ? mpx_stride : h->cfg.block;
   {
@@ -1052,7 +1051,7 @@ int fmx_downsample(void *handle, const float *d_mpx, int mpx_stride, int n, floa
   int rc;
   if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   if ((rc = tset_advance(h, h->t_mono, n, buf, nullptr)) != FMX_OK) return rc;
   AudioArgs a = audio_args(h, n, 2, &h->t_mono);
   a.in_l = d_mpx;
@@ -1077,7 +1076,7 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
   int rc;
   if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   {
     FeArgs a = fe_args(h, n, FE_IN_MPX, buf);
     a.in_f = d_mpx;
@@ -1124,7 +1123,7 @@ int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_s
   std::vector<ResampTiming> saved = h->t_af.groups;
   std::vector<int> saved_map = h->t_af.chan_group;
   int mx = 0;
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   if ((rc = tset_advance(h, h->t_af, n, buf, &mx)) != FMX_OK) return rc;
   if (mx > cap) {
     h->t_af.groups = saved;
@@ -1159,7 +1158,7 @@ int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_gro
     if (d_group_count) HIP_TRY(hipMemsetAsync(d_group_count, 0, sizeof(int) * h->C, h->sA));
     return FMX_OK;
   }
-  const int buf = static_cast<int>(h->step & 1);
+  const int buf = static_cast<int>(h->step % FMX_NBUF);
   if ((rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   {
     FeArgs a = fe_args(h, n, FE_IN_MPX, buf);

@@ -160,7 +160,9 @@ struct ResetArgs {
   float *lr_hist, *af_win, *af_iir, *mono_win, *mono_iir;
   float *rds_hist;
 };
-#define FMX_ST_BUFS 3 // rotating stereo-history buffers (frontend k+1 overlaps stereo k)
+#define FMX_NBUF 3                // per-step intermediates (MPX, pilot, RDS-rate, raw L/R): front end k
+                                  // runs while stereo/RDS/audio of steps k-1, k-2 drain
+#define FMX_ST_BUFS (FMX_NBUF + 1) // rotating stereo-history buffers
 enum ResetParts {
   RS_DECIM = 1,    // ComplexDecimator::reset
   RS_DEMOD = 2,    // FMDemod::reset (DC, IQ FIR, discriminator, mono chain)
