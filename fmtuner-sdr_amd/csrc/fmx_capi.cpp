@@ -62,6 +62,7 @@ struct Handle {
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
   hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr;
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
+  int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -453,6 +454,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     h->skip_pll = v.find("pll") != std::string::npos;
     h->skip_audio = v.find("audio") != std::string::npos;
   }
+  // k_pll / k_rds waves run at raised issue priority beside the front end's
+  // (measured 1.39 -> 1.375 ms/step); FMX_SERIAL_PRIO=0 turns it off
+  h->serial_prio = 1;
+  if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] == '0') h->serial_prio = 0;
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
   } else {
@@ -648,6 +653,7 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lr_stride = h->cfg.block;
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
+  a.prio = h->serial_prio;
   return a;
 }
 
@@ -662,6 +668,7 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
+  a.prio = h->serial_prio;
   return a;
 }
 

@@ -93,6 +93,7 @@ struct PllArgs {
   FmxStereoState *st;
   int *stereo_out, *pilot_tenths_out;
   unsigned long long *dbg; // [10] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
+  int prio;                // raise the waves' issue priority (s_setprio)
 };
 
 struct AudioArgs {
@@ -132,6 +133,7 @@ struct RdsArgs {
   int *group_count;
   uint32_t block_index;
   unsigned long long *dbg; // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
+  int prio;                // raise the waves' issue priority (s_setprio)
 };
 
 // launchers (fmx_kernels.hip); stream is a hipStream_t
