@@ -360,9 +360,22 @@ struct SigAcc {
     hard += (lo <= 1u || hi >= 254u) ? 1u : 0u;
     nearc += (lo <= 8u || hi >= 247u) ? 1u : 0u;
   }
-  __device__ __forceinline__ void word(uint32_t w) {  // bytes I0 Q0 I1 Q1
-    sample(w & 255u, (w >> 8) & 255u);
-    sample((w >> 16) & 255u, w >> 24);
+  __device__ __forceinline__ void flags(uint32_t i, uint32_t q) {
+    const uint32_t lo = min(i, q), hi = max(i, q);
+    hard += (lo <= 1u || hi >= 254u) ? 1u : 0u;
+    nearc += (lo <= 8u || hi >= 247u) ? 1u : 0u;
+  }
+  // bytes I0 Q0 I1 Q1: the four sums by byte dot products; the clip counters
+  // only when some byte is <= 8 or >= 247 (fmx_word_near_clip)
+  __device__ __forceinline__ void word(uint32_t w) {
+    sI = __builtin_amdgcn_udot4(w, 0x00010001u, sI, false);
+    sQ = __builtin_amdgcn_udot4(w, 0x01000100u, sQ, false);
+    sII = __builtin_amdgcn_udot4(w & 0x00FF00FFu, w, sII, false);
+    sQQ = __builtin_amdgcn_udot4(w & 0xFF00FF00u, w, sQQ, false);
+    if (fmx_word_near_clip(w)) {
+      flags(w & 255u, (w >> 8) & 255u);
+      flags((w >> 16) & 255u, w >> 24);
+    }
   }
 };
 
@@ -963,6 +976,11 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 #define PLL_CH 64
 #define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
 #define PLL_WAVES 5
+// Waves w and w + 4 of a workgroup share a SIMD (measured,
+// tools/ubench/hwid.hip).  The PLL chain (W0, wave 0) shares with another
+// latency-bound serial wave, never with the throughput-bound W2 waves.
+#define PLL_W1 4
+#define PLL_W3 1
 struct PllShared {
   float inp[3][PLL_CH][PLL_TS];            // pilot tiles (k+1 loading, k in W0, k-1 in W1)
   float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k loading, k-1 in W1)
@@ -1117,7 +1135,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     sh->s2_flags[tid] = f;
     sh->s2_gate[tid] = g;
   }
-  if (wave == 4) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
+  if (wave == PLL_W3) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
   __syncthreads();
 
   const int c = c0 + lane;
@@ -1225,7 +1243,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     a.st[c] = s;
     if (a.stereo_out) a.stereo_out[c] = s.detected;
     if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
-  } else if (wave == 1) {
+  } else if (wave == PLL_W1) {
     // ---------------- W1: envelopes, pilot I/Q, frequency, cos 2phi ----------------
     float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q, freq = s0.pll_freq;
     const float pmin = D->pll_min, pmax = D->pll_max;
@@ -1295,7 +1313,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     fin[4][lane] = freq;
     PLL_SYNC()
     PLL_STAMP_OUT()
-  } else if (wave == 4) {
+  } else if (wave == PLL_W3) {
     // ---------------- W3: blend recursion + outputs; loader ----------------
     float blend = s0.blend;
     const int mode = sh->s2_flags[lane] >> 8;
@@ -1407,7 +1425,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 #undef W3_STAMP
   } else {
     // ---------------- W2a/W2b: time-parallel work ----------------
-    const int t2 = tid - 128;  // 0..127
+    const int t2 = tid - 128;  // 0..127 (waves 2, 3)
     const float nominal = D->nominal;
     const float fsf = (float)D->fs;
     for (int k = 0; k < NT + 3; ++k) {

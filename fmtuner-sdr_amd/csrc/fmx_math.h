@@ -14,6 +14,8 @@
 #ifndef FMX_MATH_H
 #define FMX_MATH_H
 
+#include <stdint.h>
+
 #ifdef __HIPCC__
 #define FMX_HD __host__ __device__ __forceinline__
 #else
@@ -47,6 +49,16 @@ FMX_HD void fmx_sincos(float x, float *s, float *c) {
   const float c0 = swap ? sr : cr;
   *s = (qi & 2) ? -s0 : s0;
   *c = ((qi + 1) & 2) ? -c0 : c0;
+}
+
+// RF-level clip pre-test on one 4-byte word of u8 I/Q (signal_level.cpp:
+// computeSignalLevel counts samples with a component <= 8 or >= 247): nonzero
+// iff some byte b has (b + 9) mod 256 < 18, i.e. b <= 8 or b >= 247.  Bytewise
+// add without inter-byte carries, then the classic "some byte < n" test.
+// Exact over all 2^32 words (tests/cpp/swar_test.c checks it exhaustively).
+FMX_HD uint32_t fmx_word_near_clip(uint32_t w) {
+  const uint32_t t = ((w & 0x7F7F7F7Fu) + 0x09090909u) ^ (w & 0x80808080u);
+  return (t - 0x12121212u) & ~t & 0x80808080u;
 }
 
 #endif

@@ -19,3 +19,12 @@ def test_sincos_within_one_ulp(tmp_path):
     r = json.loads(out)
     assert r["max_ulp"] < 1.0, r
     assert r["max_abs"] < 1.2e-7, r
+
+
+def test_near_clip_word_test_exhaustive(tmp_path):
+    """fmx_word_near_clip over all 2^32 words (OpenMP, ~5 s on 8 cores)."""
+    exe = str(tmp_path / "swar_test")
+    subprocess.run(["g++", "-O2", "-fopenmp", "-std=c++17", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "swar_test.cpp")], check=True, timeout=120)
+    r = json.loads(subprocess.run([exe], check=True, capture_output=True, text=True, timeout=300).stdout)
+    assert r == {"false_negatives": 0, "false_positives": 0}
