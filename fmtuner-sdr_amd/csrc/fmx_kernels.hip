@@ -1150,8 +1150,10 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     float vcoQ, vcoI;
     fmx_sincos(d_nco_phase(theta), &vcoQ, &vcoI);
     for (int k = 0; k < NT + 3; ++k) {
-      if (k < NT) {
-        const int cnt = min(PLL_T, n - k * PLL_T);
+      // full tiles run without per-sample guards: the guards would sink the
+      // tile's LDS read into every sample (an LDS round trip on the chain)
+      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full_c)::value;
         const int ib = k % 3, ob = k & 1;
         float pv[PLL_T];
 #pragma unroll
@@ -1162,7 +1164,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
         float ph[PLL_T], sq[PLL_T], cq[PLL_T];
 #pragma unroll
         for (int t = 0; t < PLL_T; ++t) {
-          if (t < cnt) {
+          if (FULL || t < cnt) {
             const float err = pv[t] * vcoQ;
             dtheta += d_nco_constrain(err * alpha);
             theta += d_nco_constrain(err * beta);
@@ -1187,6 +1189,11 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
           *reinterpret_cast<float4 *>(&sh->s0[ob][2][lane][4 * q]) =
               make_float4(cq[4 * q], cq[4 * q + 1], cq[4 * q + 2], cq[4 * q + 3]);
         }
+      };
+      if (k < NT) {
+        const int cnt = min(PLL_T, n - k * PLL_T);
+        if (cnt == PLL_T) tile(std::true_type{}, cnt);
+        else tile(std::false_type{}, cnt);
       }
       PLL_SYNC()
     }
@@ -1252,8 +1259,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     fmx_sincos(phaseNow, &vcoQ, &vcoI);
     for (int k = 0; k < NT + 3; ++k) {
       const int kt = k - 1;
-      if (kt >= 0 && kt < NT) {
-        const int cnt = min(PLL_T, n - kt * PLL_T);
+      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full_c)::value;
         const int ib = kt % 3, sb = kt & 1;
         float pv[PLL_T], mv[PLL_T], ph[PLL_T], sq[PLL_T], cq[PLL_T];
 #pragma unroll
@@ -1272,7 +1279,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
         float o_pbm[PLL_T], o_mm[PLL_T], o_mag2[PLL_T], o_fr[PLL_T], o_c2[PLL_T];
 #pragma unroll
         for (int t = 0; t < PLL_T; ++t) {
-          if (t < cnt) {
+          if (FULL || t < cnt) {
             const float pilot = pv[t];
             pbm = (pbm * kS) + (fabsf(pilot) * kI);
             mm = (mm * kS) + (fabsf(mv[t]) * kI);
@@ -1303,6 +1310,11 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
           *reinterpret_cast<float4 *>(&sh->s1[sb][F_FREQ][lane][t]) = make_float4(o_fr[t], o_fr[t + 1], o_fr[t + 2], o_fr[t + 3]);
           *reinterpret_cast<float4 *>(&sh->s1[sb][F_COS2][lane][t]) = make_float4(o_c2[t], o_c2[t + 1], o_c2[t + 2], o_c2[t + 3]);
         }
+      };
+      if (kt >= 0 && kt < NT) {
+        const int cnt = min(PLL_T, n - kt * PLL_T);
+        if (cnt == PLL_T) tile(std::true_type{}, cnt);
+        else tile(std::false_type{}, cnt);
       }
       PLL_SYNC()
     }
@@ -1365,8 +1377,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       if (k < NT) std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
       W3_STAMP(1)
       const int kt = k - 3;
-      if (kt >= 0 && kt < NT) {
-        const int cnt = min(PLL_T, n - kt * PLL_T);
+      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full_c)::value;
         const int sb = kt & 1;
         float ov[2][PLL_T];
 #pragma unroll
@@ -1380,7 +1392,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int t = 4 * q + u;
-            if (t < cnt) {
+            if (FULL || t < cnt) {
               const float tgt = tga[u];
               const float ba = (tgt > blend) ? attack : release;
               blend += (tgt - blend) * ba;
@@ -1410,6 +1422,11 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
             }
           }
         }
+      };
+      if (kt >= 0 && kt < NT) {
+        const int cnt = min(PLL_T, n - kt * PLL_T);
+        if (cnt == PLL_T) tile(std::true_type{}, cnt);
+        else tile(std::false_type{}, cnt);
       }
       PLL_SYNC()
     }
