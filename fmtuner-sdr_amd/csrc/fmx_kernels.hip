@@ -975,14 +975,17 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
  * in the reference's order; only WHERE it runs moved. */
 #define PLL_CH 64
 #define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
-#define PLL_WAVES 5
+#define PLL_WAVES 6
 // Waves w and w + 4 of a workgroup share a SIMD (measured,
-// tools/ubench/hwid.hip).  The PLL chain (W0, wave 0) shares with another
-// latency-bound serial wave, never with the throughput-bound W2 waves.
-#define PLL_W1 4
-#define PLL_W3 1
+// tools/ubench/hwid.hip), and a SIMD retires about one wave64 VALU
+// instruction per 4 cycles whichever wave issues it: the PLL chain (W0,
+// wave 0) is alone on its SIMD (wave 4 only takes part in the barriers); W1
+// and W3 share one.
+#define PLL_W1 1
+#define PLL_IDLE 4
+#define PLL_W3 5
 struct PllShared {
-  float inp[3][PLL_CH][PLL_TS];            // pilot tiles (k+1 loading, k in W0, k-1 in W1)
+  float inp[4][PLL_CH][PLL_TS];            // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-1 in W1
   float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k loading, k-1 in W1)
   float s0[2][3][PLL_CH][PLL_TS];          // W0 -> W1: phase after the step, its sine and cosine
   float s1[2][5][PLL_CH][PLL_TS];          // W1 -> W2: PBM, MM, MAG2, FREQ, COS2
@@ -1135,7 +1138,10 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     sh->s2_flags[tid] = f;
     sh->s2_gate[tid] = g;
   }
-  if (wave == PLL_W3) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
+  if (wave == PLL_W3) {
+    pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
+    if (n > PLL_T) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[1], c0, PLL_T, min(PLL_T, n - PLL_T), lane);
+  }
   __syncthreads();
 
   const int c = c0 + lane;
@@ -1149,16 +1155,26 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     const float alpha = D->pll_alpha, beta = D->pll_beta;
     float vcoQ, vcoI;
     fmx_sincos(d_nco_phase(theta), &vcoQ, &vcoI);
+    // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
+    // iteration k), so its LDS latency overlaps the chain of the current tile
+    float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
+#pragma unroll
+    for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = *reinterpret_cast<const float4 *>(&sh->inp[0][lane][4 * q]);
     for (int k = 0; k < NT + 3; ++k) {
+      if (k + 1 < NT) {
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q)
+          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) & 3][lane][4 * q]);
+      }
       // full tiles run without per-sample guards: the guards would sink the
       // tile's LDS read into every sample (an LDS round trip on the chain)
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int ib = k % 3, ob = k & 1;
+        const int ob = k & 1;
         float pv[PLL_T];
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[ib][lane][4 * q]);
+          const float4 x = pcur[q];
           pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
         }
         float ph[PLL_T], sq[PLL_T], cq[PLL_T];
@@ -1170,8 +1186,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
             theta += d_nco_constrain(err * beta);
             theta += dtheta;
             const float phaseNext = d_nco_phase(theta);
+            const int qn = fmx_nco_quadrant(theta); // off the phase's dependency chain
             float sN, cN;
-            fmx_sincos(phaseNext, &sN, &cN); // both polynomials are needed for the quadrant anyway
+            fmx_sincos_q(phaseNext, (float)qn, qn, &sN, &cN); // both polynomials are needed for the quadrant anyway
             vcoQ = sN;
             ph[t] = phaseNext;
             sq[t] = sN;
@@ -1195,6 +1212,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
         if (cnt == PLL_T) tile(std::true_type{}, cnt);
         else tile(std::false_type{}, cnt);
       }
+#pragma unroll
+      for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = pnxt[q];
       PLL_SYNC()
     }
     PLL_SYNC() // W1 / W3 block-end values in sh->fin
@@ -1261,7 +1280,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       const int kt = k - 1;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int ib = kt % 3, sb = kt & 1;
+        const int ib = kt & 3, sb = kt & 1;
         float pv[PLL_T], mv[PLL_T], ph[PLL_T], sq[PLL_T], cq[PLL_T];
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q) {
@@ -1331,8 +1350,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     const int mode = sh->s2_flags[lane] >> 8;
     const float attack = D->blend_attack[mode], release = D->blend_release[mode];
     // loads staged in registers one iteration ahead, across the barrier:
-    // iteration k stores pilot tile k+1, mpx tile k and delay tile k-1 (for
-    // W0, W1 and W2 at iteration k+1), then issues pilot k+2, mpx k+1, delay k
+    // iteration k stores pilot tile k+2 (W0 reads it ahead at k+1), mpx tile
+    // k and delay tile k-1 (W1 and W2 at iteration k+1), then issues pilot
+    // k+3, mpx k+1, delay k
     PllStage stp, stm;
     PllDlyStage std_;
 #ifdef FMX_STAMPS
@@ -1359,12 +1379,12 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // waitcnt pass, merging states at the loop header, drains the staged
     // tile loads (vmcnt(0)) at their first use inside the loop
     __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
-    if (full(1)) stp.issue(rp, a.pilot_stride, PLL_T, lane);
+    if (full(2)) stp.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
     if (full(0)) stm.issue(rm, a.mpx_stride, 0, lane);
     for (int k = 0; k < NT + 3; ++k) {
-      if (k + 1 < NT) {
-        if (full(k + 1)) stp.store(sh->inp[(k + 1) % 3], lane);
-        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[(k + 1) % 3], c0, (k + 1) * PLL_T, tcnt(k + 1), lane);
+      if (k + 2 < NT) {
+        if (full(k + 2)) stp.store(sh->inp[(k + 2) & 3], lane);
+        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[(k + 2) & 3], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
       }
       if (k < NT) {
         if (full(k)) stm.store(sh->inm[k & 1], lane);
@@ -1372,7 +1392,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       }
       if (k - 1 >= 0 && k - 1 < NT) std_.store(sh->dly[(k - 1) & 1], lane);
       W3_STAMP(0)
-      if (full(k + 2)) stp.issue(rp, a.pilot_stride, (k + 2) * PLL_T, lane);
+      if (full(k + 3)) stp.issue(rp, a.pilot_stride, (k + 3) * PLL_T, lane);
       if (full(k + 1)) stm.issue(rm, a.mpx_stride, (k + 1) * PLL_T, lane);
       if (k < NT) std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
       W3_STAMP(1)
@@ -1435,11 +1455,15 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     PLL_STAMP_OUT()
 #ifdef FMX_STAMPS
     if (a.dbg && lane == 0) {
-      atomicAdd(a.dbg + 10, w3acc[0]);
-      atomicAdd(a.dbg + 11, w3acc[1]);
+      atomicAdd(a.dbg + 12, w3acc[0]);
+      atomicAdd(a.dbg + 13, w3acc[1]);
     }
 #endif
 #undef W3_STAMP
+  } else if (wave == PLL_IDLE) {
+    for (int k = 0; k < NT + 3; ++k) PLL_SYNC()
+    PLL_SYNC()
+    PLL_STAMP_OUT()
   } else {
     // ---------------- W2a/W2b: time-parallel work ----------------
     const int t2 = tid - 128;  // 0..127 (waves 2, 3)

@@ -23,8 +23,9 @@
 #define FMX_HD inline
 #endif
 
-FMX_HD void fmx_sincos(float x, float *s, float *c) {
-  const float q = rintf(x * 0.636619772367581343f);
+// sin and cos of x given its quadrant count qi (x ~ qi pi/2, |x - qi pi/2|
+// <= pi/4 + a few ulp); q = (float)qi.
+FMX_HD void fmx_sincos_q(float x, float q, int qi, float *s, float *c) {
   // r = x - q pi/2 as rh + rl (pi/2 in three parts)
   const float r1 = fmaf(-q, 1.57079637050628662109375f, x);
   const float rh = fmaf(-q, -4.3711388286737929e-08f, r1);
@@ -43,13 +44,24 @@ FMX_HD void fmx_sincos(float x, float *s, float *c) {
   const float w = 1.0f - hz;
   const float tail = (1.0f - w) - hz;
   const float cr = w + (fmaf(z * z, pc, tail) - rh * rl);
-  const int qi = (int)q;
   const bool swap = (qi & 1) != 0;
   const float s0 = swap ? cr : sr;
   const float c0 = swap ? sr : cr;
   *s = (qi & 2) ? -s0 : s0;
   *c = ((qi + 1) & 2) ? -c0 : c0;
 }
+
+FMX_HD void fmx_sincos(float x, float *s, float *c) {
+  const float q = rintf(x * 0.636619772367581343f);
+  fmx_sincos_q(x, q, (int)q, s, c);
+}
+
+// Quadrant count of an NCO phase word: round(theta / 2^30) in 0..4, the
+// quadrant of the exact phase 2 pi theta / 2^32.  The float phase the
+// reference computes from theta is within 0.5 ulp of it, so fmx_sincos_q of
+// that phase with this count stays inside the polynomial range; it is known
+// as soon as theta is, off the phase's dependency chain (the k_pll loop).
+FMX_HD int fmx_nco_quadrant(uint32_t theta) { return (int)((theta >> 30) + ((theta >> 29) & 1u)); }
 
 // RF-level clip pre-test on one 4-byte word of u8 I/Q (signal_level.cpp:
 // computeSignalLevel counts samples with a component <= 8 or >= 247): nonzero

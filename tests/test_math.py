@@ -19,6 +19,7 @@ def test_sincos_within_one_ulp(tmp_path):
     r = json.loads(out)
     assert r["max_ulp"] < 1.0, r
     assert r["max_abs"] < 1.2e-7, r
+    assert r["nco_max_ulp"] < 1.0, r  # quadrant count from the NCO word (k_pll)
 
 
 def test_near_clip_word_test_exhaustive(tmp_path):

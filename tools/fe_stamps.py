@@ -45,8 +45,8 @@ for k in range(8):
     print(f"  {RN[k]:10s} {v[8 + k] / tot * 100:6.1f} %  {v[8 + k] / (nwg * nblk):10.0f} ticks/launch-WG")
 nwg = (Cn + 63) // 64
 print("k_pll per wave (lane 0): work / barrier-wait ticks per launch-WG")
-for w, nm in enumerate(["W0 chain", "W3 blend+load", "W2a", "W2b", "W1 env"]):
+for w, nm in enumerate(["W0 chain", "W1 env", "W2a", "W2b", "(idle)", "W3 blend+load"]):
     wk, wt = v[16 + 2 * w], v[17 + 2 * w]
     print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}")
-print(f"  W3 issue part {v[26] / (nwg * nblk):10.0f}")
-print(f"  W3 store part {v[27] / (nwg * nblk):10.0f}")
+print(f"  W3 issue part {v[28] / (nwg * nblk):10.0f}")
+print(f"  W3 store part {v[29] / (nwg * nblk):10.0f}")
