@@ -2723,24 +2723,32 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
 };
 
-// 8 outputs j0..j0+7 of a real-tap FIR of runtime length P on a padded LDS
-// image x (input i at x[fe8_i(i)]); hz = taps with 16 zeros on each side
-// (hz[16 + k] = h[k]).  Per output the FMA chain runs oldest input first, as
-// fir_r3; outputs (2q, 2q+1) share one packed FMA.
+// 8 outputs j0..j0+7 (j0 % 8 == 0) of a real-tap FIR of runtime length P on
+// a padded LDS image x (input i at x[fe8_i(i)]); hz = taps with 16 zeros on
+// each side (hz[16 + k] = h[k]).  Per output the FMA chain runs oldest input
+// first, as fir_r3; outputs (2q, 2q+1) share one packed FMA.  The filter is
+// run as length P8 = P rounded up to 8k + 1 (up to 7 zero taps at the oldest
+// end: the chain starts with +0 products, same sums), so every group of 8
+// inputs is one 9-float row of the image: one address per group, the 8 reads
+// by immediate offsets.
+__device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
 __device__ __forceinline__ void fir8_r(const float *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = f32x2{0.0f, 0.0f};
+  const int P8 = fir8_len(P);
+  const float *xg = x + 9 * ((j0 - (P8 - 1)) >> 3);
 #pragma unroll 2
-  for (int m0 = 0; m0 < P + 7; m0 += 8) {
-    // input j0-(P-1)+m0+u feeds output r with tap (P-1)-m0+r-u = tw[7+r-u]
-    const FMX_CONST float *tw = cptr(hz) + 16 + (P - 1) - m0 - 7;
+  for (int m0 = 0; m0 < P8 + 7; m0 += 8) {
+    // input j0-(P8-1)+m0+u feeds output r with tap (P8-1)-m0+r-u = tw[7+r-u]
+    const FMX_CONST float *tw = cptr(hz) + 16 + (P8 - 1) - m0 - 7;
     float t[16];
 #pragma unroll
     for (int k = 0; k < 15; ++k) t[k] = tw[k];
     t[15] = 0.0f;
+    const float *xr = xg + 9 * (m0 >> 3);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const float v = x[fe8_i(j0 - (P - 1) + m0 + u)];
+      const float v = xr[u];
       const f32x2 vv = {v, v};
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -2752,16 +2760,19 @@ __device__ __forceinline__ void fir8_r(const float *x, int j0, const float *__re
 __device__ __forceinline__ void fir8_c(const float2 *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[8]) {
 #pragma unroll
   for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
+  const int P8 = fir8_len(P);
+  const float2 *xg = x + 9 * ((j0 - (P8 - 1)) >> 3);
 #pragma unroll 2
-  for (int m0 = 0; m0 < P + 7; m0 += 8) {
-    const FMX_CONST float *tw = cptr(hz) + 16 + (P - 1) - m0 - 7;
+  for (int m0 = 0; m0 < P8 + 7; m0 += 8) {
+    const FMX_CONST float *tw = cptr(hz) + 16 + (P8 - 1) - m0 - 7;
     float t[16];
 #pragma unroll
     for (int k = 0; k < 15; ++k) t[k] = tw[k];
     t[15] = 0.0f;
+    const float2 *xr = xg + 9 * (m0 >> 3);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const float2 v = x[fe8_i(j0 - (P - 1) + m0 + u)];
+      const float2 v = xr[u];
       const f32x2 vv = {v.x, v.y};
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
