@@ -2714,10 +2714,18 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int NPC = (HB + 2 * FE8_T * M + 1023) / 1024;     // 1-KiB LDS-DMA pieces per chunk
   static constexpr int RAW_ALLOC = NPC * 1024 > RAW_BYTES ? NPC * 1024 : RAW_BYTES;
   static constexpr int R0 = ((RAW_ALLOC > YB + YB_BYTES ? RAW_ALLOC : YB + YB_BYTES) + 15) & ~15;
+  // unpadded MPX copy for the RDS resampler (32 history + chunk + 32 slack),
+  // at the top of the raw region: the pieces below it are the next chunk's
+  // early DMA (during pilot / RDS), the pieces over it the late DMA
+  static constexpr int U_FLOATS = 32 + FE8_T + 32;
+  static constexpr int UOFF = (R0 - U_FLOATS * 4) & ~15;
+  static constexpr int NPC_EARLY = UOFF / 1024 < NPC ? UOFF / 1024 : NPC;
   static constexpr int HX = R0;                                      // IQ FIR history (FE_HALO_IQ)
   static constexpr int MX = HX + FE_HALO_IQ * 8;
-  static constexpr int RST = (MX + MN * 4 + 15) & ~15;               // RDS resampler bank [26][33]
-  static constexpr int SG = (RST + FMX_RDS_RS_SUB * (FMX_NPFB + 1) * 4 + 15) & ~15;
+  static constexpr int RS_PAIRS = FMX_NPFB + 1;                      // branch pairs (b, b+1), + the boundary pair
+  static constexpr int RS_M = FMX_RDS_RS_SUB + 1;                    // 27 terms (leading / trailing zero)
+  static constexpr int RST = (MX + MN * 4 + 15) & ~15;               // RDS resampler bank [33][27] float2
+  static constexpr int SG = (RST + RS_PAIRS * RS_M * 8 + 15) & ~15;
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
@@ -2793,7 +2801,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
   float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
   float *mx = reinterpret_cast<float *>(smem + LY::MX);
-  float(*rst)[FMX_NPFB + 1] = reinterpret_cast<float(*)[FMX_NPFB + 1]>(smem + LY::RST);
+  f32x2(*rsb)[LY::RS_M] = reinterpret_cast<f32x2(*)[LY::RS_M]>(smem + LY::RST);
+  float *uc = reinterpret_cast<float *>(smem + LY::UOFF); // uc[32 + j]: MPX sample j of the chunk
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -2861,10 +2870,22 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     sched = a.rds_sched + (size_t)g * a.rds_sched_stride;
     sched_n = a.rds_sched_n[g];
     if (tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
-    for (int k = tid; k < FMX_NPFB * FMX_RDS_RS_SUB; k += 256) {
-      const int b = k / FMX_RDS_RS_SUB, nn = k % FMX_RDS_RS_SUB;
-      rst[nn][b] = D->rds_rs_h[k];
-      if (b == 0) rst[nn][FMX_NPFB] = D->rds_rs_h[k]; // column 32 = branch 0 (a boundary pairs 31 with 0)
+    // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
+    // (boundary): branch 31 on the window, branch 0 on the window shifted by
+    // one -- 27 terms, oldest sample first, so every lane runs one chain
+    for (int idx = tid; idx < LY::RS_PAIRS * LY::RS_M; idx += 256) {
+      const int pr = idx / LY::RS_M, m = idx % LY::RS_M;
+      const float *hs = D->rds_rs_h; // [branch][26]
+      float h0, h1;
+      if (pr < FMX_NPFB) {
+        const int b1 = (pr + 1) & (FMX_NPFB - 1);
+        h0 = m < FMX_RDS_RS_SUB ? hs[pr * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
+        h1 = m < FMX_RDS_RS_SUB ? hs[b1 * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
+      } else {
+        h0 = m < FMX_RDS_RS_SUB ? hs[(FMX_NPFB - 1) * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
+        h1 = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
+      }
+      rsb[pr][m] = f32x2{h0, h1};
     }
   }
   int e_pos = 0;
@@ -2874,19 +2895,23 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   // Bytes before the row (the first chunk's halo) read 0 (out of range) and
   // are replaced by the carried decimator history.
   const __amdgpu_buffer_rsrc_t riq = make_rsrc(a.iq + (size_t)c * a.iq_stride, (uint32_t)(2L * n * M));
-  auto dma_chunk = [&](int n0p) __attribute__((always_inline)) {
-    uint32_t off = (uint32_t)(2 * n0p * M - LY::HB + 1024 * wave) + 16u * (uint32_t)lane;
+  auto dma_chunk = [&](int n0p, auto p_lo_c, auto p_hi_c) __attribute__((always_inline)) {
+    constexpr int P_LO = decltype(p_lo_c)::value, P_HI = decltype(p_hi_c)::value;
+    uint32_t off = (uint32_t)(2 * n0p * M - LY::HB + 1024 * (P_LO + wave)) + 16u * (uint32_t)lane;
 #pragma unroll
-    for (int j = 0; j < (LY::NPC + 3) / 4; ++j) {
-      const int pc = wave + 4 * j;
-      if (pc < LY::NPC)
+    for (int j = 0; j < (P_HI - P_LO + 3) / 4; ++j) {
+      const int pc = P_LO + wave + 4 * j;
+      if (pc < P_HI)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, 0);
       off += 4096u;
       asm volatile("" : "+v"(off));
     }
   };
-  dma_chunk(0);
+  using PAll0 = std::integral_constant<int, 0>;
+  using PEarly = std::integral_constant<int, LY::NPC_EARLY>;
+  using PAll = std::integral_constant<int, LY::NPC>;
+  dma_chunk(0, PAll0{}, PAll{});
 
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
@@ -3066,6 +3091,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     }
     FE_STAMP(2)
     // ================= discriminator =================
+    float mv[8];
     {
       const float ref = D->fd_ref;
 #pragma unroll
@@ -3075,6 +3101,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         const float re = p.x * r.x + p.y * r.y;
         const float im = p.x * r.y - p.y * r.x;
         const float m = atan2f(im, re) * ref;
+        mv[k] = m;
         mx[fe8_i(FMX_HIST + j)] = m;
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
@@ -3084,8 +3111,16 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
       if (tid < FE_HALO_IQ) hx[tid] = xin[fe8_i(tid + FE8_T)]; // IQ FIR history for the next chunk
     }
-    __syncthreads(); // xin / yb are dead: the next chunk may land in raw
-    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T);
+    __syncthreads(); // xin / yb are dead: the next chunk may land in raw (below uc)
+    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
+    if (rds) { // unpadded copy for the RDS resampler: its own window history first
+#pragma unroll
+      for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
+      if (tid < 32) {
+        uc[tid] = (n0 == 0) ? rds_keep : mx[fe8_i(FMX_HIST - 32 + tid)];
+        uc[32 + FE8_T + tid] = 0.0f;
+      }
+    }
     FE_STAMP(3)
     // RDS schedule entries of this chunk, fetched before the pilot FIR
     FmxSched en[8];
@@ -3107,11 +3142,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     FE_STAMP(4)
     // ================= RDS resampler 240k -> 171k =================
     if (rds) {
-      if (n0 == 0) { // first chunk: the resampler's own window before this call
-        __syncthreads();
-        if (tid < 32) mx[fe8_i(FMX_HIST - 32 + tid)] = rds_keep;
-        __syncthreads();
-      }
+      __syncthreads(); // uc complete
       int last = -1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -3120,14 +3151,14 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           const int i = (en[k].packed & 0xFFFF) - n0;
           const int b = (en[k].packed >> 16) & 0xFF;
           const bool boundary = (en[k].packed >> 24) & 1;
-          const int bb = boundary ? FMX_NPFB - 1 : b;
-          const int w0 = FMX_HIST + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1);
+          // the window's oldest sample (one earlier at a boundary), as uc index
+          const float *xu = uc + 32 + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1);
+          const f32x2 *hk = rsb[boundary ? FMX_NPFB : b];
           f32x2 y = {0.0f, 0.0f};
 #pragma unroll
-          for (int m = 0; m < FMX_RDS_RS_SUB; ++m) {
-            const float h0 = rst[FMX_RDS_RS_SUB - 1 - m][bb], h1 = rst[FMX_RDS_RS_SUB - 1 - m][bb + 1];
-            const float va = mx[fe8_i(w0 + m)], vb = mx[fe8_i(w0 + m + 1)];
-            const f32x2 p = f32x2{h0, h1} * f32x2{va, boundary ? vb : va};
+          for (int m = 0; m < LY::RS_M; ++m) {
+            const float v = xu[m];
+            const f32x2 p = hk[m] * f32x2{v, v};
             y = y + p;
           }
           const float w0f = (1.0f - en[k].mu) * y.x;
@@ -3138,7 +3169,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
       if (last >= 0) atomicMax(&sh->e_end, last + 1);
     }
-    __syncthreads();
+    __syncthreads(); // uc is dead: the rest of the next chunk may land
+    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
     if (rds) e_pos = sh->e_end;
     FE_STAMP(5)
     // ================= carry halos to the next chunk =================
@@ -3200,7 +3232,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 }
 
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
-  static_assert(Fe8Layout<M, TPP>::BYTES <= 60 * 1024, "k_fe8: two workgroups per CU plus a serial-kernel workgroup");
+  static_assert(Fe8Layout<M, TPP>::BYTES <= 63 * 1024, "k_fe8: two workgroups per CU plus a k_pll workgroup");
+  static_assert(Fe8Layout<M, TPP>::UOFF >= Fe8Layout<M, TPP>::YB, "RDS copy above the IQ image");
   const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
   static bool configured = false;
   if (!configured) {
