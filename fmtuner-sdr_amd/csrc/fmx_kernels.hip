@@ -2700,6 +2700,8 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
 __device__ __forceinline__ int fe8_i(int i) { return i + (i >> 3); }
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
 
 template <int M, int TPP> struct Fe8Layout {
   static constexpr int L = M * TPP;
@@ -3152,8 +3154,13 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           const int b = (en[k].packed >> 16) & 0xFF;
           const bool boundary = (en[k].packed >> 24) & 1;
           // the window's oldest sample (one earlier at a boundary), as uc index
-          const float *xu = uc + 32 + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1);
-          const f32x2 *hk = rsb[boundary ? FMX_NPFB : b];
+          // LDS addresses kept opaque: the reads then use the instruction's
+          // offset field (m) instead of one address add per read pair
+          uint32_t xa = (uint32_t)(uintptr_t)(lds_f32 *)(uc + 32 + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1));
+          uint32_t ha = (uint32_t)(uintptr_t)(lds_f32x2 *)rsb[boundary ? FMX_NPFB : b];
+          asm volatile("" : "+v"(xa), "+v"(ha));
+          const lds_f32 *xu = (const lds_f32 *)(uintptr_t)xa;
+          const lds_f32x2 *hk = (const lds_f32x2 *)(uintptr_t)ha;
           f32x2 y = {0.0f, 0.0f};
 #pragma unroll
           for (int m = 0; m < LY::RS_M; ++m) {
