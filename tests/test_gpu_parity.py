@@ -97,6 +97,28 @@ def test_decimation_factor_4(fmx, oracle, torch_cuda):
         check(g, outs[c], c, nblk, "m4")
 
 
+def test_decimation_factor_2(fmx, oracle, torch_cuda):
+    """M=2 (512 kS/s -> 256 kHz): the k_fe8<2, 12> instantiation."""
+    C, nblk = 2, 12
+    kw = dict(iq_rate=512_000, dsp_rate=256_000)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=512_000, M=2)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "m2")
+
+
+@pytest.mark.parametrize("B", [2048, 8192])
+def test_block_sizes_front_end_chunks(fmx, oracle, torch_cuda, B):
+    """Handle blocks of one and of four 2048-sample front-end chunks (the
+    chunk loop of k_fe8: DMA split, halo and RDS-copy carries)."""
+    C, nblk = 4, 10 if B == 2048 else 6
+    kw = dict(block=B)
+    iq, _ = make_iq(fmx, 2, C, nblk, B=B)
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, f"B{B}")
+
+
 def test_direct_u8_no_decimation(fmx, oracle, torch_cuda):
     """iq_rate == dsp_rate: FMDemod::processSplit on bytes (fm_demod.cpp:219-249)."""
     C, nblk = 2, 10
