@@ -66,13 +66,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FMX_BENCH_BACKEND=gloo: rehearsal of the N-rank flow on fewer GPUs
+    # (ranks share GPUs round-robin, the timing collectives go over gloo)
+    backend = os.environ.get("FMX_BENCH_BACKEND", "nccl")
+    gpu = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
+    cdev = dev if backend == "nccl" else torch.device("cpu")
 
     C = args.channels
     B = args.block
@@ -81,7 +89,7 @@ def main():
     cfg = fmx.make_config(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=B,
                           w0_bandwidth_hz=194_000, bandwidth_hz=0, dsp_agc=0, stereo=1, blend=1,
                           deemphasis=0, rds=1)
-    h = fmx.Handle(cfg, C, device=local if world > 1 else 0)
+    h = fmx.Handle(cfg, C, device=gpu if world > 1 else 0)
     ch0 = rank * C
     # ---- inputs: synthetic stereo + RDS IQ for every step, resident in HBM ----
     n_iq = B * M
@@ -134,7 +142,7 @@ def main():
     ngroups = int(gcnt.sum().item())
     stereo_frac = float(st.float().mean().item())
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     iq_samples = float(world) * C * args.steps * n_iq
