@@ -42,8 +42,8 @@ FP32_PEAK_TFLOPS = 157.3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--channels", type=int, default=4096, help="channels per GPU")
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
