@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfmx.so")
+LIB_PATH = os.environ.get("FMX_LIB") or os.path.join(_HERE, "libfmx.so")  # FMX_LIB: A/B builds (diagnostic)
 
 FMX_OK = 0
 FMX_AGC_OFF, FMX_AGC_FAST, FMX_AGC_SLOW = 0, 1, 2
