@@ -119,6 +119,26 @@ def test_block_sizes_front_end_chunks(fmx, oracle, torch_cuda, B):
         check(g, outs[c], c, nblk, f"B{B}")
 
 
+def test_iq_capture_replay_through_pipeline(fmx, oracle, torch_cuda, tmp_path):
+    """writeIqCapture (main.cpp:742-747) block by block, then the capture
+    replayed (fmx_iq_replay) as the input of the GPU pipeline and the oracle:
+    the replayed bytes equal the captured ones and the outputs match."""
+    C, nblk, B, M = 2, 12, 4096, 10
+    iq, _ = make_iq(fmx, 2, C, nblk)
+    blk = 2 * B * M
+    replayed = np.zeros_like(iq)
+    for c in range(C):
+        path = str(tmp_path / f"ch{c}.iq")
+        for b in range(nblk):
+            fmx.iq_capture(path, iq[c, b * blk:(b + 1) * blk], append=b > 0)
+        for b in range(nblk):
+            replayed[c, b * blk:(b + 1) * blk] = fmx.iq_replay(path, b * B * M, B * M)
+    assert np.array_equal(replayed, iq)
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, replayed, nblk)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "replay")
+
+
 def test_direct_u8_no_decimation(fmx, oracle, torch_cuda):
     """iq_rate == dsp_rate: FMDemod::processSplit on bytes (fm_demod.cpp:219-249)."""
     C, nblk = 2, 10
