@@ -457,7 +457,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   // k_pll / k_rds waves run at raised issue priority beside the front end's
   // (measured 1.39 -> 1.375 ms/step); FMX_SERIAL_PRIO=0 turns it off
   h->serial_prio = 1;
-  if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] == '0') h->serial_prio = 0;
+  if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
   } else {

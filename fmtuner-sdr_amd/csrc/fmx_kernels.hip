@@ -1079,7 +1079,8 @@ struct PllDlyStage {
 };
 
 __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
-  if (a.prio) __builtin_amdgcn_s_setprio(2);
+  if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
+  else if (a.prio) __builtin_amdgcn_s_setprio(2);
   __shared__ PllShared shm;
   PllShared *sh = &shm;
   // Stage barrier: LDS writes complete (lgkmcnt) + s_barrier.  Not
@@ -2112,7 +2113,8 @@ __device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &
  * independently, only their wrapped sum is serial, then 8 sincos and the
  * partial sums with wave-uniform (LDS broadcast) tap rows. */
 __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
-  if (a.prio) __builtin_amdgcn_s_setprio(2);
+  if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
+  else if (a.prio) __builtin_amdgcn_s_setprio(2);
   __shared__ RdsLds L;
 #ifdef FMX_STAMPS
   unsigned long long rs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
