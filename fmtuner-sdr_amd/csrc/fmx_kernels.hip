@@ -1899,6 +1899,9 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 // A wave reading one segment per lane (lane = row) then hits all 64 banks
 // once per 16 lanes (conflict-free ds_read_b128).
 #define RDS_PIECE 260
+#ifndef RDS_U
+#define RDS_U 8 // samples per chunk (divides 24)
+#endif
 #define RDS_SYMQ 24 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
 // Per-lane state lives in LDS (odd dword stride: conflict-free across lanes);
 // only the per-sample quantities (NCO, FIR partial sums, AGC, symsync
@@ -2423,7 +2426,8 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   uint32_t j_first = j_mine;
   for (int d = 32; d >= 1; d >>= 1) j_first = min(j_first, (uint32_t)__shfl_xor((int)j_first, d));
   const bool uniform_j = __ballot(act && j_mine != j_first) == 0;
-  constexpr int U = 8;
+  constexpr int U = RDS_U;
+  constexpr int NSEG = (U + 6) / 4; // 16-B segments covering U samples at any offset
   // one chunk of U samples starting at a period phase of 1, 9 or 17
   auto chunk = [&](int t) __attribute__((always_inline)) {
     need(t, U);
@@ -2450,12 +2454,17 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     }
     float xs[U];
     {
-      // 8 samples from 3 16-B segments, offset o = d & 3 is wave-uniform
+      // U samples from NSEG 16-B segments, offset o = d & 3 is wave-uniform
       const int d = t - tb, g = d >> 2, o = d & 3;
-      const float4 A = *reinterpret_cast<const float4 *>(seg_ptr(cur, g));
-      const float4 B4 = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + 1));
-      const float4 C4 = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + 2));
-      const float v[12] = {A.x, A.y, A.z, A.w, B4.x, B4.y, B4.z, B4.w, C4.x, C4.y, C4.z, C4.w};
+      float v[4 * NSEG];
+#pragma unroll
+      for (int q = 0; q < NSEG; ++q) {
+        const float4 A = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + q));
+        v[4 * q] = A.x;
+        v[4 * q + 1] = A.y;
+        v[4 * q + 2] = A.z;
+        v[4 * q + 3] = A.w;
+      }
       switch (o) {
         case 0:
 #pragma unroll
@@ -2485,7 +2494,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
       acc_add(mx[u], t + u, &L.taps[jp][0]);
     }
     RDS_STAMP(2)
-    if (j0 == 17u) {
+    if (j0 == (uint32_t)(FMX_RDS_DECIM + 1 - U)) { // the chunk ends on the FIR output
       fir_output();
       RDS_STAMP(3)
     }
@@ -2503,7 +2512,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     tend = min(tend, nmax);
     const int cend = min(tend, cmin);
     while (t < tend) {
-      if (uniform_j && t + U <= cend && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) % 8u == 1u) {
+      if (uniform_j && t + U <= cend && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) % (uint32_t)U == 1u) {
         chunk(t);
         t += U;
       } else {
