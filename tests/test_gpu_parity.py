@@ -119,6 +119,16 @@ def test_block_sizes_front_end_chunks(fmx, oracle, torch_cuda, B):
         check(g, outs[c], c, nblk, f"B{B}")
 
 
+def test_partial_lane_groups_65_channels(fmx, oracle, torch_cuda):
+    """65 channels: k_pll / k_rds run one full 64-lane workgroup and one with
+    a single live lane (rows past C read 0 through the buffer range check)."""
+    C, nblk = 65, 6
+    iq, _ = make_iq(fmx, 2, C, nblk)
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk)
+    for c in (0, 1, 31, 63, 64):
+        check(g, outs[c], c, nblk, "c65")
+
+
 def test_iq_capture_replay_through_pipeline(fmx, oracle, torch_cuda, tmp_path):
     """writeIqCapture (main.cpp:742-747) block by block, then the capture
     replayed (fmx_iq_replay) as the input of the GPU pipeline and the oracle:
