@@ -1064,8 +1064,9 @@ struct PllDlyStage {
       for (int j = 0; j < J; ++j) {
         const uint32_t om = (uint32_t)(((j * (64 / PLL_T)) * mstride + (from_m ? d0 : 0)) * 4);
         const uint32_t oh = (uint32_t)(((j * (64 / PLL_T)) * FMX_HIST + FMX_HIST + (from_m ? 0 : d0)) * 4);
-        const float x = from_m ? bload1(rm, vm + om, 0) : bload1(rh, vh + oh, 0);
-        v[j] = colok ? x : 0.0f;
+        // columns past cnt read 0 through their out-of-range offset (no
+        // select here either, nothing waits for these loads before the store)
+        v[j] = from_m ? bload1(rm, vm + om, 0) : bload1(rh, vh + oh, 0);
       }
     }
   }
@@ -1156,6 +1157,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     const float alpha = D->pll_alpha, beta = D->pll_beta;
     float vcoQ, vcoI;
     fmx_sincos(d_nco_phase(theta), &vcoQ, &vcoI);
+    uint32_t vsg = 0; // sign bit of sin(phase) not yet applied to vcoQ
     // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
     // iteration k), so its LDS latency overlaps the chain of the current tile
     float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
@@ -1182,15 +1184,20 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 #pragma unroll
         for (int t = 0; t < PLL_T; ++t) {
           if (FULL || t < cnt) {
-            const float err = pv[t] * vcoQ;
+            const float err = __uint_as_float(__float_as_uint(pv[t]) ^ vsg) * vcoQ; // pv * sin(phase)
             dtheta += d_nco_constrain(err * alpha);
             theta += d_nco_constrain(err * beta);
             theta += dtheta;
             const float phaseNext = d_nco_phase(theta);
             const int qn = fmx_nco_quadrant(theta); // off the phase's dependency chain
-            float sN, cN;
-            fmx_sincos_q(phaseNext, (float)qn, qn, &sN, &cN); // both polynomials are needed for the quadrant anyway
-            vcoQ = sN;
+            // both polynomials are needed for the quadrant anyway; the sine's
+            // sign goes onto the next pilot sample (off the chain)
+            float s0, c0;
+            fmx_sincos_q_abs(phaseNext, (float)qn, qn, &s0, &c0);
+            const float sN = (qn & 2) ? -s0 : s0;
+            const float cN = ((qn + 1) & 2) ? -c0 : c0;
+            vcoQ = s0;
+            vsg = (uint32_t)(qn & 2) << 30;
             ph[t] = phaseNext;
             sq[t] = sN;
             cq[t] = cN;
@@ -1350,12 +1357,15 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     float blend = s0.blend;
     const int mode = sh->s2_flags[lane] >> 8;
     const float attack = D->blend_attack[mode], release = D->blend_release[mode];
-    // loads staged in registers one iteration ahead, across the barrier:
-    // iteration k stores pilot tile k+2 (W0 reads it ahead at k+1), mpx tile
-    // k and delay tile k-1 (W1 and W2 at iteration k+1), then issues pilot
-    // k+3, mpx k+1, delay k
-    PllStage stp, stm;
-    PllDlyStage std_;
+    // loads staged in registers TWO iterations ahead, across the barriers
+    // (one iteration, ~0.8 us, left W3 waiting on HBM latency at the
+    // stores): iteration k stores pilot tile k+2 (W0 reads it ahead at k+1),
+    // mpx tile k and delay tile k-1 (W1 and W2 at iteration k+1), then
+    // issues pilot k+4, mpx k+2, delay k+1 into the registers just stored.
+    // Two register sets by tile parity; the loop is unrolled by two so every
+    // set is static.
+    PllStage stp0, stp1, stm0, stm1;
+    PllDlyStage sd0, sd1;
 #ifdef FMX_STAMPS
     unsigned long long w3acc[2] = {0, 0}, w3last = 0;
 #define W3_STAMP(i)                                              \
@@ -1370,8 +1380,14 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
     auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
     const int rows_valid = min(PLL_CH, a.C - c0);
+    // the staged 16-B tile loads are issued unconditionally (a fixed count
+    // per iteration keeps the waitcnt pass from draining them at the stores);
+    // tiles past the block or an unaligned layout read zeros (empty range)
+    // and are replaced by pll_load_sync at the store
     const __amdgpu_buffer_rsrc_t rp =
-        make_rsrc(a.pilot + (size_t)c0 * a.pilot_stride, (uint32_t)((size_t)rows_valid * a.pilot_stride * 4));
+        make_rsrc(a.pilot + (size_t)c0 * a.pilot_stride, vec ? (uint32_t)((size_t)rows_valid * a.pilot_stride * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t rm4 =
+        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, vec ? (uint32_t)((size_t)rows_valid * a.mpx_stride * 4) : 0u);
     const __amdgpu_buffer_rsrc_t rm =
         make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, (uint32_t)((size_t)rows_valid * a.mpx_stride * 4));
     const __amdgpu_buffer_rsrc_t rh =
@@ -1380,9 +1396,16 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // waitcnt pass, merging states at the loop header, drains the staged
     // tile loads (vmcnt(0)) at their first use inside the loop
     __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
-    if (full(2)) stp.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
-    if (full(0)) stm.issue(rm, a.mpx_stride, 0, lane);
-    for (int k = 0; k < NT + 3; ++k) {
+    stp0.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
+    stp1.issue(rp, a.pilot_stride, 3 * PLL_T, lane);
+    stm0.issue(rm4, a.mpx_stride, 0, lane);
+    stm1.issue(rm4, a.mpx_stride, PLL_T, lane);
+    sd0.issue(rm, a.mpx_stride, rh, 0, tcnt(0), lane, Dly);
+    auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
+      constexpr int P = decltype(par_c)::value; // k & 1
+      PllStage &stp = P ? stp1 : stp0;          // pilot tile k+2, then k+4
+      PllStage &stm = P ? stm1 : stm0;          // mpx tile k, then k+2
+      PllDlyStage &std_ = P ? sd0 : sd1;        // delay tile k-1, then k+1
       if (k + 2 < NT) {
         if (full(k + 2)) stp.store(sh->inp[(k + 2) & 3], lane);
         else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[(k + 2) & 3], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
@@ -1393,9 +1416,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       }
       if (k - 1 >= 0 && k - 1 < NT) std_.store(sh->dly[(k - 1) & 1], lane);
       W3_STAMP(0)
-      if (full(k + 3)) stp.issue(rp, a.pilot_stride, (k + 3) * PLL_T, lane);
-      if (full(k + 1)) stm.issue(rm, a.mpx_stride, (k + 1) * PLL_T, lane);
-      if (k < NT) std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
+      stp.issue(rp, a.pilot_stride, (k + 4) * PLL_T, lane);
+      stm.issue(rm4, a.mpx_stride, (k + 2) * PLL_T, lane);
+      std_.issue(rm, a.mpx_stride, rh, (k + 1) * PLL_T, tcnt(k + 1), lane, Dly);
       W3_STAMP(1)
       const int kt = k - 3;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
@@ -1450,6 +1473,10 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
         else tile(std::false_type{}, cnt);
       }
       PLL_SYNC()
+    };
+    for (int k = 0; k < NT + 3; k += 2) {
+      iter(k, std::integral_constant<int, 0>{});
+      if (k + 1 < NT + 3) iter(k + 1, std::integral_constant<int, 1>{});
     }
     fin[5][lane] = blend;
     PLL_SYNC()
@@ -1898,6 +1925,9 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 // segment s rotated to slot (s + 4q) & 15, pieces RDS_PIECE dwords apart.
 // A wave reading one segment per lane (lane = row) then hits all 64 banks
 // once per 16 lanes (conflict-free ds_read_b128).
+#ifndef FMX_HWSIN_RDS
+#define FMX_HWSIN_RDS 1
+#endif
 #define RDS_PIECE 260
 #ifndef RDS_U
 #define RDS_U 8 // samples per chunk (divides 24)
@@ -2229,7 +2259,16 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   };
   auto mix = [&](float x, float ph) __attribute__((always_inline)) {
     float sn, cs;
+#if FMX_HWSIN_RDS
+    // polar(1, -ph) from v_sin_f32 / v_cos_f32 on ph / 2pi (|err| <= 4e-7):
+    // 3 VALU (two quarter-rate) instead of fmx_sincos's ~28 on this
+    // issue-bound wave; the mix-down feeds only the 2.4 kHz symbol path
+    const float r = ph * 0.15915494309189535f;
+    sn = -__builtin_amdgcn_sinf(r);
+    cs = __builtin_amdgcn_cosf(r);
+#else
     fmx_sincos(-ph, &sn, &cs);
+#endif
     return f32x2{x, x} * f32x2{cs, sn};
   };
   // NCO step + quad-phase wrapper (liquid_wrappers.cpp:271-312)

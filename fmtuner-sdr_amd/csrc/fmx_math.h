@@ -23,9 +23,11 @@
 #define FMX_HD inline
 #endif
 
-// sin and cos of x given its quadrant count qi (x ~ qi pi/2, |x - qi pi/2|
-// <= pi/4 + a few ulp); q = (float)qi.
-FMX_HD void fmx_sincos_q(float x, float q, int qi, float *s, float *c) {
+// The quadrant-swapped polynomials of fmx_sincos_q before their signs:
+// sin x = (qi & 2) ? -*s0 : *s0, cos x = ((qi + 1) & 2) ? -*c0 : *c0.  A
+// recursion that multiplies by sin x can flip its other factor's sign bit
+// off the dependency chain instead (the k_pll feedback loop).
+FMX_HD void fmx_sincos_q_abs(float x, float q, int qi, float *s0, float *c0) {
   // r = x - q pi/2 as rh + rl (pi/2 in three parts)
   const float r1 = fmaf(-q, 1.57079637050628662109375f, x);
   const float rh = fmaf(-q, -4.3711388286737929e-08f, r1);
@@ -45,8 +47,15 @@ FMX_HD void fmx_sincos_q(float x, float q, int qi, float *s, float *c) {
   const float tail = (1.0f - w) - hz;
   const float cr = w + (fmaf(z * z, pc, tail) - rh * rl);
   const bool swap = (qi & 1) != 0;
-  const float s0 = swap ? cr : sr;
-  const float c0 = swap ? sr : cr;
+  *s0 = swap ? cr : sr;
+  *c0 = swap ? sr : cr;
+}
+
+// sin and cos of x given its quadrant count qi (x ~ qi pi/2, |x - qi pi/2|
+// <= pi/4 + a few ulp); q = (float)qi.
+FMX_HD void fmx_sincos_q(float x, float q, int qi, float *s, float *c) {
+  float s0, c0;
+  fmx_sincos_q_abs(x, q, qi, &s0, &c0);
   *s = (qi & 2) ? -s0 : s0;
   *c = ((qi + 1) & 2) ? -c0 : c0;
 }
