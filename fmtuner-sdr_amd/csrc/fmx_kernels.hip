@@ -947,9 +947,14 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
                                               bool fstereo, bool detected, float gate) {
   if (fmono) return 0.0f;
   if (fstereo) return 1.0f;
-  const float ratioQ = d_clamp((ratio - 0.022f) / fmaxf(0.040f - 0.022f, 1e-4f), 0.0f, 1.0f);
-  const float cohQ = d_clamp((coh - 0.11f) / fmaxf(0.18f - 0.11f, 1e-4f), 0.0f, 1.0f);
-  const float pllQ = d_clamp((320.0f - errHz) / fmaxf(320.0f - 180.0f, 1e-3f), 0.0f, 1.0f);
+  // divisions by constants as d_div_const: bit-identical to x / c for every
+  // float 0 < |x| <= 2^60 or x = +0 for these divisors (all 2^32 words
+  // checked on the host; -0 comes out +0, which the clamps, fminf and the
+  // "0 + shaped" below absorb); these numerators are 0 or >= 1e-9 in size
+  constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cP = 320.0f - 180.0f; // > the fmaxf floors
+  const float ratioQ = d_clamp(d_div_const(ratio - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
+  const float cohQ = d_clamp(d_div_const(coh - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
+  const float pllQ = d_clamp(d_div_const(320.0f - errHz, cP, 1.0f / cP), 0.0f, 1.0f);
   const float quality = fminf(ratioQ, fminf(cohQ, pllQ));
   float shaped = quality * quality;
   if (mode == 0) shaped = sqrtf(fmaxf(0.0f, quality));
@@ -962,17 +967,22 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 /* k_pll is a five-wave software pipeline over tiles of PLL_T samples for
  * PLL_CH channels (lane = channel in the serial waves):
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
- *                 pll_step, step, phase, sin(phase)         stereo_decoder.cpp:251-256
+ *                 pll_step, step, sin(phase) straight from the phase word
+ *                 (pll_sin_word); it hands the words on     stereo_decoder.cpp:251-256
+ *   W4            (lane = (channel, t)) the reference's float phase of each
+ *                 word with its sine and cosine (fmx_sincos_q) for the
+ *                 outputs; shares W0's SIMD                 :251-253
+ *   W2a, W2b      (lane = (channel, t)) everything parallel in time: the
+ *                 blend target (sqrt, divisions) and the L-R matrix   :120-166,268-284
  *   W1 (serial)   what consumes the PLL without feeding it back: pilot/MPX
  *                 envelopes, pilot I/Q integrators (cos(phase)), PLL
  *                 frequency, cos(2 phase)                    stereo_decoder.cpp:246-250,257-266,275-279
- *   W2a, W2b      (lane = (channel, t)) everything parallel in time: the
- *                 blend target (sqrt, divisions) and the L-R matrix   :120-166,268-284
  *   W3 (serial)   the blend recursion, the outputs, and the loads of later
  *                 input tiles                               :286-288
- * At iteration k, W0 runs tile k, W1 tile k-1, W2 tile k-2, W3 tile k-3;
- * LDS slots rotate.  Every value is computed with the reference's arithmetic
- * in the reference's order; only WHERE it runs moved. */
+ * At iteration k, W0 runs tile k, W4 the phases of tile k-1, W1 tile k-2,
+ * W2 tile k-3, W3 tile k-4; LDS slots rotate.  Apart from
+ * the chain's sine (below) every value is computed with the reference's
+ * arithmetic in the reference's order; only WHERE it runs moved. */
 #define PLL_CH 64
 #define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
 #define PLL_WAVES 6
@@ -984,10 +994,32 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 #define PLL_W1 1
 #define PLL_IDLE 4
 #define PLL_W3 5
+#define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
+#define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
+
+// sin(2 pi theta / 2^32) for the PLL feedback only: half-turn reduction on
+// the phase word itself, theta = m 2^31 + d (|d| <= 2^30, m's parity in bit
+// 31 of the result *sg), r = d pi / 2^31 (one rounding), and the degree-9
+// minimax sine on [-pi/2, pi/2]; sin = (*sg ? -1 : 1) * the return value.
+// 11 VALU instead of the float phase (f64 multiply) and both quadrant
+// polynomials of fmx_sincos_q.  |err| <= 1.4e-7 against the exact phase
+// (4.4e-7 against sin of the reference's float phase, whose own rounding
+// dominates); the outputs keep fmx_sincos_q of the reference's float phase.
+__device__ __forceinline__ float pll_sin_word(uint32_t theta, uint32_t *sg) {
+  const uint32_t s = (theta + 0x40000000u) & 0x80000000u;
+  const float r = (float)(int32_t)(theta ^ s) * 1.4629180792671596e-09f;
+  const float z = r * r;
+  float u = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
+  u = fmaf(u, z, 0.00833307858556509017944336f);
+  u = fmaf(u, z, -0.166666597127914428710938f);
+  *sg = s;
+  return fmaf(z, u * r, r);
+}
 struct PllShared {
-  float inp[4][PLL_CH][PLL_TS];            // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-1 in W1
-  float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k loading, k-1 in W1)
-  float s0[2][3][PLL_CH][PLL_TS];          // W0 -> W1: phase after the step, its sine and cosine
+  float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-2 in W1
+  float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k-1 loading, k-2 in W1)
+  uint32_t s0t[2][PLL_CH][PLL_TS];         // W0 -> W4: NCO phase words after each step
+  float s0[2][3][PLL_CH][PLL_TS];          // W4 -> W1: phase after the step, its sine and cosine
   float s1[2][5][PLL_CH][PLL_TS];          // W1 -> W2: PBM, MM, MAG2, FREQ, COS2
   float s2[2][4][PLL_CH][PLL_TS];          // W2 -> W3: TGT, MONO, DL, DR
   float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles for W2
@@ -1090,6 +1122,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 #define PLL_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #ifdef FMX_STAMPS
   unsigned long long pw_work = 0, pw_wait = 0, pw_last = __builtin_amdgcn_s_memtime();
+  const unsigned long long pw_rt0 = __builtin_amdgcn_s_memrealtime();
 #define PLL_SYNC()                                                   \
   {                                                                  \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
@@ -1155,19 +1188,18 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // ---------------- W0: the PLL feedback chain ----------------
     uint32_t theta = s0.theta, dtheta = s0.dtheta;
     const float alpha = D->pll_alpha, beta = D->pll_beta;
-    float vcoQ, vcoI;
-    fmx_sincos(d_nco_phase(theta), &vcoQ, &vcoI);
-    uint32_t vsg = 0; // sign bit of sin(phase) not yet applied to vcoQ
+    uint32_t vsg; // sign bit of sin(phase) not yet applied to vcoQ
+    float vcoQ = pll_sin_word(theta, &vsg);
     // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
     // iteration k), so its LDS latency overlaps the chain of the current tile
     float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
 #pragma unroll
     for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = *reinterpret_cast<const float4 *>(&sh->inp[0][lane][4 * q]);
-    for (int k = 0; k < NT + 3; ++k) {
+    for (int k = 0; k < PLL_NIT(NT); ++k) {
       if (k + 1 < NT) {
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q)
-          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) & 3][lane][4 * q]);
+          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lane][4 * q]);
       }
       // full tiles run without per-sample guards: the guards would sink the
       // tile's LDS read into every sample (an LDS round trip on the chain)
@@ -1180,40 +1212,24 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
           const float4 x = pcur[q];
           pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
         }
-        float ph[PLL_T], sq[PLL_T], cq[PLL_T];
+        uint32_t tw[PLL_T];
 #pragma unroll
         for (int t = 0; t < PLL_T; ++t) {
           if (FULL || t < cnt) {
+            // the sine's sign goes onto the pilot sample (off the chain)
             const float err = __uint_as_float(__float_as_uint(pv[t]) ^ vsg) * vcoQ; // pv * sin(phase)
             dtheta += d_nco_constrain(err * alpha);
             theta += d_nco_constrain(err * beta);
             theta += dtheta;
-            const float phaseNext = d_nco_phase(theta);
-            const int qn = fmx_nco_quadrant(theta); // off the phase's dependency chain
-            // both polynomials are needed for the quadrant anyway; the sine's
-            // sign goes onto the next pilot sample (off the chain)
-            float s0, c0;
-            fmx_sincos_q_abs(phaseNext, (float)qn, qn, &s0, &c0);
-            const float sN = (qn & 2) ? -s0 : s0;
-            const float cN = ((qn + 1) & 2) ? -c0 : c0;
-            vcoQ = s0;
-            vsg = (uint32_t)(qn & 2) << 30;
-            ph[t] = phaseNext;
-            sq[t] = sN;
-            cq[t] = cN;
+            vcoQ = pll_sin_word(theta, &vsg);
+            tw[t] = theta;
           } else {
-            ph[t] = sq[t] = cq[t] = 0.0f;
+            tw[t] = 0u;
           }
         }
 #pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          *reinterpret_cast<float4 *>(&sh->s0[ob][0][lane][4 * q]) =
-              make_float4(ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
-          *reinterpret_cast<float4 *>(&sh->s0[ob][1][lane][4 * q]) =
-              make_float4(sq[4 * q], sq[4 * q + 1], sq[4 * q + 2], sq[4 * q + 3]);
-          *reinterpret_cast<float4 *>(&sh->s0[ob][2][lane][4 * q]) =
-              make_float4(cq[4 * q], cq[4 * q + 1], cq[4 * q + 2], cq[4 * q + 3]);
-        }
+        for (int q = 0; q < PLL_T / 4; ++q)
+          *reinterpret_cast<uint4 *>(&sh->s0t[ob][lane][4 * q]) = make_uint4(tw[4 * q], tw[4 * q + 1], tw[4 * q + 2], tw[4 * q + 3]);
       };
       if (k < NT) {
         const int cnt = min(PLL_T, n - k * PLL_T);
@@ -1226,6 +1242,12 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     }
     PLL_SYNC() // W1 / W3 block-end values in sh->fin
     PLL_STAMP_OUT()
+#ifdef FMX_STAMPS
+    if (a.dbg && lane == 0) {
+      atomicAdd(a.dbg + 14, __builtin_amdgcn_s_memrealtime() - pw_rt0);
+      atomicMax(a.dbg + 15, __builtin_amdgcn_s_memrealtime() - pw_rt0);
+    }
+#endif
     if (!act) return;
     // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
     FmxStereoState s = s0;
@@ -1284,11 +1306,11 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     float phaseNow = d_nco_phase(s0.theta);
     float vcoQ, vcoI;
     fmx_sincos(phaseNow, &vcoQ, &vcoI);
-    for (int k = 0; k < NT + 3; ++k) {
-      const int kt = k - 1;
+    for (int k = 0; k < PLL_NIT(NT); ++k) {
+      const int kt = k - 2;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int ib = kt & 3, sb = kt & 1;
+        const int ib = kt % PLL_NINP, sb = kt & 1;
         float pv[PLL_T], mv[PLL_T], ph[PLL_T], sq[PLL_T], cq[PLL_T];
 #pragma unroll
         for (int q = 0; q < PLL_T / 4; ++q) {
@@ -1315,7 +1337,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
             freq = d_clamp(dphi, pmin, pmax);
             pi_ = (pi_ * kS) + ((pilot * vcoI) * kI);
             pq = (pq * kS) + ((pilot * vcoQ) * kI);
-            const float sN = sq[t], cN = cq[t]; // W0's sine / cosine of phaseNext
+            const float sN = sq[t], cN = cq[t]; // W4's sine / cosine of phaseNext
             o_pbm[t] = pbm;
             o_mm[t] = mm;
             o_mag2[t] = (pi_ * pi_) + (pq * pq);
@@ -1360,8 +1382,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // loads staged in registers TWO iterations ahead, across the barriers
     // (one iteration, ~0.8 us, left W3 waiting on HBM latency at the
     // stores): iteration k stores pilot tile k+2 (W0 reads it ahead at k+1),
-    // mpx tile k and delay tile k-1 (W1 and W2 at iteration k+1), then
-    // issues pilot k+4, mpx k+2, delay k+1 into the registers just stored.
+    // mpx tile k-1 and delay tile k-2 (W1 and W2 at iteration k+1), then
+    // issues pilot k+4, mpx k+1, delay k into the registers just stored.
     // Two register sets by tile parity; the loop is unrolled by two so every
     // set is static.
     PllStage stp0, stp1, stm0, stm1;
@@ -1399,28 +1421,27 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     stp0.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
     stp1.issue(rp, a.pilot_stride, 3 * PLL_T, lane);
     stm0.issue(rm4, a.mpx_stride, 0, lane);
-    stm1.issue(rm4, a.mpx_stride, PLL_T, lane);
-    sd0.issue(rm, a.mpx_stride, rh, 0, tcnt(0), lane, Dly);
     auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
       constexpr int P = decltype(par_c)::value; // k & 1
       PllStage &stp = P ? stp1 : stp0;          // pilot tile k+2, then k+4
-      PllStage &stm = P ? stm1 : stm0;          // mpx tile k, then k+2
-      PllDlyStage &std_ = P ? sd0 : sd1;        // delay tile k-1, then k+1
+      PllStage &stm = P ? stm0 : stm1;          // mpx tile k-1, then k+1
+      PllDlyStage &std_ = P ? sd1 : sd0;        // delay tile k-2, then k
       if (k + 2 < NT) {
-        if (full(k + 2)) stp.store(sh->inp[(k + 2) & 3], lane);
-        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[(k + 2) & 3], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
+        const int sl = (k + 2) % PLL_NINP;
+        if (full(k + 2)) stp.store(sh->inp[sl], lane);
+        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[sl], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
       }
-      if (k < NT) {
-        if (full(k)) stm.store(sh->inm[k & 1], lane);
-        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[k & 1], c0, k * PLL_T, tcnt(k), lane);
+      if (k - 1 >= 0 && k - 1 < NT) {
+        if (full(k - 1)) stm.store(sh->inm[(k - 1) & 1], lane);
+        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[(k - 1) & 1], c0, (k - 1) * PLL_T, tcnt(k - 1), lane);
       }
-      if (k - 1 >= 0 && k - 1 < NT) std_.store(sh->dly[(k - 1) & 1], lane);
+      if (k - 2 >= 0 && k - 2 < NT) std_.store(sh->dly[(k - 2) & 1], lane);
       W3_STAMP(0)
       stp.issue(rp, a.pilot_stride, (k + 4) * PLL_T, lane);
-      stm.issue(rm4, a.mpx_stride, (k + 2) * PLL_T, lane);
-      std_.issue(rm, a.mpx_stride, rh, (k + 1) * PLL_T, tcnt(k + 1), lane, Dly);
+      stm.issue(rm4, a.mpx_stride, (k + 1) * PLL_T, lane);
+      std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
       W3_STAMP(1)
-      const int kt = k - 3;
+      const int kt = k - 4;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
         const int sb = kt & 1;
@@ -1474,9 +1495,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       }
       PLL_SYNC()
     };
-    for (int k = 0; k < NT + 3; k += 2) {
+    for (int k = 0; k < PLL_NIT(NT); k += 2) {
       iter(k, std::integral_constant<int, 0>{});
-      if (k + 1 < NT + 3) iter(k + 1, std::integral_constant<int, 1>{});
+      if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
     }
     fin[5][lane] = blend;
     PLL_SYNC()
@@ -1489,7 +1510,29 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 #endif
 #undef W3_STAMP
   } else if (wave == PLL_IDLE) {
-    for (int k = 0; k < NT + 3; ++k) PLL_SYNC()
+    // ---------------- W4: phases for the outputs (shares W0's SIMD) ----------------
+    for (int k = 0; k < PLL_NIT(NT); ++k) {
+      // tile k-1 for W1 (iteration k+1): the reference's float phase of each
+      // word W0 produced and its sine / cosine (stereo_decoder.cpp:251-253)
+      const int kp = k - 1;
+      if (kp >= 0 && kp < NT) {
+        const int pb = kp & 1;
+#pragma unroll
+        for (int j = 0; j < PLL_CH * PLL_T / 64; ++j) {
+          const int idx = lane + 64 * j;
+          const int row = idx / PLL_T, t = idx % PLL_T;
+          const uint32_t th = sh->s0t[pb][row][t];
+          const float ph = d_nco_phase(th);
+          const int qn = fmx_nco_quadrant(th);
+          float sN, cN;
+          fmx_sincos_q(ph, (float)qn, qn, &sN, &cN);
+          sh->s0[pb][0][row][t] = ph;
+          sh->s0[pb][1][row][t] = sN;
+          sh->s0[pb][2][row][t] = cN;
+        }
+      }
+      PLL_SYNC()
+    }
     PLL_SYNC()
     PLL_STAMP_OUT()
   } else {
@@ -1497,8 +1540,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     const int t2 = tid - 128;  // 0..127 (waves 2, 3)
     const float nominal = D->nominal;
     const float fsf = (float)D->fs;
-    for (int k = 0; k < NT + 3; ++k) {
-      const int kt = k - 2;
+    for (int k = 0; k < PLL_NIT(NT); ++k) {
+      const int kt = k - 3;
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
         const int sb = kt & 1;
@@ -1521,7 +1564,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
             const float magNow = sqrtf(mag2);
             const float ratioNow = pbm / fmaxf(mm, 1e-3f);
             const float cohNow = magNow / fmaxf(pbm, 1e-4f);
-            const float errHzNow = fabsf(pf - nominal) * fsf / (2.0f * kPiF);
+            const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
             tgt = blend_target(ratioNow, cohNow, errHzNow, fl >> 8, false, false, true, sh->s2_gate[row]);
           }
           const float monoNorm = delayed * 0.5f;

@@ -15,7 +15,7 @@ NAMES = ["decim", "dc", "iqfir+agc", "discrim", "pilot", "rds_rs", "carry", "tai
 L = fmx.lib()
 L.fmx_debug_stamps.restype = C.c_int
 L.fmx_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
-Cn, B, M, nblk = int(os.environ.get("C", "4096")), 4096, 10, 4
+Cn, B, M, nblk = int(os.environ.get("C", "4096")), 4096, 10, int(os.environ.get("NBLK", "4"))
 h = fmx.Handle(fmx.make_config(), Cn)
 dev = torch.device("cuda")
 scfg = fmx.make_synth(kind=2, n_bits=6000)
@@ -50,3 +50,4 @@ for w, nm in enumerate(["W0 chain", "W1 env", "W2a", "W2b", "(idle)", "W3 blend+
     print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}")
 print(f"  W3 issue part {v[28] / (nwg * nblk):10.0f}")
 print(f"  W3 store part {v[29] / (nwg * nblk):10.0f}")
+print(f"  W0 realtime per WG (100 MHz ticks): mean {v[30] / (nwg * nblk):10.0f}  max over WGs and launches {v[31]:10.0f}")
