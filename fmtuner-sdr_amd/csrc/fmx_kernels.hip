@@ -985,15 +985,19 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
  * arithmetic in the reference's order; only WHERE it runs moved. */
 #define PLL_CH 64
 #define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
-#define PLL_WAVES 6
-// Waves w and w + 4 of a workgroup share a SIMD (measured,
+#define PLL_WAVES 8
+// Waves w, w + 4, w + 8 of a workgroup share a SIMD (measured,
 // tools/ubench/hwid.hip), and a SIMD retires about one wave64 VALU
-// instruction per 4 cycles whichever wave issues it: the PLL chain (W0,
-// wave 0) is alone on its SIMD (wave 4 only takes part in the barriers); W1
-// and W3 share one.
+// instruction per 4 cycles whichever wave issues it.  SIMD 0: W0 (chain),
+// W4 (output phases), W2c; SIMD 1: W1, W3, W2d; SIMD 2: W2a (+ wave 6,
+// barriers only); SIMD 3: W2b (+ wave 7, barriers only).  The blend-target
+// items (the longest per-tile work once stereo is detected) are spread over
+// all four SIMDs, one item per lane per W2 wave.
 #define PLL_W1 1
 #define PLL_IDLE 4
 #define PLL_W3 5
+#define PLL_NW2 4                          // W2 waves: 2, 3, 6, 7
+#define PLL_BARRIER_ONLY(w) false
 #define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
 #define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
 
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     pw_wait += pw_last - t_;                                         \
   }
 #define PLL_STAMP_OUT()                                              \
-  if (a.dbg && (threadIdx.x & 63) == 0) {                            \
+  if (a.dbg && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 6) { \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6), pw_work);              \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6) + 1, pw_wait);          \
   }
@@ -1509,6 +1513,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     }
 #endif
 #undef W3_STAMP
+  } else if (PLL_BARRIER_ONLY(wave)) {
+    for (int k = 0; k < PLL_NIT(NT); ++k) PLL_SYNC()
+    PLL_SYNC()
   } else if (wave == PLL_IDLE) {
     // ---------------- W4: phases for the outputs (shares W0's SIMD) ----------------
     for (int k = 0; k < PLL_NIT(NT); ++k) {
@@ -1536,8 +1543,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     PLL_SYNC()
     PLL_STAMP_OUT()
   } else {
-    // ---------------- W2a/W2b: time-parallel work ----------------
-    const int t2 = tid - 128;  // 0..127 (waves 2, 3)
+    // ---------------- W2a..W2d: time-parallel work ----------------
+    const int g2 = (wave == 2) ? 0 : (wave == 3) ? 1 : (wave == 6) ? 2 : 3; // W2a, W2b, W2c, W2d
     const float nominal = D->nominal;
     const float fsf = (float)D->fs;
     for (int k = 0; k < PLL_NIT(NT); ++k) {
@@ -1545,37 +1552,60 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
         const int sb = kt & 1;
-#pragma unroll 2
-        for (int j = 0; j < PLL_CH * PLL_T / 128; ++j) {
-          const int idx = t2 + 128 * j;
-          const int row = idx / PLL_T, t = idx % PLL_T;
-          const int fl = sh->s2_flags[row];
-          const float pbm = sh->s1[sb][F_PBM][row][t];
-          const float mm = sh->s1[sb][F_MM][row][t];
-          const float mag2 = sh->s1[sb][F_MAG2][row][t];
-          const float pf = sh->s1[sb][F_FREQ][row][t];
-          const float cos2 = sh->s1[sb][F_COS2][row][t];
-          const float delayed = sh->dly[sb][row][t];
-          float tgt;
-          if (fl & 1) tgt = 0.0f;
-          else if (fl & 2) tgt = 1.0f;
-          else if (!(fl & 4)) tgt = 0.0f;  // blend_target() returns 0 on every path
-          else {
-            const float magNow = sqrtf(mag2);
-            const float ratioNow = pbm / fmaxf(mm, 1e-3f);
-            const float cohNow = magNow / fmaxf(pbm, 1e-4f);
-            const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
-            tgt = blend_target(ratioNow, cohNow, errHzNow, fl >> 8, false, false, true, sh->s2_gate[row]);
-          }
+        // both items of a lane side by side and branch-free (the flag cases
+        // as selects), so their long dependent chains (IEEE sqrt, two IEEE
+        // divisions) interleave; blend_target's arithmetic is unchanged
+        constexpr int NJ = PLL_CH * PLL_T / (64 * PLL_NW2);
+        float tg[NJ], q[NJ];
+        int fl[NJ], row[NJ], tt[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int idx = lane + 64 * (g2 + PLL_NW2 * j);
+          row[j] = idx / PLL_T;
+          tt[j] = idx % PLL_T;
+          fl[j] = sh->s2_flags[row[j]];
+          const float pbm = sh->s1[sb][F_PBM][row[j]][tt[j]];
+          const float mm = sh->s1[sb][F_MM][row[j]][tt[j]];
+          const float mag2 = sh->s1[sb][F_MAG2][row[j]][tt[j]];
+          const float pf = sh->s1[sb][F_FREQ][row[j]][tt[j]];
+          const float gate = sh->s2_gate[row[j]];
+          const float magNow = sqrtf(mag2);
+          const float ratioNow = pbm / fmaxf(mm, 1e-3f);
+          const float cohNow = magNow / fmaxf(pbm, 1e-4f);
+          const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
+          // blend_target(ratioNow, cohNow, errHzNow, mode, false, false, true, gate)
+          constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cP = 320.0f - 180.0f;
+          const float ratioQ = d_clamp(d_div_const(ratioNow - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
+          const float cohQ = d_clamp(d_div_const(cohNow - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
+          const float pllQ = d_clamp(d_div_const(320.0f - errHzNow, cP, 1.0f / cP), 0.0f, 1.0f);
+          q[j] = fminf(ratioQ, fminf(cohQ, pllQ));
+          const bool gated = ratioNow < (0.022f * gate) || cohNow < (0.11f * gate) || errHzNow > (320.0f * 1.10f);
+          const int mode = fl[j] >> 8;
+          const float sq2 = q[j] * q[j];
+          const float shaped = (mode == 2) ? sq2 * q[j] : sq2; // mode 0 below
+          tg[j] = gated ? 0.0f : d_clamp(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
+          fl[j] |= gated ? 16 : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) { // mode 0 (soft): sqrt shaping, lanes of soft-blend channels only
+          if ((fl[j] >> 8) == 0 && !(fl[j] & 16)) tg[j] = d_clamp(0.0f + ((1.0f - 0.0f) * sqrtf(fmaxf(0.0f, q[j]))), 0.0f, 1.0f);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int f = fl[j];
+          // force mono -> 0, force stereo -> 1, not detected -> 0 (blend_target's paths)
+          const float tgt = (f & 1) ? 0.0f : ((f & 2) ? 1.0f : ((f & 4) ? tg[j] : 0.0f));
+          const float delayed = sh->dly[sb][row[j]][tt[j]];
+          const float cos2 = sh->s1[sb][F_COS2][row[j]][tt[j]];
           const float monoNorm = delayed * 0.5f;
           const float lr = 2.0f * delayed * cos2;
           const float sl = (delayed + lr) * 0.5f;
           const float sr = (delayed - lr) * 0.5f;
-          if (t < cnt) {
-            sh->s2[sb][F_TGT][row][t] = tgt;
-            sh->s2[sb][F_MONO][row][t] = monoNorm;
-            sh->s2[sb][F_DL][row][t] = sl - monoNorm;
-            sh->s2[sb][F_DR][row][t] = sr - monoNorm;
+          if (tt[j] < cnt) {
+            sh->s2[sb][F_TGT][row[j]][tt[j]] = tgt;
+            sh->s2[sb][F_MONO][row[j]][tt[j]] = monoNorm;
+            sh->s2[sb][F_DL][row[j]][tt[j]] = sl - monoNorm;
+            sh->s2[sb][F_DR][row[j]][tt[j]] = sr - monoNorm;
           }
         }
       }
