@@ -1,96 +1,246 @@
 #!/usr/bin/env python3
 """bench.py -- IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS).
 
-Workload (BASELINE.json configs[2]): 4096 independent
-2.4 MS/s channels per GPU, synthetic stereo FM (19 kHz pilot, L-R on 38 kHz,
-57 kHz RDS carrying known groups), decimate-by-10 to 240 kHz, de-emphasis
-50 us, dsp_block_samples = 4096.  One "step" = one reference block
-(40960 IQ samples) for every channel: decimator -> discriminator -> stereo
-PLL/blend -> 32 kHz audio -> RDS bits + block sync (fmx_process_block).
-All step inputs are generated into HBM before the timed region (fresh,
-phase-continuous IQ for every step).
+Workloads (BASELINE.json configs):
+  cfg3 (default)  4096 channels PER GPU of synthetic stereo FM + 57 kHz RDS
+                  (known groups), weak scaling over --gpus.
+  cfg4            16384 channels IN TOTAL sharded over the ranks with
+                  fmx_dist.shard (2048 per GPU at 8 GPUs), strong scaling.
+  --total-channels T overrides the total (sharded), --channels C the
+  per-GPU count.
+Every channel: 2.4 MS/s u8 IQ, decimate-by-10 to 240 kHz, de-emphasis 50 us,
+dsp_block_samples = 4096.  One "step" = one reference block (40960 IQ
+samples) for every channel: decimator -> discriminator -> stereo PLL/blend
+-> 32 kHz audio -> RDS bits + block sync, plus the per-block RF level
+(computeSignalLevel, main.cpp:1167) -- fmx_process_block.  All step inputs
+are generated into HBM before the timed region (fresh, phase-continuous IQ
+for every step), so `value` excludes PCIe.
 
-Multi-GPU: one process per GPU (torchrun), channels sharded by rank with no
-data-path collective (weak scaling); RCCL is used only for the barrier and
-the max-over-ranks time.
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` with no
+WORLD_SIZE in the environment re-launches itself under
+torch.distributed.run (N ranks, 127.0.0.1) before touching the GPU; under a
+launcher WORLD_SIZE must equal --gpus.  Channels are sharded by rank with no
+data-path collective; RCCL carries only the barrier, the max-over-ranks time,
+the summed channel count and the scan line's RF-level all_gather (the three
+last timed blocks of every channel are the scan's 3 reads per point,
+main.cpp:1064-1121).
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import glob
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fmtuner-sdr_amd"))
 
-# per-unit algorithmic figures: bytes and FLOP per input
-# IQ sample at M = 10 (stereo + RDS)
-BYTES_PER_IQ_FRONTEND = 2.0 + 0.4 + 0.4 + 4.0 * 0.7125 / 10.0   # u8 IQ in; MPX, pilot, RDS-rate out
-FLOP_PER_IQ_FRONTEND = 112.0 + 32.4 + 61.0 + 7.4                 # decim, IQ FIR, pilot BPF, RDS resampler
-PER_IQ = {  # kernel: (algorithmic HBM bytes, FLOP) per IQ sample
-    "frontend": (BYTES_PER_IQ_FRONTEND, FLOP_PER_IQ_FRONTEND),
-    "stereo": (0.4 + 0.8 + 0.8, 20.0),      # pilot + MPX + delayed MPX in, raw L/R out
-    "audio": (0.8 + 0.107, 48.0 + 3.0),     # raw L/R in, 32 kHz PCM out; L/R FIRs + AF
-    "rds": (4.0 * 0.7125 / 10.0, 15.0),     # 171 kHz samples in (groups out ~0)
+# algorithmic figures of the whole path per input IQ sample
+# (stereo + RDS, M = 10): 2 B u8 IQ in + 8 B stereo PCM per 32 kHz frame
+# (x 32000 / 2.4e6 = 0.107 B) = 2.107 B; 290 FLOP (decimator 112, IQ FIR
+# 32.4, pilot BPF 61, L/R FIRs 48, RDS 15, AF 3, PLL/trig 20).
+ALG_BYTES_PER_IQ = 2.107
+ALG_FLOP_PER_IQ = 290.0
+# per-kernel DESIGN figures: HBM bytes the design moves
+# per IQ sample including its own intermediates (MPX, pilot, RDS-rate, raw
+# L/R), and the kernel's share of the 290 FLOP
+PER_IQ = {
+    "frontend": (2.0 + 0.4 + 0.4 + 4.0 * 0.7125 / 10.0, 112.0 + 32.4 + 61.0 + 7.4),
+    "stereo": (0.4 + 0.8 + 0.8, 20.0),
+    "audio": (0.8 + 0.107, 48.0 + 3.0),
+    "rds": (4.0 * 0.7125 / 10.0, 15.0),
 }
-HBM_PEAK_GBS = 8000.0
-FP32_PEAK_TFLOPS = 157.3
+KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds"}
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3   # dense FP32 VALU
+METRIC = "IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS) at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE or 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--channels", type=int, default=4096, help="channels per GPU")
+    ap.add_argument("--workload", choices=["cfg3", "cfg4"], default="cfg3")
+    ap.add_argument("--channels", type=int, default=None, help="channels per GPU (cfg3 default 4096)")
+    ap.add_argument("--total-channels", type=int, default=None, help="channels in total, sharded over ranks")
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the all-core CPU sample")
     ap.add_argument("--sync-steps", action="store_true",
                     help="diagnostic: synchronize after every step (no cross-step overlap; not the reported mode)")
-    ap.add_argument("--cpu-channels", type=int, default=256)
-    ap.add_argument("--cpu-blocks", type=int, default=16)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_frontend.json"),
-                    help="per-launch HBM bytes of the frontend kernel from rocprofv3 --pmc (optional)")
-    return ap.parse_args()
+    ap.add_argument("--pmc-json", default=None,
+                    help="per-kernel HBM bytes per launch from rocprofv3 --pmc (tools/pmc_traffic.py); "
+                         "default: the newest profiles/r*_pmc*.json")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: set up the ranks / shards / collectives and print the plan (tests)")
+    return ap.parse_args(argv)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(n, argv):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def resolve_world(args):
+    """(world, spawn): world size of this run, and whether this process must
+    spawn the N ranks itself (no launcher in the environment)."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is None:
+        n = args.gpus or 1
+        return n, n > 1
+    w = int(env)
+    if args.gpus is not None and args.gpus != w:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={w}")
+    return w, False
+
+
+def plan_channels(args, world, rank):
+    """(ch0, C_local, total, scaling) for this rank."""
+    from fmx_dist import shard
+    total = args.total_channels
+    if total is None and args.workload == "cfg4":
+        total = 16384
+    if total is not None:
+        b, e = shard(total, world, rank)
+        return b, e - b, total, "strong"
+    c = args.channels or 4096
+    return rank * c, c, c * world, "weak"
+
+
+def newest_pmc():
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")))
+    return files[-1] if files else None
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(math.ceil(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"cpu_model": model, "nproc": nproc, "affinity": aff, "cgroup_cpus": quota, "usable": usable}
+
+
+def cpu_baseline(fmx, d_iq, C, nblk, n_iq, B, seconds):
+    """The oracle (CPU restatement, kind "port") on this box's host cores:
+    single-core rates for one Cfg3 channel and for Cfg1 (mono, 1 channel),
+    then one channel per thread on every usable core, sized to ~`seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+    info = cpu_info()
+    threads = info["usable"]
+    ocfg = oracle.make_cfg(block=B)
+    # single core, one Cfg3 channel (stereo + RDS)
+    nb1 = min(nblk, 40)
+    one = d_iq[:1, : 2 * n_iq * nb1].cpu().numpy().reshape(1, nb1, 2 * n_iq)
+    s1, _ = oracle.run_many(ocfg, one, nb1, 1)
+    r1 = nb1 * n_iq / s1 / 1e6
+    # single core, Cfg1: mono FM (1 kHz + 3 kHz), stereo=false path, no RDS
+    mono = fmx.synth_host(fmx.make_synth(kind=0), 0, 1, 0, n_iq * nb1)
+    sm, _ = oracle.run_many(oracle.make_cfg(block=B, stereo=0, rds=0), mono.reshape(1, nb1, 2 * n_iq), nb1, 1)
+    rm = nb1 * n_iq / sm / 1e6
+    # all usable cores: one channel per thread, enough blocks for ~`seconds`
+    want_iq = seconds * threads * r1 * 1e6
+    cc = min(C, max(threads, int(want_iq / (n_iq * nblk)) + 1))
+    cc = max(threads, (cc // threads) * threads) if C >= threads else C
+    nb = int(min(nblk, max(4, want_iq / (cc * n_iq))))
+    host = d_iq[:cc, : 2 * n_iq * nb].cpu().numpy().reshape(cc, nb, 2 * n_iq)
+    secs, _ = oracle.run_many(ocfg, host, nb, threads)
+    return {"value": round(cc * nb * n_iq / secs / 1e6, 2), "unit": "MS/s", "cores": threads, "kind": "port",
+            "sample": f"{cc} Cfg3 channels x {nb} blocks of 40960 IQ samples (stereo+RDS), oracle/fmx_oracle.cpp, "
+                      f"one channel per thread on {threads} threads, {secs:.2f} s wall",
+            "single_core": {"cfg3_one_channel_ms_s": round(r1, 3), "cfg1_mono_ms_s": round(rm, 3),
+                            "blocks": nb1},
+            **{k: info[k] for k in ("cpu_model", "nproc", "affinity", "cgroup_cpus")}}
 
 
 def main():
     args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    import fmx
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, spawn = resolve_world(args)
+    if spawn:
+        # no launcher: start the N ranks as children before any GPU call
+        sys.exit(subprocess.run(launcher_cmd(world, sys.argv[1:])).returncode)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # FMX_BENCH_BACKEND=gloo: rehearsal of the N-rank flow on fewer GPUs
-    # (ranks share GPUs round-robin, the timing collectives go over gloo)
-    backend = os.environ.get("FMX_BENCH_BACKEND", "nccl")
-    gpu = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    ch0, C, total, scaling = plan_channels(args, world, rank)
+    import torch
+    import torch.distributed as dist
+    # FMX_BENCH_BACKEND=gloo: rehearsal of the N-rank flow on fewer GPUs (ranks
+    # share GPUs round-robin, the collectives go over gloo); --dry-run: no GPU
+    backend = "gloo" if args.dry_run else os.environ.get("FMX_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(gpu)
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        from fmx_dist import gather_levels
+        lv = torch.full((C,), float(rank))
+        allv = gather_levels(lv)
+        tot = torch.tensor([float(C)])
+        if world > 1:
+            dist.all_reduce(tot)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "world_reported": dist.get_world_size() if world > 1 else 1,
+                              "backend": backend, "total_channels": total, "channels_summed": int(tot.item()),
+                              "scaling": scaling, "ch0": ch0, "channels_rank0": C,
+                              "gathered": int(allv.numel()),
+                              "gathered_ranks": [int(x) for x in allv[:: max(1, C)].tolist()]}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    import numpy as np
+    import fmx
+    import fmx_dist
+    gpu = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", gpu if world > 1 else 0)
+    dev = torch.device("cuda", gpu)
     cdev = dev if backend == "nccl" else torch.device("cpu")
+    world_reported = dist.get_world_size() if world > 1 else 1
 
-    C = args.channels
     B = args.block
     M = 10
     nblk = args.warmup + args.steps
     cfg = fmx.make_config(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=B,
                           w0_bandwidth_hz=194_000, bandwidth_hz=0, dsp_agc=0, stereo=1, blend=1,
                           deemphasis=0, rds=1)
-    h = fmx.Handle(cfg, C, device=gpu if world > 1 else 0)
-    ch0 = rank * C
+    h = fmx.Handle(cfg, C, device=gpu)
     # ---- inputs: synthetic stereo + RDS IQ for every step, resident in HBM ----
     n_iq = B * M
     n_bits = int((nblk * n_iq + 2 * 2_400_000) * 1187.5 / 2.4e6) + 208  # covers the per-channel RDS offset
@@ -100,23 +250,29 @@ def main():
     row = 2 * n_iq * nblk
     d_iq = torch.empty((C, row), dtype=torch.uint8, device=dev)
     h.synth_device(scfg, ch0, C, 0, n_iq * nblk, d_bits.data_ptr(), d_iq.data_ptr(), row)
+    del d_bits
     # ---- outputs ----
     pl = torch.empty((C, B), dtype=torch.float32, device=dev)
     pr = torch.empty((C, B), dtype=torch.float32, device=dev)
     cnt = torch.empty(C, dtype=torch.int32, device=dev)
     st = torch.empty(C, dtype=torch.int32, device=dev)
     pil = torch.empty(C, dtype=torch.int32, device=dev)
+    ind = torch.empty(C, dtype=torch.int32, device=dev)
     clip = torch.empty(C, dtype=torch.float32, device=dev)
     GS = 8
     grp = torch.empty((C, GS, 4), dtype=torch.int32, device=dev)
     gcnt = torch.empty(C, dtype=torch.int32, device=dev)
-    out = fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(), st.data_ptr(),
-                       pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS, gcnt.data_ptr())
+    # fmx_signal_level records (40 B) of the last three steps: the scan's
+    # three reads per point
+    sig = torch.zeros((3, C, 10), dtype=torch.float32, device=dev)
+    outs = [fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(), st.data_ptr(),
+                         pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS, gcnt.data_ptr(),
+                         sig[k].data_ptr(), ind.data_ptr()) for k in range(3)]
     h.sync()
     torch.cuda.synchronize()
 
     def step(b):
-        h.process_block(d_iq.data_ptr() + b * 2 * n_iq, row, B, out)
+        h.process_block(d_iq.data_ptr() + b * 2 * n_iq, row, B, outs[b % 3])
         if args.sync_steps:
             h.sync()
 
@@ -141,66 +297,100 @@ def main():
     ktimes = h.kernel_times()
     ngroups = int(gcnt.sum().item())
     stereo_frac = float(st.float().mean().item())
+    chans_all = float(C)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    iq_samples = float(world) * C * args.steps * n_iq
+        cc_ = torch.tensor([float(C)], dtype=torch.float64, device=cdev)
+        dist.all_reduce(cc_, op=dist.ReduceOp.SUM)
+        chans_all = float(cc_.item())
+    iq_samples = chans_all * args.steps * n_iq
     value = iq_samples / elapsed / 1e6  # MS/s, whole job
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # ---- roofline of the dominant kernel, from HIP events on its stream ----
-    dom = max(ktimes, key=lambda k: ktimes[k][0])
-    k_ms, k_n = ktimes["frontend"]
-    fe_avg_s = (k_ms / max(k_n, 1)) * 1e-3
-    units = C * n_iq
-    fe_flops = FLOP_PER_IQ_FRONTEND * units
-    fe_bytes = BYTES_PER_IQ_FRONTEND * units
-    achieved_tf = fe_flops / fe_avg_s / 1e12
-    traffic = None
-    if os.path.exists(args.pmc_json):
+    # ---- multi-channel scan line: every channel is a scan point; its level is
+    # the mean of the last three blocks' computeSignalLevel (main.cpp:1078-1103),
+    # gathered from all ranks (RCCL all_gather, fmx_dist.gather_levels) ----
+    level_sum = (sig[0, :, 0] + sig[1, :, 0] + sig[2, :, 0]).to(torch.float64)
+    tg0 = time.perf_counter()
+    all_levels = fmx_dist.gather_levels(level_sum.to(cdev))
+    gather_ms = (time.perf_counter() - tg0) * 1e3
+    scan = None
+    if rank == 0:
+        lv = all_levels.cpu().numpy()
+        freq = 87_500 + 50 * np.arange(lv.size, dtype=np.int64)  # synthetic channel plan, 50 kHz raster
+        line = fmx.xdr_scan_line(freq.astype(np.int32), lv, np.full(lv.size, 3, np.int32))
+        scan = {"points": int(lv.size), "reads_per_point": 3, "line_bytes": len(line),
+                "gather_ms": round(gather_ms, 3), "mean_level120": round(float(lv.mean() / 3.0), 2),
+                "head": line[:48]}
+
+    # ---- roofline: the kernel with the longest live launch (HIP events on
+    # its own stream over the timed region), against SURVEY 8(d)'s 2.107 B/IQ ----
+    units = C * n_iq  # IQ samples one launch of each kernel processes on this rank
+    avg = {k: v[0] / max(v[1], 1) * 1e-3 for k, v in ktimes.items() if v[1] > 0}
+    dom = max(avg, key=avg.get)
+    dom_s = avg[dom]
+    pmc_path = args.pmc_json or newest_pmc()
+    pmc = None
+    if pmc_path and os.path.exists(pmc_path):
         try:
-            with open(args.pmc_json) as f:
+            with open(pmc_path) as f:
                 pm = json.load(f)
             if int(pm.get("channels", -1)) == C and int(pm.get("block", -1)) == B:
-                traffic = float(pm["hbm_bytes_per_launch"])
-        except Exception:
-            traffic = None
-    achieved_gbs = fe_bytes / fe_avg_s / 1e9
-    roof = {"bound": "hbm", "kernel": "k_fe8 (frontend)", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
+                pmc = pm.get("kernels", {})
+        except (OSError, ValueError):
+            pmc = None
+    alg_bytes = ALG_BYTES_PER_IQ * units
+    achieved = alg_bytes / dom_s / 1e9
+    traffic = None
+    if pmc and KNAME[dom] in pmc:
+        traffic = pmc[KNAME[dom]].get("hbm_bytes_per_launch")
+    step_traffic = None
+    if pmc and all(KNAME[k] in pmc for k in avg):
+        step_traffic = sum(pmc[KNAME[k]]["hbm_bytes_per_launch"] for k in avg)
+    path_tflops = ALG_FLOP_PER_IQ * units / (ms_per_step * 1e-3) / 1e12
+    roof = {"bound": "hbm", "kernel": KNAME[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": os.path.relpath(pmc_path, ROOT) if pmc else None,
+            "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_iq": ALG_BYTES_PER_IQ,
+            "avg_launch_ms": round(dom_s * 1e3, 4),
+            # the whole step's counted HBM bytes (all four kernels) over the
+            # path's algorithmic bytes: intermediates round-tripping HBM
+            "step_traffic": step_traffic,
+            "step_traffic_over_algorithmic": round(step_traffic / alg_bytes, 3) if step_traffic else None,
             # the roof that binds this path (no MFMA: FIR/IIR/PLL work is FP32 VALU)
-            "valu_view": {"achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                          "algorithmic_flop_per_launch": fe_flops}}
+            "valu_path": {"achieved": round(path_tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(path_tflops / FP32_PEAK_TFLOPS, 4), "flop_per_iq": ALG_FLOP_PER_IQ,
+                          "per": "ms_per_step"}}
     kern = {}
     for k, v in ktimes.items():
-        avg_s = v[0] / max(v[1], 1) * 1e-3
+        if v[1] == 0:
+            continue
+        avg_s = avg[k]
         bpi, fpi = PER_IQ[k]
-        kern[k] = {"ms_total": round(v[0], 3), "launches": v[1], "avg_ms": round(avg_s * 1e3, 4),
-                   # live in the pipelined timed region (co-running kernels included)
-                   "hbm_gbs": round(bpi * units / max(avg_s, 1e-12) / 1e9, 1),
-                   "fp32_tflops": round(fpi * units / max(avg_s, 1e-12) / 1e12, 3)}
+        ent = {"kernel": KNAME[k], "ms_total": round(v[0], 3), "launches": v[1], "avg_ms": round(avg_s * 1e3, 4),
+               # live in the pipelined timed region (co-running kernels included)
+               "design_bytes_per_launch": bpi * units,
+               "design_hbm_gbs": round(bpi * units / avg_s / 1e9, 1),
+               "fp32_tflops": round(fpi * units / avg_s / 1e12, 3)}
+        if pmc and KNAME[k] in pmc:
+            pb = pmc[KNAME[k]]["hbm_bytes_per_launch"]
+            ent["pmc_bytes_per_launch"] = pb
+            ent["pmc_over_design"] = round(pb / (bpi * units), 3)
+        kern[k] = ent
 
     # ---- CPU baseline: the oracle on this box's host cores (rank 0, N=1) ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        cc = min(args.cpu_channels, C)
-        nb = min(args.cpu_blocks, nblk)
-        host = d_iq[:cc, : 2 * n_iq * nb].cpu().numpy().reshape(cc, nb, 2 * n_iq)
-        threads = min(16, os.cpu_count() or 1)
-        ocfg = oracle.make_cfg(block=B)
-        secs, _ = oracle.run_many(ocfg, host, nb, threads)
-        cpu = {"value": round(cc * nb * n_iq / secs / 1e6, 2), "unit": "MS/s", "cores": threads,
-               "kind": "port",
-               "sample": f"{cc} channels x {nb} blocks of 40960 IQ samples (stereo+RDS), oracle/fmx_oracle.cpp, "
-                         f"one channel per thread, {secs:.2f} s wall"}
+        cpu = cpu_baseline(fmx, d_iq, C, nblk, n_iq, B, args.cpu_seconds)
 
+    wl = {"cfg3": "cfg3: 4096 ch x 2.4 MS/s stereo FM + 57 kHz RDS per GPU",
+          "cfg4": "cfg4: 16384 ch x 2.4 MS/s stereo FM + 57 kHz RDS sharded over the GPUs"}[args.workload]
+    if args.total_channels is not None or args.channels is not None:
+        wl += f" (channels overridden: {int(chans_all)} total)"
     res = {
-        "metric": "IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS) at 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(value, 1),
         "unit": "MS/s",
         "n_gpus": world,
@@ -208,19 +398,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded stereo FM + RDS IQ generated in HBM)",
-        "config": {"workload": "cfg3: 4096 ch x 2.4 MS/s stereo FM + 57 kHz RDS per GPU, M=10 -> 240 kHz, "
-                               "dsp_block=4096, deemphasis 50 us",
-                   "channels_per_gpu": C, "block": B, "iq_rate": 2_400_000, "parallelism": f"channels/{world}gpu"},
+        "config": {"workload": wl + ", M=10 -> 240 kHz, dsp_block=4096, deemphasis 50 us",
+                   "total_channels": int(chans_all), "channels_rank0": C, "block": B, "iq_rate": 2_400_000,
+                   "parallelism": f"channels/{world}gpu", "backend": backend if world > 1 else None,
+                   "world_reported": world_reported},
         "per_gpu_ms_s": round(value / world, 1),
         "realtime_channels_per_gpu": round(value / world / 2.4, 1),
         "roofline": roof,
         "kernels": kern,
         "dominant_kernel": dom,
         "cpu_baseline": cpu,
+        "scan": scan,
         "check": {"rds_groups_last_step": ngroups, "rds_groups_warmup": groups_warm,
                   "stereo_fraction": stereo_frac},
     }
@@ -228,6 +420,7 @@ def main():
         print(json.dumps(res), flush=True)
     h.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

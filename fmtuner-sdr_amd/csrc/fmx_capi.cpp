@@ -90,6 +90,7 @@ struct Handle {
   FmxRdsState *rds = nullptr;
   int *reset_mask = nullptr;
   std::vector<int> hmask;
+  int *mute = nullptr; // [C][2] retune fade/mute {remaining, total} (main.cpp:1310-1337)
   // intermediates (double-buffered by step parity)
   float *mpx[FMX_NBUF] = {}, *pilot[FMX_NBUF] = {}, *rds_in[FMX_NBUF] = {};
   int *rds_count[FMX_NBUF] = {};
@@ -321,6 +322,7 @@ static ResetArgs reset_args(Handle *h) {
   r.mono_win = h->mono_win;
   r.mono_iir = h->mono_iir;
   r.rds_hist = h->rds_hist;
+  r.mute = h->mute;
   return r;
 }
 
@@ -556,6 +558,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->st, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->rds, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->reset_mask, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->mute, C * 2)) != FMX_OK) return rc;
   // intermediates
   for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->mpx[b], C * B)) != FMX_OK) return rc;
@@ -767,6 +770,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;
     a.pilot_tenths_out = o->d_pilot_tenths;
+    a.indicator_out = o->d_stereo_indicator;
     KTimer t(h, FMX_K_STEREO, h->sB);
     if (!h->skip_pll && (rc = launch_pll(a, h->sB)) != FMX_OK) {
       h->err = "pll launch failed";
@@ -775,6 +779,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   } else {
     if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->sB));
     if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->sB));
+    if (o->d_stereo_indicator) HIP_TRY(hipMemsetAsync(o->d_stereo_indicator, 0, sizeof(int) * h->C, h->sB));
   }
   HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
   h->evB_set[buf] = true;
@@ -790,6 +795,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.out_count = o->d_pcm_count;
     a.cap = h->cfg.block;
     a.clamp = 1;
+    a.mute = h->mute;
+    a.mute_fade = h->cfg.out_rate / 200;
     KTimer t(h, FMX_K_AUDIO, h->sD);
     if (!h->skip_audio && (rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
@@ -806,6 +813,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.out_count = o->d_pcm_count;
     a.cap = 1 << 30;
     a.clamp = 1;
+    a.mute = h->mute;
+    a.mute_fade = h->cfg.out_rate / 200;
     KTimer t(h, FMX_K_AUDIO, h->sD);
     if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
@@ -879,22 +888,41 @@ int fmx_sync(void *handle) {
 
 int fmx_num_channels(void *handle) { return handle ? H(handle)->C : 0; }
 
-int fmx_reset(void *handle, int channel) {
-  Handle *h = H(handle);
-  if (!h) return FMX_E_INVALID;
+static int reset_channels(Handle *h, int channel, int extra) {
   if (channel < -1 || channel >= h->C) {
     h->err = "channel out of range";
     return FMX_E_INVALID;
   }
   const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
   for (int c = c0; c < c1; ++c) {
-    int m = RS_DECIM | RS_DEMOD | RS_STEREO | RS_AF | RS_RDS;
+    int m = RS_DECIM | RS_DEMOD | RS_STEREO | RS_AF | RS_RDS | extra;
     if (h->agc_ready[static_cast<size_t>(c)]) m |= RS_AGC;
-    h->hmask[static_cast<size_t>(c)] |= m;
+    int &hm = h->hmask[static_cast<size_t>(c)];
+    if (m & RS_MUTE) hm &= 0xFFFF; // the latest mute length wins
+    hm |= m;
     tset_reset_channel(h->t_af, c);
     tset_reset_channel(h->t_mono, c);
   }
   return FMX_OK;
+}
+
+int fmx_reset(void *handle, int channel) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  return reset_channels(h, channel, 0);
+}
+
+int fmx_retune(void *handle, int channel, int mute_samples) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  // kRetuneMuteSamples = OUTPUT_RATE / 25 (main.cpp:696-697)
+  const int len = (mute_samples < 0) ? h->cfg.out_rate / 25 : mute_samples;
+  if (len > 65535) {
+    h->err = "mute_samples must be <= 65535";
+    return FMX_E_INVALID;
+  }
+  // a newer mute replaces any mute still running (main.cpp:1034-1035)
+  return reset_channels(h, channel, RS_MUTE | static_cast<int>(static_cast<unsigned>(len) << 16));
 }
 
 int fmx_set_param(void *handle, int channel, int key, int value) {

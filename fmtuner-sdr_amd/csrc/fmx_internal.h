@@ -92,7 +92,8 @@ struct PllArgs {
   int lr_stride;
   FmxStereoState *st;
   int *stereo_out, *pilot_tenths_out;
-  unsigned long long *dbg; // [10] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
+  int *indicator_out;      // [C] XDR stereo indicator (main.cpp:1298-1300), may be null
+  unsigned long long *dbg; // [16] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
   int prio;                // raise the waves' issue priority (s_setprio)
 };
 
@@ -118,6 +119,8 @@ struct AudioArgs {
   const int *group; // [C]
   int sched_stride;
   int clamp;
+  int *mute;       // [C][2] retune fade/mute {remaining, total} (main.cpp:1310-1337), may be null
+  int mute_fade;   // OUTPUT_RATE / 200
 };
 
 struct RdsArgs {
@@ -161,6 +164,7 @@ struct ResetArgs {
   float *st_hist; // [FMX_ST_BUFS][C][FMX_HIST]
   float *lr_hist, *af_win, *af_iir, *mono_win, *mono_iir;
   float *rds_hist;
+  int *mute;      // [C][2]
 };
 #define FMX_NBUF 3                // per-step intermediates (MPX, pilot, RDS-rate, raw L/R): front end k
                                   // runs while stereo/RDS/audio of steps k-1, k-2 drain
@@ -174,7 +178,8 @@ enum ResetParts {
   RS_RDS = 32,     // RDSDecoder::reset (symsync + NCO + block stream)
   RS_IQFIR = 64,   // IQ FIR re-created (setBandwidthHz)
   RS_DEEMPH = 128, // de-emphasis IIRs re-created (setDeemphasis)
-  RS_CREATE = 256  // object construction (everything, incl. RDS resampler/AGC)
+  RS_CREATE = 256, // object construction (everything, incl. RDS resampler/AGC)
+  RS_MUTE = 512    // retune fade/mute start; mute length in bits 16..31 (main.cpp:1034-1035)
 };
 int launch_reset(const ResetArgs &a, void *stream);
 

@@ -75,14 +75,9 @@ __device__ __forceinline__ float d_nco_phase(uint32_t theta) {
   // is folded into the constant (one v_mul_f64, same rounding)
   return (float)((double)(float)theta * (6.283185307179586 / 4294967296.0));
 }
-// x / c correctly rounded for a constant c with rc = RN(1/c) (Markstein:
-// residual exact by FMA); 3 dependent ops instead of the IEEE divide
-// sequence.  Checked against IEEE division on 6e6 phase increments (c = 57000).
-__device__ __forceinline__ float d_div_const(float x, float c, float rc) {
-  const float q = x * rc;
-  const float r = fmaf(-q, c, x);
-  return fmaf(r, rc, q);
-}
+// x / c by fmx_div_const (fmx_math.h), for the divisors whose exactness
+// against IEEE x / c tests/cpp/divconst_test.cpp checks exhaustively
+__device__ __forceinline__ float d_div_const(float x, float c, float rc) { return fmx_div_const(x, c, rc); }
 // unwrapf (liquid_wrappers.cpp / stereo_decoder.cpp): one 2pi step into
 // [-pi, pi], as selects (no divergent branches in the sample loops)
 __device__ __forceinline__ float d_unwrap(float x) {
@@ -1001,23 +996,23 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 #define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
 #define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
 
-// sin(2 pi theta / 2^32) for the PLL feedback only: half-turn reduction on
-// the phase word itself, theta = m 2^31 + d (|d| <= 2^30, m's parity in bit
-// 31 of the result *sg), r = d pi / 2^31 (one rounding), and the degree-9
-// minimax sine on [-pi/2, pi/2]; sin = (*sg ? -1 : 1) * the return value.
-// 11 VALU instead of the float phase (f64 multiply) and both quadrant
-// polynomials of fmx_sincos_q.  |err| <= 1.4e-7 against the exact phase
-// (4.4e-7 against sin of the reference's float phase, whose own rounding
-// dominates); the outputs keep fmx_sincos_q of the reference's float phase.
-__device__ __forceinline__ float pll_sin_word(uint32_t theta, uint32_t *sg) {
-  const uint32_t s = (theta + 0x40000000u) & 0x80000000u;
-  const float r = (float)(int32_t)(theta ^ s) * 1.4629180792671596e-09f;
-  const float z = r * r;
-  float u = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
-  u = fmaf(u, z, 0.00833307858556509017944336f);
-  u = fmaf(u, z, -0.166666597127914428710938f);
-  *sg = s;
-  return fmaf(z, u * r, r);
+// The chain's sine: pll_sin_word (fmx_math.h) straight from the phase word
+// (11 VALU), or with FMX_PLL_SIN_WORD=0 the reference's float phase and
+// fmx_sincos_q (the outputs' arithmetic) for A/B parity runs.
+#ifndef FMX_PLL_SIN_WORD
+#define FMX_PLL_SIN_WORD 1
+#endif
+__device__ __forceinline__ float pll_chain_sin(uint32_t theta, uint32_t *sg) {
+#if FMX_PLL_SIN_WORD
+  return pll_sin_word(theta, sg);
+#else
+  const float ph = d_nco_phase(theta);
+  const int qn = fmx_nco_quadrant(theta);
+  float s0, c0;
+  fmx_sincos_q_abs(ph, (float)qn, qn, &s0, &c0);
+  *sg = (qn & 2) ? 0x80000000u : 0u;
+  return s0;
+#endif
 }
 struct PllShared {
   float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-2 in W1
@@ -1159,6 +1154,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     if (tid < PLL_CH && ch < a.C) {
       if (a.stereo_out) a.stereo_out[ch] = a.st[ch].detected;
       if (a.pilot_tenths_out) a.pilot_tenths_out[ch] = a.st[ch].level;
+      if (a.indicator_out) a.indicator_out[ch] = a.st[ch].detected || (a.par[ch].force_mono && a.st[ch].level >= 20);
     }
     return;
   }
@@ -1193,7 +1189,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     uint32_t theta = s0.theta, dtheta = s0.dtheta;
     const float alpha = D->pll_alpha, beta = D->pll_beta;
     uint32_t vsg; // sign bit of sin(phase) not yet applied to vcoQ
-    float vcoQ = pll_sin_word(theta, &vsg);
+    float vcoQ = pll_chain_sin(theta, &vsg);
     // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
     // iteration k), so its LDS latency overlaps the chain of the current tile
     float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
@@ -1225,7 +1221,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
             dtheta += d_nco_constrain(err * alpha);
             theta += d_nco_constrain(err * beta);
             theta += dtheta;
-            vcoQ = pll_sin_word(theta, &vsg);
+            vcoQ = pll_chain_sin(theta, &vsg);
             tw[t] = theta;
           } else {
             tw[t] = 0u;
@@ -1303,6 +1299,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     a.st[c] = s;
     if (a.stereo_out) a.stereo_out[c] = s.detected;
     if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
+    // XDR stereo indicator: stereoDetected || (forceMono && stereo && pilot >= 20)
+    // (main.cpp:1298-1300; k_pll runs only with processing.stereo)
+    if (a.indicator_out) a.indicator_out[c] = (s.detected || (par.force_mono && s.level >= 20)) ? 1 : 0;
   } else if (wave == PLL_W1) {
     // ---------------- W1: envelopes, pilot I/Q, frequency, cos 2phi ----------------
     float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q, freq = s0.pll_freq;
@@ -1744,6 +1743,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const float *inl = a.in_l + (size_t)c * a.in_stride;
   const float *inr = mono ? nullptr : a.in_r + (size_t)c * a.in_stride;
   const float sc = D->lr_scale;
+  // retune fade/mute of this call (main.cpp:1310-1337): outputs o < mrem
+  // get the gain of position (mtot - mrem) + o of the fade-out/mute/fade-in
+  int mrem = 0, mtot = 0;
+  if (a.mute) {
+    mrem = a.mute[2 * c];
+    mtot = a.mute[2 * c + 1];
+  }
+  const int mdone = (mtot > mrem) ? mtot - mrem : 0;
+  const int mfade = max(1, min(a.mute_fade, mtot / 2));
   __syncthreads();
   for (int n0 = 0; n0 < n; n0 += AU2_T) {
     const int cnt = min(AU2_T, n - n0);
@@ -1910,6 +1918,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
             yr = d_clamp(yr, -1.0f, 1.0f);
           }
           const int o = o0 + 3 * tid + k;
+          if (o < mrem) {
+            const int idx = mdone + o;
+            float gain = 0.0f;
+            if (idx < mfade) gain = 1.0f - ((float)idx / (float)mfade);
+            else if (idx >= mtot - mfade) gain = (float)(mtot - idx) / (float)mfade;
+            gain = d_clamp(gain, 0.0f, 1.0f);
+            yl *= gain;
+            yr *= gain;
+          }
           if (o < a.cap) {
             a.out_l[(size_t)c * a.out_stride + o] = yl;
             if (pipe_mono) a.out_r[(size_t)c * a.out_stride + o] = yl;
@@ -1953,7 +1970,13 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         for (int k = 0; k < 4; ++k) iir[k] = S.iir[k];
       }
     }
-    if (tid == 0 && a.out_count) a.out_count[c] = S.count < a.cap ? S.count : a.cap;
+    const int nout = S.count < a.cap ? S.count : a.cap;
+    if (tid == 0 && a.out_count) a.out_count[c] = nout;
+    if (tid == 0 && a.mute && mrem > 0 && nout > 0) {
+      const int mc = min(nout, mrem);
+      a.mute[2 * c] = mrem - mc;
+      if (mrem - mc == 0) a.mute[2 * c + 1] = 0;
+    }
   }
 }
 
@@ -2781,6 +2804,12 @@ __global__ void k_reset(ResetArgs a) {
       for (int h = tid; h < 2 * FMX_RDS_RING; h += blockDim.x) a.ring[(size_t)c * 2 * FMX_RDS_RING + h] = 0.0f;
       for (int h = tid; h < 32; h += blockDim.x) a.rds_hist[(size_t)c * 32 + h] = 0.0f;
     }
+  }
+  // retune fade/mute (main.cpp:1034-1035): remaining = total = mute length
+  if (tid == 0 && (create || (m & RS_MUTE))) {
+    const int len = (m & RS_MUTE) ? (int)((uint32_t)m >> 16) : 0;
+    a.mute[2 * c] = len;
+    a.mute[2 * c + 1] = len;
   }
 }
 

@@ -65,12 +65,42 @@ FMX_HD void fmx_sincos(float x, float *s, float *c) {
   fmx_sincos_q(x, q, (int)q, s, c);
 }
 
+// x / c for a constant c with rc = RN(1/c): q = x rc, then one Markstein
+// correction with the exact FMA residual -- 3 dependent ops instead of the
+// IEEE divide sequence.  Not correctly rounded for every divisor: it is used
+// only for the divisors tests/cpp/divconst_test.cpp checks against IEEE x / c
+// over every finite float numerator (tests/test_math.py).
+FMX_HD float fmx_div_const(float x, float c, float rc) {
+  const float q = x * rc;
+  const float r = fmaf(-q, c, x);
+  return fmaf(r, rc, q);
+}
+
 // Quadrant count of an NCO phase word: round(theta / 2^30) in 0..4, the
 // quadrant of the exact phase 2 pi theta / 2^32.  The float phase the
 // reference computes from theta is within 0.5 ulp of it, so fmx_sincos_q of
 // that phase with this count stays inside the polynomial range; it is known
 // as soon as theta is, off the phase's dependency chain (the k_pll loop).
 FMX_HD int fmx_nco_quadrant(uint32_t theta) { return (int)((theta >> 30) + ((theta >> 29) & 1u)); }
+
+// sin(2 pi theta / 2^32) for the stereo PLL's feedback chain only (k_pll
+// W0, stereo_decoder.cpp:251-256): half-turn reduction on the phase word,
+// theta = m 2^31 + d (|d| <= 2^30, m's parity returned in bit 31 of *sg),
+// r = d pi / 2^31 (one rounding), and the degree-9 minimax sine on
+// [-pi/2, pi/2]; sin = (*sg ? -1 : 1) * the return value.  11 VALU instead
+// of the float phase (an f64 multiply) and both quadrant polynomials.  Its
+// error against sin of the reference's float phase is measured over all 2^32
+// words by tests/cpp/pllsin_test.cpp (tests/golden/pllsin_exhaustive.json).
+FMX_HD float pll_sin_word(uint32_t theta, uint32_t *sg) {
+  const uint32_t s = (theta + 0x40000000u) & 0x80000000u;
+  const float r = (float)(int32_t)(theta ^ s) * 1.4629180792671596e-09f;
+  const float z = r * r;
+  float u = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
+  u = fmaf(u, z, 0.00833307858556509017944336f);
+  u = fmaf(u, z, -0.166666597127914428710938f);
+  *sg = s;
+  return fmaf(z, u * r, r);
+}
 
 // RF-level clip pre-test on one 4-byte word of u8 I/Q (signal_level.cpp:
 // computeSignalLevel counts samples with a component <= 8 or >= 247): nonzero

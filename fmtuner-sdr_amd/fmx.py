@@ -47,7 +47,7 @@ class BlockOut(C.Structure):
                 ("d_stereo", C.c_void_p), ("d_pilot_tenths", C.c_void_p),
                 ("d_clip_ratio", C.c_void_p), ("d_groups", C.c_void_p),
                 ("groups_stride", C.c_int), ("d_group_count", C.c_void_p),
-                ("d_signal", C.c_void_p)]
+                ("d_signal", C.c_void_p), ("d_stereo_indicator", C.c_void_p)]
 
 
 class XdrPiState(C.Structure):
@@ -83,6 +83,7 @@ def lib():
         "fmx_sync": (i, [vp]),
         "fmx_num_channels": (i, [vp]),
         "fmx_reset": (i, [vp, i]),
+        "fmx_retune": (i, [vp, i, i]),
         "fmx_set_param": (i, [vp, i, i, i]),
         "fmx_set_signal_params": (i, [vp, i, i, C.c_double, C.c_double, C.c_double, C.c_double]),
         "fmx_process_block": (i, [vp, vp, sz, i, C.POINTER(BlockOut)]),
@@ -173,6 +174,10 @@ class Handle:
 
     def reset(self, channel=-1):
         self._ck(self.L.fmx_reset(self.h, channel), "fmx_reset")
+
+    def retune(self, channel=-1, mute_samples=-1):
+        """Runtime::reset + retune fade/mute (main.cpp:1028-1042, 1310-1337)."""
+        self._ck(self.L.fmx_retune(self.h, channel, mute_samples), "fmx_retune")
 
     def set_param(self, key, value, channel=-1):
         k = PARAM[key] if isinstance(key, str) else key

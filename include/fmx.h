@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 3
+#define FMX_ABI_VERSION 4
 
 enum {
   FMX_OK = 0,
@@ -108,6 +108,8 @@ typedef struct {
   int groups_stride;
   int *d_group_count;      /* [C]                                             */
   fmx_signal_level *d_signal; /* [C] RF level of this call's IQ (u8 input)    */
+  int *d_stereo_indicator; /* [C] XDR stereo flag: isStereo() || (forceMono &&
+                              stereo && pilot >= 2.0 kHz), main.cpp:1298-1300 */
 } fmx_block_out;
 
 /* ---- lifetime ---- */
@@ -122,6 +124,13 @@ int fmx_num_channels(void *handle);
  * decimator) plus the RDS worker reset (main.cpp:909-916).  channel = -1
  * resets every channel. */
 int fmx_reset(void *handle, int channel);
+/* The retune path of main.cpp:1028-1042: the same reset fan-out, then the
+ * PCM of the next mute_samples 32 kHz outputs (per channel, across calls) is
+ * faded out over OUTPUT_RATE/200 samples, muted, and faded back in, as
+ * main.cpp:1310-1337 does after the clamp.  mute_samples < 0 takes the
+ * reference's kRetuneMuteSamples = OUTPUT_RATE/25 (main.cpp:696-697); 0
+ * cancels a running mute.  At most 65535. */
+int fmx_retune(void *handle, int channel, int mute_samples);
 
 /* Per-channel settings mirroring the reference setters; channel = -1 = all. */
 enum {

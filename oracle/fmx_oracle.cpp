@@ -133,18 +133,35 @@ static inline float dot_rf(const float *hrev, const float *w, unsigned n) {
   return r;
 }
 
-/* linear window: keeps last n samples, oldest first (liquid window/wdelay) */
+/* linear window: keeps last n samples, oldest first (liquid window/wdelay).
+ * Like liquid's windowcf, the buffer is longer than the window (n + slack)
+ * and the live n samples are shifted back to the front only when the write
+ * position reaches the end: O(1) amortised per push, same contents. */
 template <typename T> struct Window {
   std::vector<T> buf;
-  unsigned n = 0;
-  void init(unsigned len) { n = len; buf.assign(len, T{}); }
-  void reset() { std::fill(buf.begin(), buf.end(), T{}); }
+  unsigned n = 0, rd = 0, cap = 0;
+  void init(unsigned len) {
+    n = len;
+    cap = len + std::max(len, 256u);
+    buf.assign(cap, T{});
+    rd = 0;
+  }
+  void reset() {
+    std::fill(buf.begin(), buf.end(), T{});
+    rd = 0;
+  }
   void push(T x) {
     if (n == 0) return;
-    std::memmove(buf.data(), buf.data() + 1, (n - 1) * sizeof(T));
-    buf[n - 1] = x;
+    if (rd + n == cap) {
+      std::memmove(buf.data(), buf.data() + rd + 1, (n - 1) * sizeof(T));
+      rd = 0;
+      buf[n - 1] = x;
+      return;
+    }
+    rd++;
+    buf[rd + n - 1] = x;
   }
-  const T *data() const { return buf.data(); }
+  const T *data() const { return buf.data() + rd; }
 };
 
 /* firfilt_crcf: y = scale * sum_i h[i] x[t-i] */
@@ -1436,6 +1453,8 @@ struct Pipeline {
   std::vector<cf> bb;
   std::vector<float> mpx, l, r, ol, orr;
   uint32_t blockIndex = 0;
+  // retuneMuteSamplesRemaining / retuneMuteTotalSamples (main.cpp:1034-1035)
+  size_t muteRemaining = 0, muteTotal = 0;
 
   explicit Pipeline(const oracle_cfg &c)
       : cfg(c), M(c.iq_rate / c.dsp_rate), demod(c.dsp_rate, c.out_rate),
@@ -1473,6 +1492,12 @@ struct Pipeline {
     af.reset();
     decim.reset();
     if (rds) rds->reset();
+  }
+  void retune(int muteSamples) {
+    reset();
+    const size_t k = (muteSamples < 0) ? static_cast<size_t>(cfg.out_rate / 25) : static_cast<size_t>(muteSamples);
+    muteRemaining = k;
+    muteTotal = k;
   }
   int block(const uint8_t *iq, int iqSamples, float *mpxOut, float *pl, float *pr, int cap,
             oracle_group *groups, int gcap, oracle_blockinfo *info) {
@@ -1512,9 +1537,33 @@ struct Pipeline {
       sd = stereo.stereoDetected ? 1 : 0;
       pt = stereo.pilotLevelTenthsKHz;
     }
+    // XDR stereo indicator (main.cpp:1298-1300)
+    const int indicator = (sd != 0 || (stereo.forceMono && cfg.stereo && pt >= 20)) ? 1 : 0;
     for (size_t i = 0; i < nOut; ++i) {
       ol[i] = std::clamp(ol[i], -1.0f, 1.0f);
       orr[i] = std::clamp(orr[i], -1.0f, 1.0f);
+    }
+    // retune fade-out / mute / fade-in (main.cpp:1310-1337)
+    if (muteRemaining > 0 && nOut > 0) {
+      const size_t muteCount = std::min(nOut, muteRemaining);
+      const size_t alreadyMuted = (muteTotal > muteRemaining) ? (muteTotal - muteRemaining) : 0;
+      const size_t fadeSamples =
+          std::max<size_t>(1, std::min(static_cast<size_t>(cfg.out_rate / 200), muteTotal / 2));
+      for (size_t i = 0; i < muteCount; ++i) {
+        const size_t idx = alreadyMuted + i;
+        float gain = 0.0f;
+        if (idx < fadeSamples) {
+          gain = 1.0f - (static_cast<float>(idx) / static_cast<float>(fadeSamples));
+        } else if (idx >= (muteTotal - fadeSamples)) {
+          const size_t tail = muteTotal - idx;
+          gain = static_cast<float>(tail) / static_cast<float>(fadeSamples);
+        }
+        gain = std::clamp(gain, 0.0f, 1.0f);
+        ol[i] *= gain;
+        orr[i] *= gain;
+      }
+      muteRemaining -= muteCount;
+      if (muteRemaining == 0) muteTotal = 0;
     }
     if (mpxOut) std::memcpy(mpxOut, mpx.data(), n * sizeof(float));
     size_t nc = std::min(nOut, static_cast<size_t>(std::max(cap, 0)));
@@ -1527,6 +1576,7 @@ struct Pipeline {
       info->pilot_tenths_khz = pt;
       info->clip_ratio = demod.clipRatio;
       info->n_groups = ng;
+      info->stereo_indicator = indicator;
     }
     blockIndex++;
     return static_cast<int>(nOut);
@@ -1547,6 +1597,7 @@ void *oracle_pipeline_create(const oracle_cfg *cfg) {
 }
 void oracle_pipeline_destroy(void *p) { delete static_cast<ref::Pipeline *>(p); }
 void oracle_pipeline_reset(void *p) { static_cast<ref::Pipeline *>(p)->reset(); }
+void oracle_pipeline_retune(void *p, int mute_samples) { static_cast<ref::Pipeline *>(p)->retune(mute_samples); }
 int oracle_pipeline_block(void *p, const uint8_t *iq, int iq_samples, float *mpx_out, float *pcm_l,
                           float *pcm_r, int pcm_cap, oracle_group *groups, int groups_cap,
                           oracle_blockinfo *info) {

@@ -57,12 +57,16 @@ typedef struct {
   int pilot_tenths_khz;
   float clip_ratio;
   int n_groups;
+  int stereo_indicator; /* main.cpp:1298-1300 */
 } oracle_blockinfo;
 
 /* ---- full per-channel pipeline (restates main.cpp:1232-1308) ---- */
 void *oracle_pipeline_create(const oracle_cfg *cfg);
 void oracle_pipeline_destroy(void *p);
 void oracle_pipeline_reset(void *p); /* Runtime::reset fan-out main.cpp:686-691 + RDS reset */
+/* retune (main.cpp:1028-1042): reset + fade/mute of mute_samples outputs
+ * (< 0: kRetuneMuteSamples = OUTPUT_RATE/25, main.cpp:696-697) */
+void oracle_pipeline_retune(void *p, int mute_samples);
 /* iq: 2*iq_samples bytes (iq_samples = block*M).  Outputs may be NULL. */
 int oracle_pipeline_block(void *p, const uint8_t *iq, int iq_samples,
                           float *mpx_out, float *pcm_l, float *pcm_r,

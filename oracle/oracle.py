@@ -31,7 +31,7 @@ class OracleGroup(C.Structure):
 class BlockInfo(C.Structure):
     _fields_ = [("n_mpx", C.c_int), ("n_pcm", C.c_int), ("stereo_detected", C.c_int),
                 ("pilot_tenths_khz", C.c_int), ("clip_ratio", C.c_float),
-                ("n_groups", C.c_int)]
+                ("n_groups", C.c_int), ("stereo_indicator", C.c_int)]
 
 
 _lib = None
@@ -47,6 +47,7 @@ def lib():
             "oracle_pipeline_create": (vp, [C.POINTER(OracleCfg)]),
             "oracle_pipeline_destroy": (None, [vp]),
             "oracle_pipeline_reset": (None, [vp]),
+            "oracle_pipeline_retune": (None, [vp, i]),
             "oracle_pipeline_block": (i, [vp, vp, i, vp, vp, vp, i, vp, i, C.POINTER(BlockInfo)]),
             "oracle_pipeline_taps": (i, [vp, i, vp, i]),
             "oracle_pipeline_set": (None, [vp, i, i]),
@@ -145,6 +146,9 @@ class Pipeline:
     def reset(self):
         self.L.oracle_pipeline_reset(self.p)
 
+    def retune(self, mute_samples=-1):
+        self.L.oracle_pipeline_retune(self.p, mute_samples)
+
     PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
                  force_mono=6, force_stereo=7, bandwidth_mode=8)
 
@@ -165,6 +169,7 @@ class Pipeline:
                                          pl.ctypes.data, pr.ctypes.data, B, g, 64, C.byref(info))
         return dict(mpx=mpx[:info.n_mpx], pcm_l=pl[:n], pcm_r=pr[:n],
                     stereo=info.stereo_detected, pilot=info.pilot_tenths_khz,
+                    indicator=info.stereo_indicator,
                     clip=info.clip_ratio, groups=groups_to_tuples(g, min(info.n_groups, 64)))
 
     def taps(self, which):

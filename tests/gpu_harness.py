@@ -4,8 +4,10 @@ block and returns both outputs."""
 import numpy as np
 
 
-def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None):
-    """iq: uint8 [C][nblk * 2*B*M]. Returns per-block lists of numpy outputs."""
+def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None, retunes=None):
+    """iq: uint8 [C][nblk * 2*B*M]. Returns per-block lists of numpy outputs.
+    resets {block: channel}, retunes {block: (channel, mute_samples)},
+    params {block: [(key, value, channel)]} are applied before that block."""
     C = iq.shape[0]
     B = cfg.block
     M = cfg.iq_rate // cfg.dsp_rate
@@ -20,17 +22,20 @@ def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None
     st = torch.zeros(C, dtype=torch.int32, device=dev)
     pil = torch.zeros(C, dtype=torch.int32, device=dev)
     clip = torch.zeros(C, dtype=torch.float32, device=dev)
+    ind = torch.zeros(C, dtype=torch.int32, device=dev)
     GS = 8
     grp = torch.zeros((C, GS, 4), dtype=torch.int32, device=dev)  # 16-byte fmx_rds_group
     gcnt = torch.zeros(C, dtype=torch.int32, device=dev)
     out = fmx.BlockOut(mpx.data_ptr(), B, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(),
                        st.data_ptr(), pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS,
-                       gcnt.data_ptr())
+                       gcnt.data_ptr(), None, ind.data_ptr())
     res = []
     row = iq.shape[1]
     for b in range(nblk):
         if resets and b in resets:
             h.reset(resets[b])
+        if retunes and b in retunes:
+            h.retune(*retunes[b])
         if params and b in params:
             for (k, v, ch) in params[b]:
                 h.set_param(k, v, ch)
@@ -50,12 +55,13 @@ def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None
         res.append(dict(mpx=mpx[:, :n].cpu().numpy().copy(), pcm_l=pl.cpu().numpy().copy(),
                         pcm_r=pr.cpu().numpy().copy(), count=cnt.cpu().numpy().copy(),
                         stereo=st.cpu().numpy().copy(), pilot=pil.cpu().numpy().copy(),
-                        clip=clip.cpu().numpy().copy(), groups=groups))
+                        clip=clip.cpu().numpy().copy(), indicator=ind.cpu().numpy().copy(),
+                        groups=groups))
     h.close()
     return res
 
 
-def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=None):
+def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=None, retunes=None):
     B = ocfg.block
     M = ocfg.iq_rate // ocfg.dsp_rate
     n = n or B
@@ -64,6 +70,8 @@ def run_oracle_pipeline(oracle, ocfg, iq_row, nblk, n=None, resets=None, params=
     for b in range(nblk):
         if resets and b in resets:
             p.reset()
+        if retunes and b in retunes:
+            p.retune(retunes[b])
         if params and b in params:
             for (k, v) in params[b]:
                 p.set_param(k, v)
@@ -82,6 +90,7 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
     pil_mismatch = 0
     pil_maxdiff = 0
     cnt_mismatch = 0
+    ind_mismatch = 0
     g_gpu, g_ora = [], []
     for b in range(nblk):
         o, g = ores[b], gres[b]
@@ -90,6 +99,7 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
         if int(g["count"][c]) != k:
             cnt_mismatch += 1
         st_mismatch += int(o["stereo"] != int(g["stereo"][c]))
+        ind_mismatch += int(o["indicator"] != int(g["indicator"][c]))
         g_gpu += g["groups"][c]
         g_ora += o["groups"]
         if pcm_blocks is not None and b not in pcm_blocks:
@@ -103,5 +113,65 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
         pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
         pil_maxdiff = max(pil_maxdiff, abs(int(o["pilot"]) - int(g["pilot"][c])))
     return dict(mpx_max=mpx_err, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
-                stereo_mismatch=st_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
+                stereo_mismatch=st_mismatch, indicator_mismatch=ind_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
                 groups_gpu=g_gpu, groups_oracle=g_ora)
+
+
+def run_gpu_sampled(fmx, torch, cfg, C, scfg, nblk, keep, setup=None, retunes=None, n_bits=None):
+    """Full-size run: C channels of synthetic IQ generated in HBM
+    (fmx_synth_device), every block through fmx_process_block, and only the
+    rows of the channels in `keep` copied back.  setup: [(key, value,
+    channel)] applied after creation; retunes: {block: (channel, mute)}.
+    Returns (per-block results indexed by position in keep, host IQ rows of
+    keep [len(keep)][nblk * 2*B*M], transmitted groups of keep)."""
+    import numpy as np
+    B = cfg.block
+    M = cfg.iq_rate // cfg.dsp_rate
+    n_iq = B * M
+    h = fmx.Handle(cfg, C)
+    for (k, v, ch) in (setup or []):
+        h.set_param(k, v, ch)
+    dev = torch.device("cuda")
+    bits, tx = fmx.synth_rds_bits(scfg, 0, C)
+    d_bits = torch.from_numpy(bits).to(dev)
+    row = 2 * n_iq * nblk
+    d_iq = torch.empty((C, row), dtype=torch.uint8, device=dev)
+    h.synth_device(scfg, 0, C, 0, n_iq * nblk, d_bits.data_ptr(), d_iq.data_ptr(), row)
+    kidx = torch.tensor(keep, dtype=torch.long, device=dev)
+    mpx = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    pl = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    pr = torch.zeros((C, B), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    st = torch.zeros(C, dtype=torch.int32, device=dev)
+    pil = torch.zeros(C, dtype=torch.int32, device=dev)
+    clip = torch.zeros(C, dtype=torch.float32, device=dev)
+    ind = torch.zeros(C, dtype=torch.int32, device=dev)
+    GS = 8
+    grp = torch.zeros((C, GS, 4), dtype=torch.int32, device=dev)
+    gcnt = torch.zeros(C, dtype=torch.int32, device=dev)
+    out = fmx.BlockOut(mpx.data_ptr(), B, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(),
+                       st.data_ptr(), pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS,
+                       gcnt.data_ptr(), None, ind.data_ptr())
+    res = []
+    for b in range(nblk):
+        if retunes and b in retunes:
+            h.retune(*retunes[b])
+        h.process_block(d_iq.data_ptr() + b * 2 * n_iq, row, B, out)
+        h.sync()
+        sel = lambda t: t.index_select(0, kidx).cpu().numpy().copy()  # noqa: E731
+        g = sel(grp).view(np.uint8).reshape(len(keep), GS, 16)
+        gc = sel(gcnt)
+        groups = []
+        for j in range(len(keep)):
+            lst = []
+            for k in range(min(int(gc[j]), GS)):
+                w = g[j, k]
+                a, bb, cc, d = np.frombuffer(w[:8].tobytes(), dtype=np.uint16)
+                lst.append((int(a), int(bb), int(cc), int(d), int(w[8])))
+            groups.append(lst)
+        res.append(dict(mpx=sel(mpx), pcm_l=sel(pl), pcm_r=sel(pr), count=sel(cnt), stereo=sel(st),
+                        pilot=sel(pil), clip=sel(clip), indicator=sel(ind), groups=groups,
+                        stereo_all=float(st.float().mean().item())))
+    iq_keep = d_iq.index_select(0, kidx).cpu().numpy()
+    h.close()
+    return res, iq_keep, tx[keep]

@@ -29,3 +29,41 @@ def test_near_clip_word_test_exhaustive(tmp_path):
                     os.path.join(ROOT, "tests", "cpp", "swar_test.cpp")], check=True, timeout=120)
     r = json.loads(subprocess.run([exe], check=True, capture_output=True, text=True, timeout=300).stdout)
     assert r == {"false_negatives": 0, "false_positives": 0}
+
+
+def test_div_const_matches_ieee_division(tmp_path):
+    """fmx_div_const (the kernels' division by a constant) is bit-identical
+    to IEEE x / c for every normal numerator 1e-30 <= |x| <= 2^60 and zero,
+    for the five divisors it is used with (blend target cR / cC / cP, PLL
+    error 2 pi, RDS quad-phase 57000).  Mismatches exist only below 1e-30
+    (residual underflow), where the kernels' numerators never are.  The
+    exhaustive sweep (stride 1) is committed in tests/golden/divconst_exhaustive.json;
+    this runs every 7th bit pattern."""
+    exe = str(tmp_path / "divconst_test")
+    subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "divconst_test.cpp")], check=True, timeout=120)
+    r = json.loads(subprocess.run([exe, "7"], check=True, capture_output=True, text=True, timeout=600).stdout)
+    for name in ("cR", "cC", "cP", "2pi", "57000"):
+        assert r[name]["bad_ge_1e-30"] == 0, (name, r[name])
+    with open(os.path.join(ROOT, "tests", "golden", "divconst_exhaustive.json")) as f:
+        ex = json.load(f)
+    for name in ("cR", "cC", "cP", "2pi", "57000"):
+        assert ex[name]["bad_ge_1e-30"] == 0 and ex[name]["max_bad_abs"] < 1e-30
+
+
+def test_pll_chain_sine_error_bounds(tmp_path):
+    """pll_sin_word (k_pll's feedback sine from the NCO word) against sin of
+    the reference's float phase and of the exact phase.  Exhaustive over all
+    2^32 words: tests/golden/pllsin_exhaustive.json (4.4e-7 vs the float
+    phase, 1.3e-7 vs the exact phase; fmx_sincos_q on the float phase: 5e-8 /
+    4.3e-7).  This runs every 61st word and checks the same bounds."""
+    exe = str(tmp_path / "pllsin_test")
+    subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "pllsin_test.cpp")], check=True, timeout=120)
+    r = json.loads(subprocess.run([exe, "61"], check=True, capture_output=True, text=True, timeout=600).stdout)
+    assert r["pll_sin_word_vs_float_phase"] < 4.5e-7, r
+    assert r["pll_sin_word_vs_exact"] < 1.4e-7, r
+    assert r["sincos_q_vs_float_phase"] < 6e-8, r
+    with open(os.path.join(ROOT, "tests", "golden", "pllsin_exhaustive.json")) as f:
+        ex = json.load(f)
+    assert ex["stride"] == 1 and ex["pll_sin_word_vs_float_phase"] < 4.5e-7 and ex["pll_sin_word_vs_exact"] < 1.4e-7
