@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=None,
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc (tools/pmc_traffic.py); "
                          "default: the newest profiles/r*_pmc*.json")
+    ap.add_argument("--no-signal-level", action="store_true",
+                    help="diagnostic: skip the per-block RF level (computeSignalLevel) output")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: set up the ranks / shards / collectives and print the plan (tests)")
     return ap.parse_args(argv)
@@ -267,7 +269,7 @@ def main():
     sig = torch.zeros((3, C, 10), dtype=torch.float32, device=dev)
     outs = [fmx.BlockOut(None, 0, pl.data_ptr(), pr.data_ptr(), B, cnt.data_ptr(), st.data_ptr(),
                          pil.data_ptr(), clip.data_ptr(), grp.data_ptr(), GS, gcnt.data_ptr(),
-                         sig[k].data_ptr(), ind.data_ptr()) for k in range(3)]
+                         None if args.no_signal_level else sig[k].data_ptr(), ind.data_ptr()) for k in range(3)]
     h.sync()
     torch.cuda.synchronize()
 

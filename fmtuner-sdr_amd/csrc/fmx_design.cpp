@@ -270,6 +270,11 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     float sc = 1.0f;
     design_fir(d->rds_fir, sc, FMX_RDS_FIR, 2400.0f / kTarget, 60.0f, 0.0f);
     d->rds_fir_scale = sc;
+    for (int jp = 0; jp < FMX_RDS_DECIM; ++jp)
+      for (int i = 0; i < 12; ++i) {
+        const int k = jp + FMX_RDS_DECIM * i;
+        d->rds_rows[jp][i] = (i < FMX_RDS_NACC && k < FMX_RDS_FIR) ? d->rds_fir[k] : 0.0f;
+      }
     d->agc_bw = 500.0f / kTarget;
     d->agc_g0 = 0.08f;
     const float k2Pi = 2.f * kPiF;

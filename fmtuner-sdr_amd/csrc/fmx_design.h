@@ -70,6 +70,9 @@ typedef struct {
   // RDS subcarrier (subcarrier.cpp:94-106, liquid_wrappers.cpp)
   float rds_fir[FMX_RDS_NACC * FMX_RDS_DECIM]; // 255 taps + zeros to 264 (k_rds reads rows jp + 24 i)
   float rds_fir_scale;
+  // k_rds tap rows for the wave-uniform decimation phase jp: row jp holds
+  // h[jp + 24 i], i = 0..10, and a zero (48-B rows, read into SGPRs)
+  float rds_rows[FMX_RDS_DECIM][12] __attribute__((aligned(16)));
   float agc_bw, agc_g0;
   uint32_t rds_dtheta0;
   float rds_alpha, rds_beta;

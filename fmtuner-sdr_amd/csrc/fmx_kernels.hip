@@ -1689,7 +1689,10 @@ __device__ __forceinline__ void au_scan_prev(float A, float BL, float BR, float 
 }
 
 __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
-  __shared__ AuShared S;
+  // dynamic LDS, as k_rds: a static 45 KB made the backend pad the VGPR
+  // allocation from 111 to 129 (occupancy 3 by LDS)
+  extern __shared__ __align__(16) unsigned char au_smem[];
+  AuShared &S = *reinterpret_cast<AuShared *>(au_smem);
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
@@ -2015,20 +2018,21 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
          ((uint32_t)bs_block_number(ooff) + d / 26) % 4 == (uint32_t)bs_block_number(off);
 }
 
-// k_rds input tiles: 64 samples x 64 channels, filled by 16-B LDS-DMA.
-// One DMA instruction writes a 1-KiB piece = 4 channel rows of 16 segments
-// of 4 samples; piece p holds rows 4p..4p+3, row q at dword q*64, its
-// segment s rotated to slot (s + 4q) & 15, pieces RDS_PIECE dwords apart.
-// A wave reading one segment per lane (lane = row) then hits all 64 banks
-// once per 16 lanes (conflict-free ds_read_b128).
+// k_rds input: a ring of RDS_RING samples x 64 channels in LDS, sample-major
+// (tin[s][lane]), filled by LDS-DMA one dword per lane per instruction: lane
+// l's buffer load from its own channel row lands at LDS dword l of the
+// instruction's row, so a tile of RDS_TILE samples is RDS_TILE instructions
+// and every read of one sample by the wave is 64 consecutive dwords
+// (conflict-free ds_read_b32).
 #ifndef FMX_HWSIN_RDS
 #define FMX_HWSIN_RDS 1
 #endif
-#define RDS_PIECE 260
+#define RDS_TILE 8  // samples per LDS-DMA tile
+#define RDS_RING 32 // ring of 4 tiles: up to 3 in flight ahead of the one being read
 #ifndef RDS_U
 #define RDS_U 8 // samples per chunk (divides 24)
 #endif
-#define RDS_SYMQ 24 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
+#define RDS_SYMQ 12 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
 // Per-lane state lives in LDS (odd dword stride: conflict-free across lanes);
 // only the per-sample quantities (NCO, FIR partial sums, AGC, symsync
 // scalars) are held in registers.  Block sync / biphase state is touched once
@@ -2103,14 +2107,25 @@ __device__ __forceinline__ void rds_bits_store(FmxRdsState &g, const RdsBits &b)
   }
   g.bs_bits_since_lost = b.bs_bits_since_lost;
 }
+// The 8 chunk taps of one accumulator (two 16-B broadcast LDS reads).  The
+// __restrict__ parameter gives the inlined loads alias-scope metadata, which
+// lets the wait-count pass see they cannot alias the input ring's LDS-DMA
+// writes in flight (without it every chunk waited vmcnt(0) for them).
+__device__ __forceinline__ void rds_taps8(const float *__restrict__ p, float (&t)[8]) {
+  const float4 a = *reinterpret_cast<const float4 *>(p);
+  const float4 b = *reinterpret_cast<const float4 *>(p + 4);
+  t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w;
+  t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
+}
 struct RdsLds {
-  float taps[24][12] __attribute__((aligned(16))); // row jp: h[jp + 24 i], i = 0..10, zero pad
+  // chunk taps by accumulator: tT[p][i][u] = h[J - u + 24 i] for the chunk
+  // starting at period phase j0 = 1 + 8p (J = 24 - j0), zero past tap 254
+  float tT[3][FMX_RDS_NACC][8] __attribute__((aligned(16)));
   float mf[FMX_NPFB * FMX_SS_SUB];
   float dmf[FMX_NPFB * FMX_SS_SUB];
   uint32_t esyn[5][52];
   uint32_t eerr[5][52];
-  float tin[2][16 * RDS_PIECE]; // double-buffered tiles of 64 samples x 64 channels (rds_tile_* layout)
-  f32x2 win[2 * FMX_SS_SUB][64]; // symsync window ring per lane: sample at p and p + 18
+  f32x2 win[FMX_SS_SUB][64];     // symsync window ring per lane, newest at wp
   float symq[RDS_SYMQ][64];      // symbols (real part) awaiting biphase / block sync
   RdsCold cold[64];
 };
@@ -2241,10 +2256,28 @@ __device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &
  * period): the 7 NCO phases with no PLL update in between are evaluated
  * independently, only their wrapped sum is serial, then 8 sincos and the
  * partial sums with wave-uniform (LDS broadcast) tap rows. */
-__global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
+// s_waitcnt as a builtin plus a compiler-only memory barrier: no inline asm
+// in k_rds, so the backend can prove it uses no AGPRs and does not reserve
+// the whole register file for them (inline asm there made every k_rds wave
+// allocate 257 registers, leaving no room for two k_fe8 waves on its SIMD)
+#define rds_wait(imm)                    \
+  do {                                    \
+    __atomic_signal_fence(__ATOMIC_SEQ_CST); \
+    __builtin_amdgcn_s_waitcnt(imm);      \
+    __atomic_signal_fence(__ATOMIC_SEQ_CST); \
+  } while (0)
+__global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
   else if (a.prio) __builtin_amdgcn_s_setprio(2);
-  __shared__ RdsLds L;
+  // dynamic LDS (sizeof(RdsLds) at launch): with a static size the backend
+  // sees an LDS-limited occupancy and pads every wave's register allocation
+  // up to it (257 VGPRs), which keeps k_rds off SIMDs running k_fe8
+  extern __shared__ __align__(16) unsigned char rds_smem[];
+  RdsLds &L = *reinterpret_cast<RdsLds *>(rds_smem);
+  // the LDS-DMA input ring (sample t of lane l at tin[t % RDS_RING][l]) is a
+  // separate (static, 8 KB) object: reads of the tables in L then provably
+  // do not alias the DMA writes in flight and need no vmcnt wait
+  __shared__ __align__(16) float tin[RDS_RING][64];
 #ifdef FMX_STAMPS
   unsigned long long rs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long rs_last = __builtin_amdgcn_s_memtime();
@@ -2263,10 +2296,10 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   const bool act = c < a.C;
   const FmxDesign *__restrict__ D = a.des;
   // ---- LDS tables ----
-  for (int idx = lane; idx < 24 * 12; idx += 64) {
-    const int jp = idx / 12, i = idx % 12;
-    const int k = jp + 24 * i;
-    L.taps[jp][i] = (i < FMX_RDS_NACC && k < FMX_RDS_FIR) ? D->rds_fir[k] : 0.0f;
+  for (int idx = lane; idx < 3 * FMX_RDS_NACC * 8; idx += 64) {
+    const int p = idx / (FMX_RDS_NACC * 8), i = (idx / 8) % FMX_RDS_NACC, u = idx % 8;
+    const int k = (FMX_RDS_DECIM - 1 - 8 * p) - u + FMX_RDS_DECIM * i;
+    L.tT[p][i][u] = (k < FMX_RDS_FIR) ? D->rds_fir[k] : 0.0f;
   }
   for (int idx = lane; idx < FMX_NPFB * FMX_SS_SUB; idx += 64) {
     L.mf[idx] = D->ss_mf[idx];
@@ -2299,7 +2332,6 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   for (int m = 0; m < FMX_SS_SUB; ++m) {
     const f32x2 w = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
     L.win[m][lane] = w;
-    L.win[m + FMX_SS_SUB][lane] = w;
   }
   int wp = FMX_SS_SUB - 1; // newest window sample at wp (and wp + 18)
   if (act && G.rebuild) {
@@ -2336,22 +2368,28 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   float last_symi = 0.0f;
 
   // one mixed sample into the 11 streaming partial sums (reference order)
-  auto acc_add = [&](f32x2 m, int t, const float *tp) __attribute__((always_inline)) {
-    const float4 h0 = *reinterpret_cast<const float4 *>(tp);
-    const float4 h1 = *reinterpret_cast<const float4 *>(tp + 4);
-    const float4 h2 = *reinterpret_cast<const float4 *>(tp + 8);
-    const float h[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
-#pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC; ++i) {
-      const f32x2 p = f32x2{h[i], h[i]} * m;
-      acc[i] = acc[i] + p;
-    }
-    if (t >= ring_from) { // wave-uniform test first: only the last FMX_RDS_RING samples are kept
+  // the last FMX_RDS_RING mixed samples of the call are kept (decimation-
+  // phase rebuild after a reset)
+  auto ring_store = [&](f32x2 m, int t) __attribute__((always_inline)) {
+    if (t >= ring_from) { // wave-uniform test first
       if (t >= count - FMX_RDS_RING) {
         const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
         *reinterpret_cast<f32x2 *>(ring + 2 * idx) = m;
       }
     }
+  };
+  // tp: the sample's tap row (D->rds_rows[jp]); through the constant address
+  // space (SGPR operands) when jp is wave-uniform, a per-lane global row otherwise
+  auto acc_add = [&](f32x2 m, int t, auto tp) __attribute__((always_inline)) {
+    float h[FMX_RDS_NACC];
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC; ++i) h[i] = tp[i];
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC; ++i) {
+      const f32x2 p = f32x2{h[i], h[i]} * m;
+      acc[i] = acc[i] + p;
+    }
+    ring_store(m, t);
   };
   auto mix = [&](float x, float ph) __attribute__((always_inline)) {
     float sn, cs;
@@ -2394,19 +2432,23 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     // ---- symsync: push into both MF banks' window ----
     wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
     L.win[wp][lane] = f32x2{yr, yi};
-    L.win[wp + FMX_SS_SUB][lane] = f32x2{yr, yi};
     if (ss_valid < FMX_SS_SUB) ss_valid++;
-    const int w0 = wp + 1; // oldest
+    const int w0 = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1; // oldest
+    // window entry m (oldest first) of the ring
+    auto wat = [&](int m) __attribute__((always_inline)) {
+      const int i = w0 + m;
+      return L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][lane];
+    };
     int ns = 0;
     f32x2 sym = f32x2{0.0f, 0.0f};
     while (ss_b < FMX_NPFB && ns < 16) {
       const float *hm = L.mf + ss_b * FMX_SS_SUB;
       f32x2 acm = f32x2{0.0f, 0.0f};
-      const int first = FMX_SS_SUB - ss_valid;
+      // entries not pushed since the reset are the zeros k_reset wrote
 #pragma unroll
       for (int m = 0; m < FMX_SS_SUB; ++m) {
         const float h = hm[FMX_SS_SUB - 1 - m];
-        const f32x2 w = (m >= first) ? L.win[w0 + m][lane] : f32x2{0.0f, 0.0f};
+        const f32x2 w = wat(m);
         const f32x2 p = f32x2{h, h} * w;
         acm = acm + p;
       }
@@ -2418,7 +2460,7 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
 #pragma unroll
         for (int m = 0; m < FMX_SS_SUB; ++m) {
           const float h = hd[FMX_SS_SUB - 1 - m];
-          const f32x2 p = f32x2{h, h} * L.win[w0 + m][lane];
+          const f32x2 p = f32x2{h, h} * wat(m);
           acd = acd + p;
         }
         float q = acm.x * acd.x + acm.y * acd.y;
@@ -2485,74 +2527,56 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     if (nq > 0) S.bi_prev_im = last_symi;
     nq = 0;
   };
-  // ---- input tiles [tb, tb + RDS_TW) of 64 channels in LDS; the next 64
-  // samples of every row prefetched into registers (one coalesced 256-B row
-  // per load, 64 loads in flight) while the current tile is consumed ----
-  __syncthreads();
-  // Tile k = samples [64k, 64k + 64) of the 64 channels; tiles k and k+1 sit
-  // in L.tin[cur] / L.tin[cur ^ 1].  Tile k+2 is requested by LDS-DMA as soon
-  // as tile k is left behind.  Rows past C read as 0 (buffer range check).
+  __syncthreads(); // LDS tables and per-lane state written
+  // ---- input ring (see RdsLds::tin): tiles k = samples [8k, 8k + 8), tile
+  // k in ring rows (8k) % RDS_RING.  Tiles up to `ti` - 1 are issued; a tile
+  // is read once two later tiles were issued after it (vmcnt(2 x 8) then
+  // guarantees it landed, whatever stores sit between).  Rows past C read 0.
   const int rows_valid = min(64, a.C - c0);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + (size_t)c0 * a.in_stride,
                                                (uint32_t)((size_t)rows_valid * a.in_stride * sizeof(float)));
-  const int my_row = (lane >> 2) * RDS_PIECE + (lane & 3) * 64; // dword of this lane's row in a tile
-  const int my_rot = (lane & 3) * 4;
-  // DMA lane i of a piece: row q = i / 16, slot i & 15 holds segment (slot - 4q) & 15
-  const uint32_t dma_lane_off =
-      (uint32_t)(((lane >> 4) * a.in_stride + 4 * (((lane & 15) - 4 * (lane >> 4)) & 15)) * 4);
-  auto dma_tile = [&](int buf, int base) __attribute__((always_inline)) {
-    uint32_t off = dma_lane_off + (uint32_t)base * 4u;
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rin, (__attribute__((address_space(3))) void *)&L.tin[buf][p * RDS_PIECE], 16, off, 0, 0, 0);
-      off += (uint32_t)a.in_stride * 16u; // 4 rows
-      asm volatile("" : "+v"(off));
-    }
-  };
-  // segment g (0..31, counted from the start of tile cur) of this lane's row
-  auto seg_ptr = [&](int cur_, int g) __attribute__((always_inline)) {
-    return &L.tin[cur_ ^ (g >> 4)][my_row + (((g & 15) + my_rot) & 15) * 4];
+  const uint32_t row_off = (uint32_t)(lane * a.in_stride * 4);
+  int ti = 0;     // next tile to issue
+  int landed = -1; // tiles <= landed are in LDS
+  auto dma_tile = [&](int k) __attribute__((always_inline)) {
+    k = __builtin_amdgcn_readfirstlane(k); // wave-uniform: M0 without a waterfall loop
+    float *dst = &tin[(RDS_TILE * k) & (RDS_RING - 1)][0];
+    // the instruction's immediate offset would move the LDS address too: the
+    // sample offset goes into soffset
+    const int so = RDS_TILE * 4 * k;
+#define RDS_DMA1(i)                                                                                           \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void *)(dst + 64 * (i)), 4, \
+                                           row_off, so + 4 * (i), 0, 0)
+    static_assert(RDS_TILE == 8, "dma_tile issues 8 samples");
+    RDS_DMA1(0); RDS_DMA1(1); RDS_DMA1(2); RDS_DMA1(3); RDS_DMA1(4); RDS_DMA1(5); RDS_DMA1(6); RDS_DMA1(7);
+#undef RDS_DMA1
   };
   RDS_STAMP(0)
-  int tb = 0, cur = 0; // sample index of L.tin[cur] column 0
-  dma_tile(0, 0);
-  dma_tile(1, 64);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  bool nxt_ok = true; // tile k+1 has landed
-  // make [t, t + len) resident (t moves forward, len <= 8)
+  // make samples [t, t + len) readable (t moves forward, len <= RDS_TILE)
   auto need = [&](int t, int len) __attribute__((always_inline)) {
-    if (t >= tb + 64) {
-      RDS_STAMP(2)
-      // tile k is done: its buffer takes tile k+2
-      if (!nxt_ok) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      dma_tile(cur, tb + 128);
-      tb += 64;
-      cur ^= 1;
-      nxt_ok = false;
-      RDS_STAMP(1)
+    t = __builtin_amdgcn_readfirstlane(t); // the sample loop's t is wave-uniform
+    const int k0 = t / RDS_TILE;
+    if (ti <= k0 + 3) {
+      // the ring slots being refilled were read by earlier chunks only
+      rds_wait(0xC07F); // lgkmcnt(0)
+      while (ti <= k0 + 3) dma_tile(ti++);
+      ti = __builtin_amdgcn_readfirstlane(ti);
     }
-    if (t + len > tb + 64 && !nxt_ok) { // first read reaching into tile k+1
+    if ((t + len - 1) / RDS_TILE > landed) {
       RDS_STAMP(2)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      nxt_ok = true;
+      rds_wait(0x4F70); // vmcnt(16)
+      landed = __builtin_amdgcn_readfirstlane(ti - 3);
       RDS_STAMP(1)
     }
   };
-  auto read1 = [&](int t) __attribute__((always_inline)) {
-    const int d = t - tb;
-    return seg_ptr(cur, d >> 2)[d & 3];
-  };
-  // one sample for every lane that still has input: own tap row from LDS
+  auto read1 = [&](int t) __attribute__((always_inline)) { return tin[t & (RDS_RING - 1)][lane]; };
+  // one sample for every lane that still has input: its own tap row
   auto step_one = [&](int t) __attribute__((always_inline)) {
     need(t, 1);
     if (act && t < count) {
       const int j = (int)(ssr % FMX_RDS_DECIM);
       const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
-      acc_add(mix(read1(t), phase0), t, &L.taps[jp][0]);
+      acc_add(mix(read1(t), phase0), t, &D->rds_rows[jp][0]);
       if (j == 0) fir_output();
       nco_step();
     }
@@ -2560,11 +2584,17 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   const uint32_t j_mine = act ? (ssr % FMX_RDS_DECIM) : 0xFFFFFFFFu;
   uint32_t j_first = j_mine;
   for (int d = 32; d >= 1; d >>= 1) j_first = min(j_first, (uint32_t)__shfl_xor((int)j_first, d));
+  j_first = (uint32_t)__builtin_amdgcn_readfirstlane((int)j_first); // same in every lane: an SGPR
   const bool uniform_j = __ballot(act && j_mine != j_first) == 0;
   constexpr int U = RDS_U;
-  constexpr int NSEG = (U + 6) / 4; // 16-B segments covering U samples at any offset
+  static_assert(U == 8, "the chunk tap table tT holds 8 samples");
   // one chunk of U samples starting at a period phase of 1, 9 or 17
-  auto chunk = [&](int t) __attribute__((always_inline)) {
+  // RING: the chunk may hold some of the last FMX_RDS_RING samples (a
+  // separate instantiation: a store there makes the register allocator's
+  // reuse of its address VGPRs cost a vmcnt(0) wait in every chunk)
+  auto chunk = [&](int t, auto ring_c) __attribute__((always_inline)) {
+    constexpr bool RING = decltype(ring_c)::value;
+    t = __builtin_amdgcn_readfirstlane(t); // wave-uniform
     need(t, U);
     const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;
     float ph[U];
@@ -2588,45 +2618,31 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
       ssr += U - 1;
     }
     float xs[U];
-    {
-      // U samples from NSEG 16-B segments, offset o = d & 3 is wave-uniform
-      const int d = t - tb, g = d >> 2, o = d & 3;
-      float v[4 * NSEG];
 #pragma unroll
-      for (int q = 0; q < NSEG; ++q) {
-        const float4 A = *reinterpret_cast<const float4 *>(seg_ptr(cur, g + q));
-        v[4 * q] = A.x;
-        v[4 * q + 1] = A.y;
-        v[4 * q + 2] = A.z;
-        v[4 * q + 3] = A.w;
-      }
-      switch (o) {
-        case 0:
-#pragma unroll
-          for (int u = 0; u < U; ++u) xs[u] = v[u];
-          break;
-        case 1:
-#pragma unroll
-          for (int u = 0; u < U; ++u) xs[u] = v[u + 1];
-          break;
-        case 2:
-#pragma unroll
-          for (int u = 0; u < U; ++u) xs[u] = v[u + 2];
-          break;
-        default:
-#pragma unroll
-          for (int u = 0; u < U; ++u) xs[u] = v[u + 3];
-          break;
-      }
-    }
+    for (int u = 0; u < U; ++u) xs[u] = read1(t + u);
     f32x2 mx[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) mx[u] = mix(xs[u], ph[u]);
+    // accumulator by accumulator, the chunk's samples oldest first: every
+    // partial sum sees the same products in the same order as the
+    // per-sample push (h[jp + 24 i] * mix, jp = 24 - j); the 8 taps of one
+    // accumulator are two broadcast 16-B LDS reads
+    if (RING) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t j = j0 + (uint32_t)u; // 1..24
-      const int jp = (j == FMX_RDS_DECIM) ? 0 : FMX_RDS_DECIM - (int)j;
-      acc_add(mx[u], t + u, &L.taps[jp][0]);
+      for (int u = 0; u < U; ++u) ring_store(mx[u], t + u);
+    }
+    {
+      const int p = (int)(j0 >> 3); // j0 = 1, 9, 17
+#pragma unroll
+      for (int i = 0; i < FMX_RDS_NACC; ++i) {
+        float tu[8];
+        rds_taps8(&L.tT[p][i][0], tu);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const f32x2 pr = f32x2{tu[u], tu[u]} * mx[u];
+          acc[i] = acc[i] + pr;
+        }
+      }
     }
     RDS_STAMP(2)
     if (j0 == (uint32_t)(FMX_RDS_DECIM + 1 - U)) { // the chunk ends on the FIR output
@@ -2648,7 +2664,8 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     const int cend = min(tend, cmin);
     while (t < tend) {
       if (uniform_j && t + U <= cend && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) % (uint32_t)U == 1u) {
-        chunk(t);
+        if (t + U > ring_from) chunk(t, std::true_type{});
+        else chunk(t, std::false_type{});
         t += U;
       } else {
         step_one(t++);
@@ -2658,6 +2675,8 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
     flush_symbols();
     RDS_STAMP(5)
   }
+  // no LDS-DMA may still be in flight when the workgroup's LDS is released
+  rds_wait(0x0F70); // vmcnt(0)
   if (!act) return;
   // ---- registers -> state ----
   FmxRdsState *out = a.st + c;
@@ -2675,7 +2694,8 @@ __global__ __launch_bounds__(64) void k_rds(RdsArgs a) {
   out->agc_g = agc_g;
   out->agc_y2p = agc_y2p;
   for (int m = 0; m < FMX_SS_SUB; ++m) {
-    const f32x2 w = L.win[wp + 1 + m][lane];
+    const int i = wp + 1 + m;
+    const f32x2 w = L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][lane];
     out->ss_win_re[m] = w.x;
     out->ss_win_im[m] = w.y;
   }
@@ -2771,8 +2791,13 @@ __global__ void k_reset(ResetArgs a) {
       s.theta = 0;
       s.dtheta = D->rds_dtheta0;
       s.sample_since_reset = 0;
-      // symsync reset (matched filter bank only)
+      // symsync reset (matched filter bank only): firpfb_crcf_reset clears
+      // the shared MF / dMF window
       s.ss_mf_valid = 0;
+      for (int m = 0; m < FMX_SS_SUB; ++m) {
+        s.ss_win_re[m] = 0.0f;
+        s.ss_win_im[m] = 0.0f;
+      }
       s.ss_rate = 3.0f;
       s.ss_del = 3.0f;
       s.ss_tau = 0.0f;
@@ -3454,11 +3479,14 @@ int launch_pll(const PllArgs &a, void *stream) {
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_rds(const RdsArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  // two k_fe8 workgroups (2 x 60.5 KB) leave 39 KB of a CU's 160 KB: k_rds
+  // fits beside them (as k_pll's 35.5 KB does)
+  static_assert(sizeof(RdsLds) + RDS_RING * 64 * 4 <= 39 * 1024, "k_rds LDS must fit beside two k_fe8 workgroups");
+  hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_reset(const ResetArgs &a, void *stream) {

@@ -83,6 +83,8 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
     """Per-channel comparison stats.  pcm_blocks (optional) restricts the PCM
     and pilot-level statistics to those blocks."""
     mpx_err = 0.0
+    mpx_sq = 0.0
+    mpx_n = 0
     pcm_sq = 0.0
     pcm_n = 0
     pcm_max = 0.0
@@ -94,7 +96,10 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
     g_gpu, g_ora = [], []
     for b in range(nblk):
         o, g = ores[b], gres[b]
-        mpx_err = max(mpx_err, float(np.max(np.abs(o["mpx"] - g["mpx"][c, :len(o["mpx"])]))))
+        dm = o["mpx"] - g["mpx"][c, :len(o["mpx"])]
+        mpx_err = max(mpx_err, float(np.max(np.abs(dm))))
+        mpx_sq += float(np.sum(dm.astype(np.float64) ** 2))
+        mpx_n += dm.size
         k = len(o["pcm_l"])
         if int(g["count"][c]) != k:
             cnt_mismatch += 1
@@ -112,7 +117,7 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
         pcm_max = max(pcm_max, float(np.max(np.abs(dl))) if k else 0.0, float(np.max(np.abs(dr))) if k else 0.0)
         pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
         pil_maxdiff = max(pil_maxdiff, abs(int(o["pilot"]) - int(g["pilot"][c])))
-    return dict(mpx_max=mpx_err, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
+    return dict(mpx_max=mpx_err, mpx_rms=(mpx_sq / max(mpx_n, 1)) ** 0.5, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
                 stereo_mismatch=st_mismatch, indicator_mismatch=ind_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
                 groups_gpu=g_gpu, groups_oracle=g_ora)
 
