@@ -189,8 +189,12 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     for (int p = 0; p < M; ++p)
       for (int q = 0; q < d->dec_tpp; ++q) d->dec_poly[p * d->dec_tpp + q] = d->dec_taps[q * M + p];
     for (int i = 0; i < d->dec_len; ++i) d->dec_pad[FMX_DEC_PAD + i] = d->dec_taps[i];
+    double dc = 0.0;
+    for (int i = 0; i < d->dec_len; ++i) dc += static_cast<double>(d->dec_taps[i]);
+    d->dec_dc = static_cast<float>(127.5 * dc);
   } else {
     d->dec_scale = 1.0f;
+    d->dec_dc = 0.0f;
   }
   // ---- FMDemod IQ filters ----
   for (int i = 0; i < 30; ++i) {

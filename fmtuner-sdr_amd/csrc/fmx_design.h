@@ -38,6 +38,9 @@ typedef struct {
   // by the u8 normalisation 1/127.5, plus the firdecim scale 2*fc.
   int dec_len, dec_tpp;
   float dec_scale;
+  // 127.5 * sum(dec_taps): the u8 decimators run the FIR on the raw bytes
+  // and subtract this once per output (instead of 127.5 from every sample)
+  float dec_dc;
   float dec_taps[FMX_MAX_DEC];
   float dec_taps_raw[FMX_MAX_DEC];
   float dec_poly[FMX_MAX_DEC]; // [p][q] = dec_taps[q*M + p]  (phase-major)

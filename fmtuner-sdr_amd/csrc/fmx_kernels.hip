@@ -135,7 +135,9 @@ __device__ __forceinline__ void fe_decimate(const __half2 *inq, int Q, const flo
 // s = 0.. of the window origin n0*M - L, 2 bytes each; outputs j = 3*tid + r
 // need s in [j*M + 1, j*M + L].  Thread t reads dwords (3M/2)*t + e: for
 // M = 10 the stride is 15 dwords, conflict-free.  hpad = dec_pad (+PAD);
-// (I, Q) pairs go through packed FP32 FMAs.
+// (I, Q) pairs go through packed FP32 FMAs on the raw byte values; the
+// caller subtracts D->dec_dc = 127.5 * sum(h) per output (the reference's
+// per-sample (v - 127.5) offset, factored out of the dot product).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int M, int TPP>
 __device__ __forceinline__ void fe_decimate_u8(const uint8_t *raw, const float *__restrict__ hpad, int tid,
@@ -143,7 +145,6 @@ __device__ __forceinline__ void fe_decimate_u8(const uint8_t *raw, const float *
   constexpr int L = M * TPP;
   constexpr int NB = TPP + 3;  // blocks of M samples covering s in [0, 2M + L]
   const uint32_t *rw = reinterpret_cast<const uint32_t *>(raw) + (3 * M / 2) * tid;
-  const f32x2 off = {-127.5f, -127.5f};
 #pragma unroll
   for (int r = 0; r < 3; ++r) acc[r] = f32x2{0.0f, 0.0f};
 #pragma unroll 1
@@ -159,7 +160,6 @@ __device__ __forceinline__ void fe_decimate_u8(const uint8_t *raw, const float *
       const int sh0 = (u & 1) ? 16 : 0;  // v_cvt_f32_ubyte{0..3}
       x.x = (float)((ww >> sh0) & 255u);
       x.y = (float)((ww >> (sh0 + 8)) & 255u);
-      x = x + off;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const float h = hq[r * M - u];
@@ -345,12 +345,13 @@ __device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i
 // RF level accumulators of the raw u8 IQ (computeSignalLevel,
 // signal_level.cpp:145-204): exact integer sums, clip counts per sample.
 struct SigAcc {
+  // sQ and sQQ are kept as sI + sQ and sII + sQQ (one byte dot product each)
   uint32_t sI = 0, sQ = 0, sII = 0, sQQ = 0, hard = 0, nearc = 0;
   __device__ __forceinline__ void sample(uint32_t i, uint32_t q) {
     sI += i;
-    sQ += q;
+    sQ += i + q;
     sII += i * i;
-    sQQ += q * q;
+    sQQ += i * i + q * q;
     const uint32_t lo = min(i, q), hi = max(i, q);
     hard += (lo <= 1u || hi >= 254u) ? 1u : 0u;
     nearc += (lo <= 8u || hi >= 247u) ? 1u : 0u;
@@ -362,23 +363,41 @@ struct SigAcc {
   }
   // bytes I0 Q0 I1 Q1: the four sums by byte dot products; the clip counters
   // only when some byte is <= 8 or >= 247 (fmx_word_near_clip)
-  __device__ __forceinline__ void word(uint32_t w) {
+  __device__ __forceinline__ void sums(uint32_t w) {
     sI = __builtin_amdgcn_udot4(w, 0x00010001u, sI, false);
-    sQ = __builtin_amdgcn_udot4(w, 0x01000100u, sQ, false);
+    sQ = __builtin_amdgcn_udot4(w, 0x01010101u, sQ, false);
     sII = __builtin_amdgcn_udot4(w & 0x00FF00FFu, w, sII, false);
-    sQQ = __builtin_amdgcn_udot4(w & 0xFF00FF00u, w, sQQ, false);
-    if (fmx_word_near_clip(w)) {
-      flags(w & 255u, (w >> 8) & 255u);
-      flags((w >> 16) & 255u, w >> 24);
+    sQQ = __builtin_amdgcn_udot4(w, w, sQQ, false);
+  }
+  // 16 bytes (8 IQ samples): the near-clip pre-test of the four words ORed,
+  // one branch per 16 B
+  template <typename V4> __device__ __forceinline__ void word4(const V4 &w) {
+    sums(w.x);
+    sums(w.y);
+    sums(w.z);
+    sums(w.w);
+    if (fmx_word_near_clip(w.x) | fmx_word_near_clip(w.y) | fmx_word_near_clip(w.z) | fmx_word_near_clip(w.w)) {
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        flags(ww[k] & 255u, (ww[k] >> 8) & 255u);
+        flags((ww[k] >> 16) & 255u, ww[k] >> 24);
+      }
     }
+  }
+  // the separate sums back from the combined ones
+  __device__ __forceinline__ void finish() {
+    sQ -= sI;
+    sQQ -= sII;
   }
 };
 
 // RF-level epilogue of a frontend workgroup (computeSignalLevel +
 // smoothSignalLevel, signal_level.cpp:145-214): block-reduce the exact byte
 // sums, then thread 0 evaluates the reference's formulas in double.
-__device__ __forceinline__ void fe_signal_level(const FeArgs &a, const SigAcc &sig, unsigned long long *sgp, int c,
+__device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, unsigned long long *sgp, int c,
                                                 long samples, int lane, int wave, int tid) {
+  sig.finish();
   unsigned long long v[6] = {sig.sI, sig.sQ, sig.sII, sig.sQQ, sig.hard, sig.nearc};
 #pragma unroll
   for (int k = 0; k < 6; ++k)
@@ -584,10 +603,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         if (off < LY::HB + 2 * FE_T * M && (n0 > 0 || off >= LY::HB))
           *reinterpret_cast<u32x4 *>(raw + off) = pf[j];
         if (want_sig && off >= LY::HB && off < LY::HB + 2 * cnt * M) {
-          sig.word(pf[j].x);
-          sig.word(pf[j].y);
-          sig.word(pf[j].z);
-          sig.word(pf[j].w);
+          sig.word4(pf[j]);
         }
       }
       if (n0 == 0) {  // halo = the carried history (dec_valid == L-1 here)
@@ -608,8 +624,8 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       for (int r = 0; r < 3; ++r) {
         const int j = 3 * tid + r;
         if (j < cnt) {
-          const float yr = acc[r].x * D->dec_scale;
-          const float yi = acc[r].y * D->dec_scale;
+          const float yr = (acc[r].x - D->dec_dc) * D->dec_scale;
+          const float yi = (acc[r].y - D->dec_dc) * D->dec_scale;
           if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
           xin[FE_HALO_IQ + j] = make_float2(yr, yi);
           if (a.bb_out) {
@@ -3113,10 +3129,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         const int off = 16 * (tid + 256 * j);
         if (off >= LY::HB && off < LY::HB + 2 * FE8_T * M) {
           const u32x4 w = *reinterpret_cast<const u32x4 *>(raw + off);
-          sig.word(w.x);
-          sig.word(w.y);
-          sig.word(w.z);
-          sig.word(w.w);
+          sig.word4(w);
         }
       }
     }
@@ -3129,7 +3142,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
       const u32x4 *rw = reinterpret_cast<const u32x4 *>(raw) + M * tid;
       const FMX_CONST float *hd = cptr(D->dec_taps);
-      const f32x2 off = {-127.5f, -127.5f};
       // one group of 8 samples: live (s, r) pairs known at compile time
       // (head / tail of the window), or all live (middle, runtime loop with
       // the tap base in SGPRs)
@@ -3153,9 +3165,9 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           const uint32_t wd = ww[u >> 1];
           const int sh0 = (u & 1) ? 16 : 0;
           f32x2 x;
+          // raw byte values: 127.5 * sum(h) comes off once per output below
           x.x = (float)((wd >> sh0) & 255u);
           x.y = (float)((wd >> (sh0 + 8)) & 255u);
-          x = x + off;
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
             if (known) {
@@ -3178,8 +3190,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       int myclip = 0;
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const float yr = acc[r].x * D->dec_scale;
-        const float yi = acc[r].y * D->dec_scale;
+        const float yr = (acc[r].x - D->dec_dc) * D->dec_scale;
+        const float yi = (acc[r].y - D->dec_dc) * D->dec_scale;
         if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
         xv[r] = make_float2(yr, yi);
       }
