@@ -10,6 +10,7 @@
 #include "fmx_blocks.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <stdexcept>
 #include <string>
 
@@ -79,12 +80,6 @@ public:
   size_t cap[6] = {0, 0, 0, 0, 0, 0};
 };
 
-static int deemph_code(int tau_us) {
-  if (tau_us <= 0) return FMX_DEEMPH_OFF;
-  if (tau_us == 50) return FMX_DEEMPH_50US;
-  if (tau_us == 75) return FMX_DEEMPH_75US;
-  throw std::invalid_argument("fmx: de-emphasis must be 50 or 75 us (or <= 0 for off)");
-}
 
 }  // namespace detail
 
@@ -113,7 +108,7 @@ void ComplexDecimator::reset() {
 }
 
 std::size_t ComplexDecimator::executeComplex(const uint8_t *iqIn, std::size_t inSamples, std::complex<float> *iqOut,
-                                             std::size_t outCapacity) {
+                                             std::size_t outCapacity) const {
   if (!iqIn || !iqOut || inSamples == 0 || outCapacity == 0 || !slot_) return 0;
   const std::size_t blocks = std::min(inSamples / factor_, outCapacity);
   std::size_t done = 0;
@@ -127,6 +122,26 @@ std::size_t ComplexDecimator::executeComplex(const uint8_t *iqIn, std::size_t in
                               2 * n),
                  "fmx_decimate");
     slot_->down(iqOut + done, d_out, 8 * static_cast<size_t>(n));
+    done += static_cast<std::size_t>(n);
+  }
+  return blocks;
+}
+
+std::size_t ComplexDecimator::execute(const uint8_t *iqIn, std::size_t inSamples, uint8_t *iqOut,
+                                      std::size_t outCapacity) const {
+  if (!iqIn || !iqOut || inSamples == 0 || outCapacity == 0 || !slot_) return 0;
+  const std::size_t blocks = std::min(inSamples / factor_, outCapacity);
+  std::size_t done = 0;
+  while (done < blocks) {
+    const int n = static_cast<int>(std::min<std::size_t>(blocks - done, kSlotBlock));
+    const size_t in_bytes = 2 * static_cast<size_t>(n) * factor_;
+    void *d_in = slot_->dev(0, in_bytes);
+    void *d_out = slot_->dev(1, 2 * static_cast<size_t>(n));
+    slot_->up(d_in, iqIn + 2 * done * factor_, in_bytes);
+    slot_->check(fmx_decimate_u8(slot_->h, static_cast<const uint8_t *>(d_in), in_bytes, n,
+                                 static_cast<uint8_t *>(d_out), 2 * static_cast<size_t>(n)),
+                 "fmx_decimate_u8");
+    slot_->down(iqOut + 2 * done, d_out, 2 * static_cast<size_t>(n));
     done += static_cast<std::size_t>(n);
   }
   return blocks;
@@ -210,10 +225,27 @@ std::size_t FMDemod::downsampleAudio(const float *demod, float *audio, std::size
   return out;
 }
 
+void FMDemod::process(const uint8_t *iq, float *audio, std::size_t numSamples) {
+  // demodulate + downsampleAudio: the MPX goes to a scratch, the audio out
+  if (!iq || !audio || numSamples == 0) return;
+  scratch_.resize(numSamples);
+  lastAudio_ = processSplit(iq, scratch_.data(), audio, numSamples);
+}
+void FMDemod::processComplex(const std::complex<float> *iq, float *audio, std::size_t numSamples) {
+  if (!iq || !audio || numSamples == 0) return;
+  scratch_.resize(numSamples);
+  lastAudio_ = processSplitComplex(iq, scratch_.data(), audio, numSamples);
+}
+void FMDemod::processNoDownsample(const uint8_t *iq, float *audio, std::size_t numSamples) {
+  if (!iq || !audio || numSamples == 0) return;
+  processSplit(iq, audio, nullptr, numSamples);
+}
 void FMDemod::reset() { slot_->reset(); }
-void FMDemod::setDeemphasis(int tau_us) { slot_->set(FMX_PARAM_DEEMPHASIS, detail::deemph_code(tau_us)); }
+void FMDemod::setDeemphasis(int tau_us) { slot_->set(FMX_PARAM_DEEMPH_US, tau_us); }
 void FMDemod::setDeviation(double deviation) {
-  if (deviation != 75000.0) throw std::invalid_argument("fmx: FMDemod deviation is fixed at 75 kHz");
+  const double hz = std::floor(deviation + 0.5);
+  if (!(hz >= 1.0 && hz <= 1e9)) throw std::invalid_argument("fmx: FMDemod deviation must be 1 Hz .. 1 GHz");
+  slot_->set(FMX_PARAM_DEVIATION_HZ, static_cast<int>(hz));
 }
 void FMDemod::setBandwidthMode(int mode) { slot_->set(FMX_PARAM_BANDWIDTH_MODE, mode); }
 void FMDemod::setBandwidthHz(int bwHz) { slot_->set(FMX_PARAM_BANDWIDTH_HZ, bwHz); }
@@ -259,7 +291,7 @@ AFPostProcessor::AFPostProcessor(int inputRate, int outputRate)
 }
 AFPostProcessor::~AFPostProcessor() = default;
 void AFPostProcessor::reset() { slot_->reset(); }
-void AFPostProcessor::setDeemphasis(int tau_us) { slot_->set(FMX_PARAM_DEEMPHASIS, detail::deemph_code(tau_us)); }
+void AFPostProcessor::setDeemphasis(int tau_us) { slot_->set(FMX_PARAM_DEEMPH_US, tau_us); }
 
 std::size_t AFPostProcessor::process(const float *inL, const float *inR, std::size_t inSamples, float *outL,
                                      float *outR, std::size_t outCapacity) {

@@ -91,6 +91,7 @@ struct Handle {
   int *reset_mask = nullptr;
   std::vector<int> hmask;
   int *mute = nullptr; // [C][2] retune fade/mute {remaining, total} (main.cpp:1310-1337)
+  float *dec_scratch = nullptr; // [C][2 * block] complex, fmx_decimate_u8 (allocated on first use)
   // intermediates (double-buffered by step parity)
   float *mpx[FMX_NBUF] = {}, *pilot[FMX_NBUF] = {}, *rds_in[FMX_NBUF] = {};
   int *rds_count[FMX_NBUF] = {};
@@ -378,6 +379,29 @@ static void set_bandwidth(Handle *h, int c, int bw) { // fm_demod.cpp:168-204
 static void set_deemph(Handle *h, int c, int code) { // main.cpp:699-708 -> both objects
   h->hpar[static_cast<size_t>(c)].deemph = code;
   if (code != FMX_DEEMPH_OFF) h->hmask[static_cast<size_t>(c)] |= RS_DEEMPH;
+  h->par_dirty = true;
+}
+// setDeemphasis(tau_us) with any tau (fm_demod.cpp:50-62, af_post_processor.cpp:31-45):
+// tau <= 0 disables it (filter state kept), else alpha = dt / (tau + dt) in
+// float and the IIR re-created
+static void set_deemph_us(Handle *h, int c, int tau_us) {
+  FmxChanParam &p = h->hpar[static_cast<size_t>(c)];
+  if (tau_us <= 0) {
+    p.deemph = FMX_DEEMPH_OFF;
+  } else {
+    const float tau = static_cast<float>(tau_us) * 1e-6f;
+    const float dt = 1.0f / static_cast<float>(h->cfg.out_rate);
+    p.deemph = 3;
+    p.deemph_alpha = dt / (tau + dt);
+    h->hmask[static_cast<size_t>(c)] |= RS_DEEMPH;
+  }
+  h->par_dirty = true;
+}
+// setDeviation: kf = (float)(deviation / Fs), freqdem re-created (r_prev = 0)
+static void set_deviation(Handle *h, int c, int hz) {
+  const float kf = static_cast<float>(static_cast<double>(hz) / static_cast<double>(h->hdes->fs));
+  h->hpar[static_cast<size_t>(c)].fd_ref = static_cast<float>(1.0 / (2.0 * 3.14159265358979323846 * static_cast<double>(kf)));
+  h->hmask[static_cast<size_t>(c)] |= RS_FREQDEM;
   h->par_dirty = true;
 }
 static void set_agc(Handle *h, int c, int mode) { // fm_demod.cpp:210-217
@@ -940,6 +964,14 @@ int fmx_set_param(void *handle, int channel, int key, int value) {
       case FMX_PARAM_BANDWIDTH_MODE: set_bandwidth(h, c, tef_bandwidth_hz(value)); break;
       case FMX_PARAM_W0_HZ: h->w0[static_cast<size_t>(c)] = std::clamp(value, 0, 400000); break;
       case FMX_PARAM_DEEMPHASIS: set_deemph(h, c, std::clamp(value, 0, 2)); break;
+      case FMX_PARAM_DEEMPH_US: set_deemph_us(h, c, value); break;
+      case FMX_PARAM_DEVIATION_HZ:
+        if (value <= 0) {
+          h->err = "deviation must be > 0 Hz";
+          return FMX_E_INVALID;
+        }
+        set_deviation(h, c, value);
+        break;
       case FMX_PARAM_DSP_AGC: set_agc(h, c, std::clamp(value, 0, 2)); break;
       case FMX_PARAM_BLEND:
         p.blend = std::clamp(value, 0, 2);
@@ -1017,6 +1049,20 @@ int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out,
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) return rc;
     dec_advance(h, n_out);
   }
+  return stage_end(h);
+}
+
+int fmx_decimate_u8(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, uint8_t *d_out,
+                    size_t out_stride) {
+  Handle *h = H(handle);
+  if (!h || !d_out) return FMX_E_INVALID;
+  int rc;
+  if ((rc = check_n(h, n_out)) != FMX_OK) return rc;
+  if (!h->dec_scratch && (rc = dalloc(h, &h->dec_scratch, static_cast<size_t>(h->C) * 2 * h->cfg.block)) != FMX_OK)
+    return rc;
+  if ((rc = fmx_decimate(handle, d_iq, iq_stride, n_out, h->dec_scratch, 2 * h->cfg.block)) != FMX_OK) return rc;
+  if ((rc = launch_iq_to_u8(h->dec_scratch, 2 * h->cfg.block, h->C, n_out, d_out, out_stride, h->sA)) != FMX_OK)
+    return rc;
   return stage_end(h);
 }
 

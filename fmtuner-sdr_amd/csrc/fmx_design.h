@@ -93,8 +93,9 @@ typedef struct {
   int blend;       // 0 soft, 1 normal, 2 aggressive
   int force_mono;
   int force_stereo;
-  int deemph;      // 0 -> 50us, 1 -> 75us, 2 -> off
-  int pad0, pad1;
+  int deemph;      // 0 -> 50us, 1 -> 75us, 2 -> off, 3 -> deemph_alpha (setDeemphasis(tau_us))
+  float deemph_alpha; // dt / (tau + dt) of a custom tau (fm_demod.cpp:50-62, af_post_processor.cpp:31-45)
+  float fd_ref;       // 1 / (2 pi kf) of a custom deviation (fm_demod.cpp:64-71); 0 = the design's 75 kHz
 } FmxChanParam;
 
 // StereoDecoder scalars (stereo_decoder.h:27-50)

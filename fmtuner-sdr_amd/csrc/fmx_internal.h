@@ -179,9 +179,11 @@ enum ResetParts {
   RS_IQFIR = 64,   // IQ FIR re-created (setBandwidthHz)
   RS_DEEMPH = 128, // de-emphasis IIRs re-created (setDeemphasis)
   RS_CREATE = 256, // object construction (everything, incl. RDS resampler/AGC)
-  RS_MUTE = 512    // retune fade/mute start; mute length in bits 16..31 (main.cpp:1034-1035)
+  RS_MUTE = 512,   // retune fade/mute start; mute length in bits 16..31 (main.cpp:1034-1035)
+  RS_FREQDEM = 1024 // discriminator re-created (FMDemod::setDeviation)
 };
 int launch_reset(const ResetArgs &a, void *stream);
+int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, size_t out_stride, void *stream);
 
 } // namespace fmx
 

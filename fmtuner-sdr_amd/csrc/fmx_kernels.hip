@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       }
       FE_STAMP(2)
       // ================= discriminator =================
-      const float ref = D->fd_ref;
+      const float ref = (par.fd_ref != 0.0f) ? par.fd_ref : D->fd_ref; // freqdem 1 / (2 pi kf)
       for (int j = tid; j < cnt; j += 256) {
         const float2 p = yb[j], r = yb[1 + j];
         const float re = p.x * r.x + p.y * r.y;
@@ -1719,7 +1719,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const bool af = (a.mode != 4);
   const bool pipe_mono = (a.mode == 3);
   const int deemph = par.deemph;
-  const float dalpha = (deemph == 0) ? D->deemph_alpha[0] : D->deemph_alpha[1];
+  const float dalpha = (deemph == 0) ? D->deemph_alpha[0] : ((deemph == 1) ? D->deemph_alpha[1] : par.deemph_alpha);
   const bool de_on = deemph != 2;
   const float dc_alpha = mono ? 0.0008f : 0.005f;
   const float de_a1 = -(1.0f - dalpha);
@@ -2751,6 +2751,12 @@ __global__ void k_reset(ResetArgs a) {
     for (int h = tid; h < FMX_IQ_MAXLEN - 1; h += blockDim.x)
       a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{0.0f, 0.0f};
   }
+  if (m & RS_FREQDEM) { // freqdem re-created (setDeviation): r_prev = 0
+    if (tid == 0) {
+      a.fd_prev[2 * c] = 0.0f;
+      a.fd_prev[2 * c + 1] = 0.0f;
+    }
+  }
   if (create || (m & RS_DEMOD)) {
     if (tid == 0) {
       a.dc_v[2 * c] = 0.0f;
@@ -2852,6 +2858,20 @@ __global__ void k_reset(ResetArgs a) {
     a.mute[2 * c] = len;
     a.mute[2 * c + 1] = len;
   }
+}
+
+/* ComplexDecimator::execute's requantisation (liquid_primitives.cpp:448-452):
+ * clamp(y * 127.5 + 127.5, 0, 255) truncated to u8, for C rows of n complex
+ * outputs (separate multiply and add: the file builds with fp-contract off) */
+__global__ void k_iq_to_u8(const float *in, int in_stride, int n, uint8_t *out, size_t out_stride) {
+  const int c = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float yr = in[(size_t)c * in_stride + 2 * i], yi = in[(size_t)c * in_stride + 2 * i + 1];
+  const float ir = d_clamp((yr * 127.5f) + 127.5f, 0.0f, 255.0f);
+  const float qr = d_clamp((yi * 127.5f) + 127.5f, 0.0f, 255.0f);
+  out[(size_t)c * out_stride + 2 * i] = (uint8_t)ir;
+  out[(size_t)c * out_stride + 2 * i + 1] = (uint8_t)qr;
 }
 
 /* ================================================================== */
@@ -3284,7 +3304,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     // ================= discriminator =================
     float mv[8];
     {
-      const float ref = D->fd_ref;
+      const float ref = (par.fd_ref != 0.0f) ? par.fd_ref : D->fd_ref; // freqdem 1 / (2 pi kf)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int j = tid + 256 * k;
@@ -3499,6 +3519,12 @@ int launch_rds(const RdsArgs &a, void *stream) {
   // fits beside them (as k_pll's 35.5 KB does)
   static_assert(sizeof(RdsLds) + RDS_RING * 64 * 4 <= 39 * 1024, "k_rds LDS must fit beside two k_fe8 workgroups");
   hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, size_t out_stride, void *stream) {
+  if (C <= 0 || n <= 0) return FMX_OK;
+  hipLaunchKernelGGL(k_iq_to_u8, dim3((n + 255) / 256, C), dim3(256), 0, static_cast<hipStream_t>(stream), in,
+                     in_stride, n, out, out_stride);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_reset(const ResetArgs &a, void *stream) {

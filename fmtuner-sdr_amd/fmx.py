@@ -16,7 +16,7 @@ FMX_AGC_OFF, FMX_AGC_FAST, FMX_AGC_SLOW = 0, 1, 2
 FMX_BLEND_SOFT, FMX_BLEND_NORMAL, FMX_BLEND_AGGRESSIVE = 0, 1, 2
 FMX_DEEMPH_50US, FMX_DEEMPH_75US, FMX_DEEMPH_OFF = 0, 1, 2
 PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
-             force_mono=6, force_stereo=7, bandwidth_mode=8)
+             force_mono=6, force_stereo=7, bandwidth_mode=8, deemph_us=9, deviation_hz=10)
 K_FRONTEND, K_STEREO, K_AUDIO, K_RDS = 0, 1, 2, 3
 KERNEL_NAMES = ["frontend", "stereo", "audio", "rds"]
 
@@ -88,6 +88,7 @@ def lib():
         "fmx_set_signal_params": (i, [vp, i, i, C.c_double, C.c_double, C.c_double, C.c_double]),
         "fmx_process_block": (i, [vp, vp, sz, i, C.POINTER(BlockOut)]),
         "fmx_decimate": (i, [vp, vp, sz, i, vp, i]),
+        "fmx_decimate_u8": (i, [vp, vp, sz, i, vp, sz]),
         "fmx_demod": (i, [vp, vp, i, i, vp, i, vp, i, vp]),
         "fmx_stereo": (i, [vp, vp, i, i, vp, vp, i, vp, vp]),
         "fmx_afpost": (i, [vp, vp, vp, i, i, vp, vp, i, i, vp]),
@@ -195,6 +196,10 @@ class Handle:
     def decimate(self, d_iq, iq_stride, n_out, d_out, out_stride):
         self._ck(self.L.fmx_decimate(self.h, C.c_void_p(d_iq), iq_stride, n_out,
                                      C.c_void_p(d_out), out_stride), "fmx_decimate")
+
+    def decimate_u8(self, d_iq, iq_stride, n_out, d_out, out_stride):
+        self._ck(self.L.fmx_decimate_u8(self.h, C.c_void_p(d_iq), iq_stride, n_out,
+                                        C.c_void_p(d_out), out_stride), "fmx_decimate_u8")
 
     def demod(self, d_iq, in_stride, n, d_mpx, mpx_stride, d_mono=None, mono_stride=0, d_count=None):
         self._ck(self.L.fmx_demod(self.h, C.c_void_p(d_iq), in_stride, n, C.c_void_p(d_mpx), mpx_stride,

@@ -141,7 +141,10 @@ enum {
   FMX_PARAM_BLEND = 5,         /* StereoDecoder::setBlendMode                  */
   FMX_PARAM_FORCE_MONO = 6,    /* StereoDecoder::setForceMono                  */
   FMX_PARAM_FORCE_STEREO = 7,  /* StereoDecoder::setForceStereo                */
-  FMX_PARAM_BANDWIDTH_MODE = 8 /* FMDemod::setBandwidthMode (TEF table)        */
+  FMX_PARAM_BANDWIDTH_MODE = 8, /* FMDemod::setBandwidthMode (TEF table)       */
+  FMX_PARAM_DEEMPH_US = 9,     /* setDeemphasis(tau_us) of FMDemod + AFPostProcessor,
+                                  any tau; <= 0 switches it off (fm_demod.cpp:50-62) */
+  FMX_PARAM_DEVIATION_HZ = 10  /* FMDemod::setDeviation(Hz) (fm_demod.cpp:64-71)  */
 };
 int fmx_set_param(void *handle, int channel, int key, int value);
 /* computeSignalLevel's arguments (main.cpp:1166-1170): applied tuner gain
@@ -162,6 +165,11 @@ int fmx_process_block(void *handle, const uint8_t *d_iq, size_t iq_stride, int n
 /* ComplexDecimator::executeComplex: d_out [C][out_stride] complex float */
 int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, float *d_out,
                  int out_stride);
+/* ComplexDecimator::execute (liquid_primitives.cpp:422-459): the same
+ * decimation, requantised to interleaved u8 (clamp(y*127.5 + 127.5) -> u8);
+ * d_out [C][out_stride] bytes, 2 per output sample */
+int fmx_decimate_u8(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, uint8_t *d_out,
+                    size_t out_stride);
 /* FMDemod::processSplitComplex(iq, mpx, mono, n): d_iq_cf complex float
  * [C][in_stride]; d_mono may be NULL (stereo mode: returns 0 samples). */
 int fmx_demod(void *handle, const float *d_iq_cf, int in_stride, int n, float *d_mpx, int mpx_stride,

@@ -18,9 +18,9 @@
 // for new code is fmx::Receiver (a thin owner of fmx_process_block).
 //
 // Error behaviour follows the reference: construction / design failures
-// throw std::runtime_error, null or empty inputs return 0, and settings the
-// GPU build does not implement (arbitrary de-emphasis constants, deviation
-// other than 75 kHz) throw std::invalid_argument instead of silently
+// throw std::runtime_error and null or empty inputs return 0.  Settings the
+// GPU build does not implement (ComplexDecimator designs other than the ones
+// main.cpp creates) throw std::invalid_argument instead of silently
 // differing.  There is no CPU fallback: without a GPU the constructors throw.
 #ifndef FMX_BLOCKS_HPP
 #define FMX_BLOCKS_HPP
@@ -52,9 +52,13 @@ public:
   void init(std::uint32_t factor, std::uint32_t tapsPerPhase = 12, float stopBandAtten = 70.0f);
   void reset();
   // Like the reference: min(inSamples / factor, outCapacity) outputs; a
-  // remainder of inSamples % factor samples is dropped, not buffered.
+  // remainder of inSamples % factor samples is dropped, not buffered.  const
+  // as in the reference (the filter state lives in the device handle).
   std::size_t executeComplex(const uint8_t *iqIn, std::size_t inSamples, std::complex<float> *iqOut,
-                             std::size_t outCapacity);
+                             std::size_t outCapacity) const;
+  // u8 -> u8: the same decimation requantised to interleaved bytes
+  // (liquid_primitives.cpp:422-459)
+  std::size_t execute(const uint8_t *iqIn, std::size_t inSamples, uint8_t *iqOut, std::size_t outCapacity) const;
   bool ready() const { return slot_ != nullptr; }
   std::uint32_t factor() const { return factor_; }
 
@@ -69,6 +73,13 @@ public:
   FMDemod(int inputRate, int outputRate);
   ~FMDemod();
 
+  // demodulate + downsampleAudio into audio (fm_demod.cpp:228-243); the
+  // reference returns nothing, the 32 kHz count is getLastAudioCount()
+  void process(const uint8_t *iq, float *audio, std::size_t numSamples);
+  void processComplex(const std::complex<float> *iq, float *audio, std::size_t numSamples);
+  // discriminator MPX only (fm_demod.cpp:276-279)
+  void processNoDownsample(const uint8_t *iq, float *audio, std::size_t numSamples);
+  std::size_t getLastAudioCount() const { return lastAudio_; }
   // mpxOut: n discriminator samples; monoOut (may be null): 32 kHz audio
   // (downsampleAudio of the MPX); returns the mono sample count.
   std::size_t processSplit(const uint8_t *iq, float *mpxOut, float *monoOut, std::size_t n);
@@ -76,8 +87,8 @@ public:
   std::size_t downsampleAudio(const float *demod, float *audio, std::size_t numSamples);
   void reset();
 
-  void setDeemphasis(int tau_us);   // 50, 75 or <= 0 (off)
-  void setDeviation(double deviation);  // 75000 only
+  void setDeemphasis(int tau_us);       // any tau, <= 0 = off (fm_demod.cpp:50-62)
+  void setDeviation(double deviation);  // Hz, rounded to an integer (fm_demod.cpp:64-71)
   void setBandwidthMode(int mode);
   void setBandwidthHz(int bwHz);
   void setW0BandwidthHz(int bwHz);
@@ -90,6 +101,8 @@ private:
   int inputRate_, outputRate_;
   bool clipping_ = false;
   float clipRatio_ = 0.0f;
+  std::size_t lastAudio_ = 0;
+  std::vector<float> scratch_;
 };
 
 class StereoDecoder {
@@ -118,7 +131,7 @@ public:
   ~AFPostProcessor();
 
   void reset();
-  void setDeemphasis(int tau_us);  // 50, 75 or <= 0 (off)
+  void setDeemphasis(int tau_us);  // any tau, <= 0 = off (af_post_processor.cpp:31-45)
   std::size_t process(const float *inL, const float *inR, std::size_t inSamples, float *outL, float *outR,
                       std::size_t outCapacity);
 

@@ -612,6 +612,24 @@ struct ComplexDecimator {
     }
     return blocks;
   }
+  // execute: u8 -> u8 requantised (liquid_primitives.cpp:422-459)
+  size_t execute(const uint8_t *in, size_t inSamples, uint8_t *out, size_t cap) {
+    if (!in || !out || inSamples == 0 || cap == 0) return 0;
+    if (factor == 1) {
+      size_t n = std::min(inSamples, cap);
+      std::copy_n(in, n * 2, out);
+      return n;
+    }
+    std::vector<cf> y(std::min(inSamples / factor, cap));
+    const size_t blocks = executeComplex(in, inSamples, y.data(), y.size());
+    for (size_t b = 0; b < blocks; ++b) {
+      const float iOut = std::clamp((y[b].real() * 127.5f) + 127.5f, 0.0f, 255.0f);
+      const float qOut = std::clamp((y[b].imag() * 127.5f) + 127.5f, 0.0f, 255.0f);
+      out[2 * b] = static_cast<uint8_t>(iOut);
+      out[2 * b + 1] = static_cast<uint8_t>(qOut);
+    }
+    return blocks;
+  }
 };
 
 /* liquid_primitives FIRFilter::init(length, cutoff, As, center) :62-113 */
@@ -1630,6 +1648,11 @@ void oracle_pipeline_set(void *pp, int key, int v) {
     case 6: p->stereo.forceMono = v != 0; break;
     case 7: p->stereo.forceStereo = v != 0; break;
     case 8: p->demod.setBandwidthMode(v); break;
+    case 9:  // setDeemphasis(tau_us) on both objects
+      p->af.setDeemphasis(v);
+      p->demod.setDeemphasis(v);
+      break;
+    case 10: p->demod.setDeviation(static_cast<double>(v)); break;
     default: break;
   }
 }
@@ -1671,6 +1694,9 @@ void oracle_decim_destroy(void *p) { delete static_cast<ref::ComplexDecimator *>
 void oracle_decim_reset(void *p) { static_cast<ref::ComplexDecimator *>(p)->reset(); }
 size_t oracle_decim_execute_complex(void *p, const uint8_t *iq, size_t n, float *out, size_t cap) {
   return static_cast<ref::ComplexDecimator *>(p)->executeComplex(iq, n, reinterpret_cast<cf *>(out), cap);
+}
+size_t oracle_decim_execute(void *p, const uint8_t *iq, size_t n, uint8_t *out, size_t cap) {
+  return static_cast<ref::ComplexDecimator *>(p)->execute(iq, n, out, cap);
 }
 
 void *oracle_demod_create(int in, int out) { return new ref::FMDemod(in, out); }

@@ -84,6 +84,8 @@ void oracle_decim_destroy(void *p);
 void oracle_decim_reset(void *p);
 size_t oracle_decim_execute_complex(void *p, const uint8_t *iq, size_t in_samples,
                                     float *out_cf, size_t out_cap);
+size_t oracle_decim_execute(void *p, const uint8_t *iq, size_t in_samples, uint8_t *out_u8,
+                            size_t out_cap);
 
 void *oracle_demod_create(int input_rate, int output_rate);
 void oracle_demod_destroy(void *p);

@@ -55,6 +55,7 @@ def lib():
             "oracle_decim_destroy": (None, [vp]),
             "oracle_decim_reset": (None, [vp]),
             "oracle_decim_execute_complex": (sz, [vp, vp, sz, vp, sz]),
+            "oracle_decim_execute": (sz, [vp, vp, sz, vp, sz]),
             "oracle_demod_create": (vp, [i, i]),
             "oracle_demod_destroy": (None, [vp]),
             "oracle_demod_reset": (None, [vp]),
@@ -150,7 +151,7 @@ class Pipeline:
         self.L.oracle_pipeline_retune(self.p, mute_samples)
 
     PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
-                 force_mono=6, force_stereo=7, bandwidth_mode=8)
+                 force_mono=6, force_stereo=7, bandwidth_mode=8, deemph_us=9, deviation_hz=10)
 
     def set_param(self, key, value):
         k = self.PARAM[key] if isinstance(key, str) else key

@@ -2,7 +2,9 @@
 // against the oracle's reference objects on the same synthetic IQ.
 // Run on a GPU by tests/test_facades.py; prints one line per check and
 // exits non-zero on failure.  Tolerances as tests/test_gpu_parity.py.
+#include <algorithm>
 #include <cmath>
+#include <stdexcept>
 #include <complex>
 #include <cstdio>
 #include <cstdlib>
@@ -145,16 +147,120 @@ int main() {
     expect(go.size() >= 2, "RDSDecoder decoded groups", (double)go.size());
     oracle_rds_destroy(orr);
   }
-  // ---- unsupported settings fail loudly ----
+  // ---- ComplexDecimator::execute: u8 -> u8 requantised (liquid_primitives.cpp:422-459) ----
+  {
+    fmx::ComplexDecimator dec;
+    dec.init(M, 28, 80.0f);
+    void *od = oracle_decim_create(M, 28, 80.0f);
+    std::vector<uint8_t> of(2 * NS), oo(2 * NS);
+    const size_t nf = dec.execute(iq.data(), NS * M, of.data(), NS);
+    const size_t no = oracle_decim_execute(od, iq.data(), NS * M, oo.data(), NS);
+    int maxdiff = 0;
+    size_t differ = 0;
+    for (size_t i = 0; i < 2 * no; ++i) {
+      const int d = std::abs((int)of[i] - (int)oo[i]);
+      maxdiff = std::max(maxdiff, d);
+      differ += d != 0;
+    }
+    expect(nf == no, "ComplexDecimator::execute count", (double)nf);
+    // float parity (< 1e-5) leaves truncation at .999 / .000 boundaries: one LSB
+    expect(maxdiff <= 1, "ComplexDecimator::execute max |d| (LSB)", maxdiff);
+    expect(differ * 1000 <= 2 * no, "ComplexDecimator::execute bytes differing", (double)differ / (2.0 * no));
+    oracle_decim_destroy(od);
+  }
+  // ---- FMDemod::process / processComplex / processNoDownsample (fm_demod.cpp:228-279) ----
+  {
+    // u8 IQ at the DSP rate (256 kHz, FMDemod's own byte path)
+    fmx_synth_config s2 = sc;
+    s2.iq_rate = 256000;
+    const size_t N2 = 4096 * 12;
+    std::vector<uint8_t> bits2(sc.n_bits);
+    fmx_synth_rds_bits(&s2, 9, 1, bits2.data(), nullptr);
+    std::vector<uint8_t> iq2(2 * N2);
+    fmx_synth_host(&s2, 9, 1, 0, (int)N2, bits2.data(), iq2.data(), iq2.size(), 4);
+    fmx::FMDemod dm(256000, 32000), dn(256000, 32000), dc(240000, 32000);
+    void *om = oracle_demod_create(256000, 32000), *on = oracle_demod_create(256000, 32000);
+    void *oc = oracle_demod_create(240000, 32000);
+    std::vector<float> af(N2), ao(N2), mf(N2), mo(N2), scratch(N2), cf_(NS), co(NS);
+    size_t kf = 0, ko = 0, kcf = 0, kco = 0;
+    for (size_t off = 0; off < N2; off += 4096) {
+      dm.process(iq2.data() + 2 * off, af.data() + kf, 4096);
+      kf += dm.getLastAudioCount();
+      ko += oracle_demod_process_split(om, iq2.data() + 2 * off, scratch.data(), ao.data() + ko, 4096);
+      dn.processNoDownsample(iq2.data() + 2 * off, mf.data() + off, 4096);
+      oracle_demod_process_split(on, iq2.data() + 2 * off, mo.data() + off, nullptr, 4096);
+    }
+    for (size_t off = 0; off < 4096 * 12; off += 4096) {
+      dc.processComplex(bb_o.data() + off, cf_.data() + kcf, 4096);
+      kcf += dc.getLastAudioCount();
+      kco += oracle_demod_process_split_complex(oc, reinterpret_cast<const float *>(bb_o.data() + off),
+                                                scratch.data(), co.data() + kco, 4096);
+    }
+    expect(kf == ko && ko > 0, "FMDemod::process audio count", (double)kf);
+    expect(rms(af.data(), ao.data(), ko) < 1e-5, "FMDemod::process audio RMS", rms(af.data(), ao.data(), ko));
+    expect(maxd(mf.data(), mo.data(), N2) < 3e-4, "FMDemod::processNoDownsample MPX max |d|",
+           maxd(mf.data(), mo.data(), N2));
+    expect(kcf == kco && kco > 0, "FMDemod::processComplex audio count", (double)kcf);
+    expect(rms(cf_.data(), co.data(), kco) < 1e-5, "FMDemod::processComplex audio RMS",
+           rms(cf_.data(), co.data(), kco));
+    oracle_demod_destroy(om);
+    oracle_demod_destroy(on);
+    oracle_demod_destroy(oc);
+  }
+  // ---- any de-emphasis constant and deviation (fm_demod.cpp:50-71, af_post_processor.cpp:31-45) ----
+  {
+    fmx::FMDemod dm(240000, 32000);
+    void *od = oracle_demod_create(240000, 32000);
+    fmx::AFPostProcessor af(240000, 32000);
+    void *oa = oracle_afpost_create(240000, 32000);
+    std::vector<float> mf(NS), mo(NS), aof(NS), aoo(NS), alf(NS), arf(NS), alo(NS), aro(NS);
+    size_t kf = 0, ko = 0, kaf = 0, kao = 0;
+    for (size_t b = 0; b < 12; ++b) {
+      if (b == 0) {
+        dm.setDeemphasis(60);
+        oracle_demod_set(od, 1, 60);
+        dm.setDeviation(50000.0);
+        oracle_demod_set(od, 5, 50000);
+        af.setDeemphasis(100);
+        oracle_afpost_set_deemphasis(oa, 100);
+      }
+      if (b == 6) {  // a second change mid-stream: the IIR / discriminator re-created
+        dm.setDeemphasis(120);
+        oracle_demod_set(od, 1, 120);
+        dm.setDeviation(67500.0);
+        oracle_demod_set(od, 5, 67500);
+        af.setDeemphasis(0);
+        oracle_afpost_set_deemphasis(oa, 0);
+      }
+      kf += dm.processSplitComplex(bb_o.data() + b * B, mf.data() + b * B, aof.data() + kf, B);
+      ko += oracle_demod_process_split_complex(od, reinterpret_cast<const float *>(bb_o.data() + b * B),
+                                               mo.data() + b * B, aoo.data() + ko, B);
+      kaf += af.process(l_o.data() + b * B, r_o.data() + b * B, B, alf.data() + kaf, arf.data() + kaf, B);
+      kao += oracle_afpost_process(oa, l_o.data() + b * B, r_o.data() + b * B, B, alo.data() + kao,
+                                   aro.data() + kao, B);
+    }
+    expect(kf == ko, "FMDemod tau 60/120 us, 50/67.5 kHz: count", (double)kf);
+    expect(maxd(mf.data(), mo.data(), 12 * B) < 3e-4, "FMDemod custom deviation MPX max |d|",
+           maxd(mf.data(), mo.data(), 12 * B));
+    expect(rms(aof.data(), aoo.data(), ko) < 1e-5, "FMDemod custom de-emphasis mono RMS",
+           rms(aof.data(), aoo.data(), ko));
+    expect(kaf == kao, "AFPostProcessor tau 100 us / off: count", (double)kaf);
+    expect(std::max(rms(alf.data(), alo.data(), kao), rms(arf.data(), aro.data(), kao)) < 1e-5,
+           "AFPostProcessor custom de-emphasis RMS",
+           std::max(rms(alf.data(), alo.data(), kao), rms(arf.data(), aro.data(), kao)));
+    oracle_demod_destroy(od);
+    oracle_afpost_destroy(oa);
+  }
+  // ---- settings outside the GPU build fail loudly ----
   {
     bool threw = false;
     try {
-      fmx::FMDemod dm(240000, 32000);
-      dm.setDeemphasis(60);
+      fmx::ComplexDecimator dec;
+      dec.init(3, 12, 80.0f);
     } catch (const std::invalid_argument &) {
       threw = true;
     }
-    expect(threw, "unsupported de-emphasis throws", threw);
+    expect(threw, "unsupported decimator design throws", threw);
   }
   std::printf(g_fail ? "FACADES FAIL\n" : "FACADES OK\n");
   return g_fail;

@@ -25,5 +25,7 @@ def test_facade_symbols_exported():
     out = subprocess.run(["nm", "-DC", lib], capture_output=True, text=True, check=True).stdout
     for sym in ("fmx::FMDemod::processSplitComplex", "fmx::StereoDecoder::processAudio",
                 "fmx::AFPostProcessor::process", "fmx::RDSDecoder::process",
-                "fmx::ComplexDecimator::executeComplex", "fmx::Receiver::processBlock"):
+                "fmx::ComplexDecimator::executeComplex", "fmx::ComplexDecimator::execute",
+                "fmx::FMDemod::process", "fmx::FMDemod::processComplex", "fmx::FMDemod::processNoDownsample",
+                "fmx::FMDemod::setDeviation", "fmx::Receiver::processBlock"):
         assert sym in out, sym

@@ -249,6 +249,20 @@ def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
               pilot_tol=PILOT_UNLOCKED_TOL if narrow else 0, narrow=narrow)
 
 
+def test_custom_deemphasis_and_deviation(fmx, oracle, torch_cuda):
+    """setDeemphasis(tau_us) with any tau on both FMDemod and AFPostProcessor
+    (fm_demod.cpp:50-62, af_post_processor.cpp:31-45: alpha = dt / (tau + dt),
+    IIR re-created) and FMDemod::setDeviation (fm_demod.cpp:64-71: kf =
+    deviation / Fs, discriminator re-created), mid-stream and per channel."""
+    C, nblk = 3, 24
+    iq, _ = make_iq(fmx, 2, C, nblk, ch0=120)
+    params = {0: [("deemph_us", 60, -1)], 6: [("deviation_hz", 70000, 1)],
+              10: [("deemph_us", 0, 0), ("deemph_us", 100, 2)], 16: [("deviation_hz", 75000, 1)]}
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, params=params)
+    for c in range(C):
+        check(g, outs[c], c, nblk, "tau/deviation")
+
+
 @pytest.mark.parametrize("n", [1500, 333])
 def test_ragged_call_sizes(fmx, oracle, torch_cuda, n):
     """Calls of n < dsp_block samples that do not divide the kernel chunks."""
