@@ -32,19 +32,36 @@ namespace fmx {
 // Timing groups: channels whose resampler timing state is identical share
 // one host-simulated output schedule (the schedule does not depend on the
 // signal, only on the state and the number of inputs).
+//
+// Every step's schedules reach the GPU in ONE copy per set: slot b (step k
+// mod FMX_NBUF) is [group map (C ints) | counts (cap ints) | schedules (G x
+// stride)] in one device allocation, staged from a pinned host image of the
+// same layout.  process_block uploads the NEXT step's schedules one step
+// early, on the PLL stream (sB) while the front end runs, assuming the same
+// n and no reset in between (`spec`); a step that breaks the assumption rolls
+// the speculation back and uploads on sA as before.  On sA the uploads sat
+// between consecutive front-end kernels: 6 copies, ~0.1 ms per step
+// (rocprofv3 --memory-copy-trace).
 struct TimingSet {
   float del = 1.0f;
   std::vector<ResampTiming> groups;
   std::vector<int> chan_group;
-  std::vector<FmxSched> hsched;
-  std::vector<int> hcount;
-  // device copies, double-buffered by step parity: step k+1 uploads while
-  // the consumers of step k may still run on another stream
+  int stride = 0, cap_groups = 0;
+  int G = 0;   // groups in the last simulated step
+  int cur = 0; // slot holding the schedules of the step being launched
+  size_t slot_bytes = 0;
+  unsigned char *d_slot[FMX_NBUF] = {};
+  unsigned char *h_slot[FMX_NBUF] = {}; // pinned
   FmxSched *d_sched[FMX_NBUF] = {};
   int *d_count[FMX_NBUF] = {};
   int *d_group[FMX_NBUF] = {};
-  int stride = 0, cap_groups = 0;
-  int cur = 0; // buffer holding the latest upload
+  hipEvent_t ev_up[FMX_NBUF] = {}; // after the last copy out of h_slot[b]
+  bool ev_up_set[FMX_NBUF] = {};
+  // speculation: state before the speculative advance, its n and slot
+  bool spec = false;
+  int spec_n = 0, spec_slot = -1;
+  std::vector<ResampTiming> spec_groups;
+  std::vector<int> spec_map;
 };
 
 struct Handle {
@@ -130,6 +147,18 @@ template <typename T> static int dalloc(Handle *h, T **p, size_t count) {
   return dmalloc(h, reinterpret_cast<void **>(p), count * sizeof(T));
 }
 
+// Events that only order work on this device (stream joins, kernel timing)
+// skip the system-scope fence at record time (hipEventDisableSystemFence);
+// FMX_EVENT_SYSFENCE=1 keeps HIP's default, for A/B runs.
+static unsigned ev_flags(bool timing) {
+  static const bool sysfence = [] {
+    const char *e = std::getenv("FMX_EVENT_SYSFENCE");
+    return e && e[0] == '1';
+  }();
+  return (timing ? 0u : static_cast<unsigned>(hipEventDisableTiming)) |
+         (sysfence ? 0u : static_cast<unsigned>(hipEventDisableSystemFence));
+}
+
 static hipEvent_t ev_get(Handle *h) {
   if (!h->pool.empty()) {
     hipEvent_t e = h->pool.back();
@@ -137,7 +166,7 @@ static hipEvent_t ev_get(Handle *h) {
     return e;
   }
   hipEvent_t e;
-  hipEventCreate(&e);
+  hipEventCreateWithFlags(&e, ev_flags(true));
   return e;
 }
 
@@ -175,6 +204,39 @@ static void collect_timing(Handle *h) {
 }
 
 /* ---------------- timing sets ---------------- */
+// slot layout: group map, counts, then the schedules 16-B aligned
+static size_t tset_sched_off(const Handle *h, const TimingSet &t) {
+  return (sizeof(int) * (static_cast<size_t>(h->C) + t.cap_groups) + 15) & ~static_cast<size_t>(15);
+}
+static FmxSched *tset_hsched(const Handle *h, TimingSet &t, int b) {
+  return reinterpret_cast<FmxSched *>(t.h_slot[b] + tset_sched_off(h, t));
+}
+static void tset_free_slots(Handle *h, TimingSet &t) {
+  for (int b = 0; b < FMX_NBUF; ++b) {
+    if (t.d_slot[b]) {
+      h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_slot[b])),
+                      h->allocs.end());
+      hipFree(t.d_slot[b]);
+    }
+    if (t.h_slot[b]) hipHostFree(t.h_slot[b]);
+    t.d_slot[b] = t.h_slot[b] = nullptr;
+  }
+}
+static int tset_alloc_slots(Handle *h, TimingSet &t) {
+  const size_t off = tset_sched_off(h, t);
+  t.slot_bytes = off + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.cap_groups;
+  int rc;
+  for (int b = 0; b < FMX_NBUF; ++b) {
+    if ((rc = dalloc(h, &t.d_slot[b], t.slot_bytes)) != FMX_OK) return rc;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.h_slot[b]), t.slot_bytes, hipHostMallocDefault));
+    std::memset(t.h_slot[b], 0, t.slot_bytes);
+    t.d_group[b] = reinterpret_cast<int *>(t.d_slot[b]);
+    t.d_count[b] = t.d_group[b] + h->C;
+    t.d_sched[b] = reinterpret_cast<FmxSched *>(t.d_slot[b] + off);
+    if (!t.ev_up[b]) HIP_TRY(hipEventCreateWithFlags(&t.ev_up[b], ev_flags(false)));
+  }
+  return FMX_OK;
+}
 static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.del = del;
   ResampTiming r;
@@ -184,15 +246,14 @@ static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.chan_group.assign(static_cast<size_t>(h->C), 0);
   t.stride = static_cast<int>(std::ceil(static_cast<double>(max_in) / std::max(0.5, (double)del))) + 8;
   t.cap_groups = 4;
-  t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
-  t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
-  int rc;
-  for (int b = 0; b < FMX_NBUF; ++b) {
-    if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
-    if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
-    if ((rc = dalloc(h, &t.d_group[b], static_cast<size_t>(h->C))) != FMX_OK) return rc;
-  }
-  return FMX_OK;
+  return tset_alloc_slots(h, t);
+}
+// undo a speculative advance (a reset, a stage call or another n follows)
+static void tset_unspec(TimingSet &t) {
+  if (!t.spec) return;
+  t.groups = t.spec_groups;
+  t.chan_group = t.spec_map;
+  t.spec = false;
 }
 
 // channel c's resampler was reset (liquid resamp_reset): move it to a group
@@ -241,47 +302,79 @@ static void tset_compact(TimingSet &t) {
   t.groups = ng;
 }
 
-// Simulate n inputs for every group and upload the schedules into buffer
-// `buf` (step parity) on stream sA; returns the largest output count.
-static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
+// Simulate n inputs for every group into the pinned image of slot `buf`
+// (the caller uploads it); returns the largest output count in *max_count.
+static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
   tset_compact(t);
   const int G = static_cast<int>(t.groups.size());
   if (G > t.cap_groups) {
     HIP_TRY(hipDeviceSynchronize());
-    for (int b = 0; b < FMX_NBUF; ++b) {
-      for (void *p : {static_cast<void *>(t.d_sched[b]), static_cast<void *>(t.d_count[b])}) {
-        h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), p), h->allocs.end());
-        HIP_TRY(hipFree(p));
-      }
-    }
+    tset_free_slots(h, t);
     t.cap_groups = G * 2;
-    t.hsched.resize(static_cast<size_t>(t.stride) * t.cap_groups);
-    t.hcount.assign(static_cast<size_t>(t.cap_groups), 0);
+    for (int b = 0; b < FMX_NBUF; ++b) t.ev_up_set[b] = false;
     int rc;
-    for (int b = 0; b < FMX_NBUF; ++b) {
-      if ((rc = dalloc(h, &t.d_sched[b], static_cast<size_t>(t.stride) * t.cap_groups)) != FMX_OK) return rc;
-      if ((rc = dalloc(h, &t.d_count[b], static_cast<size_t>(t.cap_groups))) != FMX_OK) return rc;
-    }
+    if ((rc = tset_alloc_slots(h, t)) != FMX_OK) return rc;
   }
+  // the previous copy out of this pinned image must have run
+  if (t.ev_up_set[buf]) HIP_TRY(hipEventSynchronize(t.ev_up[buf]));
+  FmxSched *hs = tset_hsched(h, t, buf);
+  int *hc = reinterpret_cast<int *>(t.h_slot[buf]) + h->C;
   int mx = 0;
   for (int g = 0; g < G; ++g) {
-    const int k = timing_run(t.groups[static_cast<size_t>(g)], n,
-                             t.hsched.data() + static_cast<size_t>(g) * t.stride, t.stride);
+    const int k = timing_run(t.groups[static_cast<size_t>(g)], n, hs + static_cast<size_t>(g) * t.stride, t.stride);
     if (k > t.stride) {
       h->err = "resampler schedule overflow";
       return FMX_E_CAPACITY;
     }
-    t.hcount[static_cast<size_t>(g)] = k;
+    hc[g] = k;
     mx = std::max(mx, k);
   }
-  // pageable-memory copies are staged before hipMemcpyAsync returns, so the
-  // host vectors can be reused by the next call immediately
-  HIP_TRY(hipMemcpyAsync(t.d_sched[buf], t.hsched.data(), sizeof(FmxSched) * static_cast<size_t>(t.stride) * G,
-                         hipMemcpyHostToDevice, h->sA));
-  HIP_TRY(hipMemcpyAsync(t.d_count[buf], t.hcount.data(), sizeof(int) * G, hipMemcpyHostToDevice, h->sA));
-  HIP_TRY(hipMemcpyAsync(t.d_group[buf], t.chan_group.data(), sizeof(int) * h->C, hipMemcpyHostToDevice, h->sA));
-  t.cur = buf;
+  std::memcpy(t.h_slot[buf], t.chan_group.data(), sizeof(int) * h->C);
+  t.G = G;
   if (max_count) *max_count = mx;
+  return FMX_OK;
+}
+static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
+  const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
+  HIP_TRY(hipMemcpyAsync(t.d_slot[buf], t.h_slot[buf], bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(t.ev_up[buf], s));
+  t.ev_up_set[buf] = true;
+  return FMX_OK;
+}
+// Simulate n inputs and upload the schedules into slot `buf` on sA.
+static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
+  tset_unspec(t);
+  int rc;
+  if ((rc = tset_simulate(h, t, n, buf, max_count)) != FMX_OK) return rc;
+  // an earlier copy into this slot may still be queued on another stream
+  if (t.ev_up_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, t.ev_up[buf], 0));
+  if ((rc = tset_upload(h, t, buf, h->sA)) != FMX_OK) return rc;
+  t.cur = buf;
+  return FMX_OK;
+}
+// process_block: the schedules of this step were uploaded one step early
+// into `buf` (same n, nothing reset since) -- use them
+static bool tset_take_spec(TimingSet &t, int n, int buf) {
+  if (!t.spec || t.spec_n != n || t.spec_slot != buf) return false;
+  t.spec = false;
+  t.cur = buf;
+  return true;
+}
+// process_block: simulate the next step (n inputs again) from the state this
+// step leaves and upload it into `buf` on stream s
+static int tset_speculate(Handle *h, TimingSet &t, int n, int buf, hipStream_t s) {
+  t.spec_groups = t.groups;
+  t.spec_map = t.chan_group;
+  int rc;
+  if ((rc = tset_simulate(h, t, n, buf, nullptr)) != FMX_OK) {
+    t.spec = true;
+    tset_unspec(t);
+    return rc;
+  }
+  if ((rc = tset_upload(h, t, buf, s)) != FMX_OK) return rc;
+  t.spec = true;
+  t.spec_n = n;
+  t.spec_slot = buf;
   return FMX_OK;
 }
 
@@ -424,6 +517,11 @@ static void destroy(Handle *h) {
     hipEventDestroy(p.b);
   }
   for (auto e : h->pool) hipEventDestroy(e);
+  for (TimingSet *t : {&h->t_af, &h->t_mono, &h->t_rds}) {
+    tset_free_slots(h, *t);
+    for (hipEvent_t e : t->ev_up)
+      if (e) hipEventDestroy(e);
+  }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
     for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
@@ -521,14 +619,14 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     }
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
-    HIP_TRY(hipEventCreateWithFlags(&h->evA[b], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&h->evB[b], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&h->evC[b], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&h->evD[b], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(false)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evB[b], ev_flags(false)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(false)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(false)));
   }
-  HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&h->evTmpD, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, ev_flags(false)));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, ev_flags(false)));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpD, ev_flags(false)));
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
@@ -738,9 +836,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     if (h->evC_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
     if (h->evD_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
   }
-  if (rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
+  // resampler schedules of this step: uploaded one step early (below), or now on sA
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
-  if ((rc = tset_advance(h, *tau, n, buf, nullptr)) != FMX_OK) return rc;
+  const bool hit_rds = rds && tset_take_spec(h->t_rds, n, buf);
+  const bool hit_af = tset_take_spec(*tau, n, buf);
+  if (rds && !hit_rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
+  if (!hit_af && (rc = tset_advance(h, *tau, n, buf, nullptr)) != FMX_OK) return rc;
+  if (hit_rds) HIP_TRY(hipStreamWaitEvent(h->sA, h->t_rds.ev_up[buf], 0)); // the front end reads it
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
   // ---- front end (sA) ----
@@ -786,6 +888,16 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
   h->evC_set[buf] = true;
+  // ---- next step's schedules, one step early, on sB ahead of this step's
+  // PLL (off the front end's stream).  Slot nb was last read by step
+  // k+1-FMX_NBUF's front end (sB's previous PLL waited for a later one) and
+  // audio (sD).
+  {
+    const int nb = (buf + 1) % FMX_NBUF;
+    if (h->evD_set[nb]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[nb], 0));
+    if (rds && (rc = tset_speculate(h, h->t_rds, n, nb, h->sB)) != FMX_OK) return rc;
+    if ((rc = tset_speculate(h, *tau, n, nb, h->sB)) != FMX_OK) return rc;
+  }
   // ---- stereo PLL (sB), audio (sD) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   if (stereo) {
@@ -857,6 +969,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
 static int stage_begin(Handle *h, int n) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
+  for (TimingSet *t : {&h->t_af, &h->t_mono, &h->t_rds}) tset_unspec(*t);
   if ((rc = prepare(h)) != FMX_OK) return rc;
   return join_into_A(h);
 }
@@ -918,6 +1031,9 @@ static int reset_channels(Handle *h, int channel, int extra) {
     return FMX_E_INVALID;
   }
   const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
+  tset_unspec(h->t_af);
+  tset_unspec(h->t_mono);
+  tset_unspec(h->t_rds);
   for (int c = c0; c < c1; ++c) {
     int m = RS_DECIM | RS_DEMOD | RS_STEREO | RS_AF | RS_RDS | extra;
     if (h->agc_ready[static_cast<size_t>(c)]) m |= RS_AGC;

@@ -975,7 +975,7 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
   return 0.0f;
 }
 
-/* k_pll is a five-wave software pipeline over tiles of PLL_T samples for
+/* k_pll is an eight-wave software pipeline over tiles of PLL_T samples for
  * PLL_CH channels (lane = channel in the serial waves):
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
  *                 pll_step, step, sin(phase) straight from the phase word
@@ -983,7 +983,7 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
  *   W4            (lane = (channel, t)) the reference's float phase of each
  *                 word with its sine and cosine (fmx_sincos_q) for the
  *                 outputs; shares W0's SIMD                 :251-253
- *   W2a, W2b      (lane = (channel, t)) everything parallel in time: the
+ *   W2a..W2d      (lane = (channel, t)) everything parallel in time: the
  *                 blend target (sqrt, divisions) and the L-R matrix   :120-166,268-284
  *   W1 (serial)   what consumes the PLL without feeding it back: pilot/MPX
  *                 envelopes, pilot I/Q integrators (cos(phase)), PLL
@@ -997,18 +997,18 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 #define PLL_CH 64
 #define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
 #define PLL_WAVES 8
-// Waves w, w + 4, w + 8 of a workgroup share a SIMD (measured,
+// Waves w and w + 4 of a workgroup share a SIMD (measured,
 // tools/ubench/hwid.hip), and a SIMD retires about one wave64 VALU
-// instruction per 4 cycles whichever wave issues it.  SIMD 0: W0 (chain),
-// W4 (output phases), W2c; SIMD 1: W1, W3, W2d; SIMD 2: W2a (+ wave 6,
-// barriers only); SIMD 3: W2b (+ wave 7, barriers only).  The blend-target
-// items (the longest per-tile work once stereo is detected) are spread over
-// all four SIMDs, one item per lane per W2 wave.
+// instruction per 4 cycles whichever wave issues it.  Wave numbers:
+// 0 = W0, 1 = W1, 2/3/6/7 = W2a/W2b/W2c/W2d, 4 = W4, 5 = W3, so
+// SIMD 0: W0 (chain) + W4 (output phases); SIMD 1: W1 + W3;
+// SIMD 2: W2a + W2c; SIMD 3: W2b + W2d.  The blend-target items (the
+// longest per-tile work once stereo is detected) are spread over four
+// waves on two SIMDs, one item per lane per W2 wave.
 #define PLL_W1 1
 #define PLL_IDLE 4
 #define PLL_W3 5
 #define PLL_NW2 4                          // W2 waves: 2, 3, 6, 7
-#define PLL_BARRIER_ONLY(w) false
 #define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
 #define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
 
@@ -1528,9 +1528,6 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     }
 #endif
 #undef W3_STAMP
-  } else if (PLL_BARRIER_ONLY(wave)) {
-    for (int k = 0; k < PLL_NIT(NT); ++k) PLL_SYNC()
-    PLL_SYNC()
   } else if (wave == PLL_IDLE) {
     // ---------------- W4: phases for the outputs (shares W0's SIMD) ----------------
     for (int k = 0; k < PLL_NIT(NT); ++k) {
@@ -3517,7 +3514,7 @@ int launch_audio(const AudioArgs &a, void *stream) {
 int launch_rds(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 60.5 KB) leave 39 KB of a CU's 160 KB: k_rds
   // fits beside them (as k_pll's 35.5 KB does)
-  static_assert(sizeof(RdsLds) + RDS_RING * 64 * 4 <= 39 * 1024, "k_rds LDS must fit beside two k_fe8 workgroups");
+  static_assert(sizeof(RdsLds) + RDS_RING * 64 * 4 <= 38 * 1024, "k_rds LDS must fit beside two k_fe8 workgroups");
   hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }

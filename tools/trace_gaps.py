@@ -1,0 +1,23 @@
+"""Front-end kernel gaps and the ops between them, from a rocprofv3
+--kernel-trace --memory-copy-trace CSV directory (tools/gpu_trace.sh)."""
+import csv
+import glob
+import os
+import sys
+
+d = sys.argv[1]
+ks = list(csv.DictReader(open(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0])))
+mc = glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True)
+ms = list(csv.DictReader(open(mc[0]))) if mc else []
+ev = [(int(k["Start_Timestamp"]), int(k["End_Timestamp"]), k["Kernel_Name"][:28]) for k in ks]
+ev += [(int(m["Start_Timestamp"]), int(m["End_Timestamp"]), "copy " + m["Direction"][12:]) for m in ms]
+ev.sort()
+fe = [e for e in ev if "k_fe8" in e[2]]
+gaps = [(b[0] - a[1]) / 1e3 for a, b in zip(fe, fe[1:])]
+print("front-end launches", len(fe), "avg us", sum((e[1] - e[0]) for e in fe) / max(1, len(fe)) / 1e3)
+print("gaps between front ends (us):", " ".join("%.1f" % g for g in gaps[-12:]))
+if len(fe) > 4:
+    a, b = fe[-4], fe[-3]
+    for e in ev:
+        if a[0] <= e[0] < b[0] + 1:
+            print("  %9.1f %8.1f %s" % ((e[0] - a[0]) / 1e3, (e[1] - e[0]) / 1e3, e[2]))
