@@ -1538,6 +1538,12 @@ int fmx_synth_device(void *handle, const fmx_synth_config *cfg, uint32_t ch0, in
 }
 
 /* ---------------- diagnostics (no GPU needed) ---------------- */
+static double f16_value(uint16_t h) {
+  const int e = (h >> 10) & 31;
+  const double m = static_cast<double>(h & 0x3FF);
+  const double v = (e == 0) ? std::ldexp(m, -24) : std::ldexp(m + 1024.0, e - 25);
+  return (h & 0x8000u) ? -v : v;
+}
 int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
   if (!cfg) return FMX_E_INVALID;
   FmxDesign *d = new FmxDesign();
@@ -1564,6 +1570,14 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
     case 6: v.assign(d->rds_fir, d->rds_fir + FMX_RDS_FIR); break;
     case 7: v = ex.rrc; break;
     case 8: v = ex.rrc_d; break;
+    case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
+      for (int cp = 0; cp < 2; ++cp)
+        for (int k = 0; k < d->dec_len; ++k) {
+          const int x = (d->dec_len - k) - FMX_DQ_MIN + 2 * cp;
+          const double q = f16_value(d->dec_q16[cp][0][x]) + f16_value(d->dec_q16[cp][1][x]);
+          v.push_back(static_cast<float>(q / 65536.0 * 127.5));
+        }
+      break;
     default: delete d; return FMX_E_INVALID;
   }
   delete d;

@@ -30,6 +30,34 @@ namespace fmx {
 static constexpr double kPiD = 3.14159265358979323846;
 static constexpr float kPiF = 3.14159265358979323846f;
 
+// IEEE binary16 <-> binary32 (round to nearest even) for the MFMA tap tables
+static float f16_bits_to_f32(uint16_t h) {
+  const int e = (h >> 10) & 31;
+  const uint32_t m = h & 0x3FFu;
+  float v;
+  if (e == 0) v = std::ldexp(static_cast<float>(m), -24);
+  else if (e == 31) v = m ? std::numeric_limits<float>::quiet_NaN() : std::numeric_limits<float>::infinity();
+  else v = std::ldexp(static_cast<float>(m | 0x400u), e - 25);
+  return (h & 0x8000u) ? -v : v;
+}
+static uint16_t f32_to_f16_bits(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint16_t sign = static_cast<uint16_t>((x >> 16) & 0x8000u);
+  const uint32_t ax = x & 0x7FFFFFFFu;
+  if (ax > 0x7F800000u) return sign | 0x7E00u;
+  if (ax >= 0x477FF000u) return sign | 0x7C00u; // >= 65520 rounds to infinity
+  if (ax <= 0x33000000u) return sign;           // <= 2^-25 rounds to zero
+  const int e = static_cast<int>(ax >> 23) - 127;
+  const uint32_t m = (ax & 0x7FFFFFu) | 0x800000u;
+  const int shift = (e < -14) ? 13 + (-14 - e) : 13;
+  uint32_t r = m >> shift;
+  const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
+  if (rem > half || (rem == half && (r & 1u))) ++r;
+  if (e < -14) return sign | static_cast<uint16_t>(r); // subnormal (a carry lands on the smallest normal)
+  return sign | static_cast<uint16_t>((static_cast<uint32_t>(e + 15) << 10) + (r - 0x400u));
+}
+
 static float kaiser_beta_As(float As) {
   As = std::fabs(As);
   if (As > 50.0f) return 0.1102f * (As - 8.7f);
@@ -192,6 +220,20 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     double dc = 0.0;
     for (int i = 0; i < d->dec_len; ++i) dc += static_cast<double>(d->dec_taps[i]);
     d->dec_dc = static_cast<float>(127.5 * dc);
+    // MFMA decimator tables (k_fe8): taps reversed, scaled by 2^16 (the
+    // smallest stay f16-normal), hi/lo f16 split; bytes enter as b - 128
+    const int L = d->dec_len;
+    for (int cp = 0; cp < 2; ++cp)
+      for (int x = 0; x < FMX_DQ_N; ++x) {
+        const int dd = x - 2 * cp + FMX_DQ_MIN;
+        const float q = (dd >= 1 && dd <= L) ? d->dec_taps[L - dd] * 65536.0f : 0.0f;
+        const uint16_t hi = f32_to_f16_bits(q);
+        const uint16_t lo = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+        d->dec_q16[cp][0][x] = hi;
+        d->dec_q16[cp][1][x] = lo;
+      }
+    d->dec_dc16 = static_cast<float>(-0.5 * 65536.0 * dc);
+    d->dec_scale16 = d->dec_scale * (1.0f / 65536.0f);
   } else {
     d->dec_scale = 1.0f;
     d->dec_dc = 0.0f;

@@ -26,6 +26,8 @@
 #define FMX_HIST 512         // stereo MPX history (>= pilot taps - 1 and delay line)
 #define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
+#define FMX_DQ_MIN (-152)    // k_fe8 MFMA decimator tap table: first tap offset (multiple of 8, <= -15 M)
+#define FMX_DQ_N 608         // entries per copy and split (covers 32 K-steps of 16 outputs for M <= 10)
 
 typedef struct {
   float x, y;
@@ -45,6 +47,14 @@ typedef struct {
   float dec_taps_raw[FMX_MAX_DEC];
   float dec_poly[FMX_MAX_DEC]; // [p][q] = dec_taps[q*M + p]  (phase-major)
   float dec_pad[FMX_MAX_DEC + 2 * FMX_DEC_PAD]; // [FMX_DEC_PAD + k] = dec_taps[k], zeros around
+  // k_fe8's MFMA decimator (16 outputs x 16 blocks per v_mfma_f32_16x16x32_f16):
+  // q[d] = dec_taps[L - d] * 2^16 for d in [1, L] (0 elsewhere), d in
+  // [FMX_DQ_MIN, FMX_DQ_MIN + FMX_DQ_N), split into f16 hi + lo (22 significant
+  // bits); copy 1 is shifted by two entries so that every lane's 8-tap
+  // fragment starts 8-B aligned in one of the copies.  Output y = (acc -
+  // dec_dc16) * dec_scale16 with acc = sum (byte - 128) * q.
+  uint16_t dec_q16[2][2][FMX_DQ_N] __attribute__((aligned(16))); // [copy][hi, lo][d - FMX_DQ_MIN + 2 * copy]
+  float dec_dc16, dec_scale16;
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
   int iq_len[FMX_IQ_DESIGNS];
   float iq_scale[FMX_IQ_DESIGNS];

@@ -2909,7 +2909,13 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * ~58 KB of LDS per workgroup: two workgroups (8 waves) per CU leave room
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
-__device__ __forceinline__ int fe8_i(int i) { return i + (i >> 3); }
+__host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
+#ifndef FMX_DEC_MFMA
+#define FMX_DEC_MFMA 1 // k_fe8 decimator on v_mfma_f32_16x16x32_f16 (0: packed-FMA VALU decimator, A/B runs)
+#endif
+#ifndef FMX_DEC_KS_UNROLL
+#define FMX_DEC_KS_UNROLL 7
+#endif
 typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
 
@@ -2941,6 +2947,15 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
+  // MFMA decimator tap tables (FmxDesign::dec_q16), per chunk in the MPX
+  // image's chunk part (floats from fe8_i(FMX_HIST), short of its zero slack)
+  static constexpr int TQ = (fe8_i(FMX_HIST) + 3) & ~3;
+  static constexpr int TQ_WORDS = 2 * FMX_DQ_N; // [copy][hi, lo][FMX_DQ_N] f16
+  static_assert(TQ + TQ_WORDS <= fe8_i(FMX_HIST + FE8_T), "tap tables inside the MPX chunk part");
+  // the MFMA decimator's outputs on their way to the 8-per-thread layout
+  // (16-B aligned, above the complex image, inside the dead raw region)
+  static constexpr int STG = (YB + 15) & ~15;
+  static_assert(STG + FE8_T * 8 <= R0, "decimator staging inside the raw region");
 };
 
 // 8 outputs j0..j0+7 (j0 % 8 == 0) of a real-tap FIR of runtime length P on
@@ -3129,6 +3144,19 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     if (rds && tid == 0) sh->e_end = e_pos;
     FE_STAMP(7)
     // ================= decimator =================
+#if FMX_DEC_MFMA
+    // the MFMA tap tables into the MPX image's chunk part (dead until the
+    // discriminator below writes it)
+    {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(&D->dec_q16[0][0][0]);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(mx + LY::TQ);
+#pragma unroll
+      for (int k = 0; k < (LY::TQ_WORDS + 255) / 256; ++k) {
+        const int i = tid + 256 * k;
+        if (i < LY::TQ_WORDS) dst[i] = src[i];
+      }
+    }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
     if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (full history)
@@ -3151,6 +3179,92 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
     }
     float2 xv[8]; // decimator outputs of this thread
+#if FMX_DEC_MFMA
+    {
+      // Decimator as v_mfma_f32_16x16x32_f16 tiles.  Output o = 16 B + r of
+      // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
+      // [M r + 1, M r + L], with tap L + M r - t: per block, Y[r] = sum_t
+      // T[r][t] X[t] with T[r][t] = q[t - M r] (FmxDesign::dec_q16) -- one
+      // 16 x 16 tile is 16 outputs (rows, A = taps) of 16 blocks (columns,
+      // B = bytes), K = the block's 15 M + L + 1 input samples in steps of 32.
+      // Each wave runs two tiles (512 outputs); the bytes enter exactly as
+      // f16 (b - 128), the taps as f16 hi + lo, both products accumulate in
+      // f32.  The C layout gives each lane 4 consecutive outputs; they reach
+      // the 8-per-thread layout of the stages below through LDS.
+      typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+      typedef float f32x4_t __attribute__((ext_vector_type(4)));
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      constexpr int KS = (15 * M + L + 1 + 31) / 32;
+      static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN, "tap table range");
+      const int col = lane & 15, g = lane >> 4;
+      const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0
+      const int cp = ((d00 & 3) == 2) ? 1 : 0;     // the copy where it starts 8-B aligned
+      const uint32_t *ta = reinterpret_cast<const uint32_t *>(mx + LY::TQ) + cp * FMX_DQ_N +
+                           ((d00 - FMX_DQ_MIN + 2 * cp) >> 1);
+      const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 16 * g;
+      f32x4_t acc[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      // bytes (I0 Q0 I1 Q1) -> f16 pairs (1024 + b, 1024 + b') by v_perm with
+      // the f16 exponent byte 0x64, then - 1152: b - 128 exactly
+      auto cvt = [](uint32_t w, uint32_t sel) __attribute__((always_inline)) {
+        return __builtin_bit_cast(f16x2_t, __builtin_amdgcn_perm(0x64646464u, w, sel)) -
+               f16x2_t{(_Float16)1152.0f, (_Float16)1152.0f};
+      };
+#pragma unroll FMX_DEC_KS_UNROLL
+      for (int ks = 0; ks < KS; ++ks) {
+        const u32x2 h0 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks);
+        const u32x2 h1 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks + 2);
+        const u32x2 l0 = *reinterpret_cast<const u32x2 *>(ta + FMX_DQ_N / 2 + 16 * ks);
+        const u32x2 l1 = *reinterpret_cast<const u32x2 *>(ta + FMX_DQ_N / 2 + 16 * ks + 2);
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, u32x4{h0.x, h0.y, h1.x, h1.y});
+        const f16x8_t alo = __builtin_bit_cast(f16x8_t, u32x4{l0.x, l0.y, l1.x, l1.y});
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const u32x4 w = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * ks);
+          const f16x2_t i0 = cvt(w.x, 0x04020400u), i1 = cvt(w.y, 0x04020400u);
+          const f16x2_t i2 = cvt(w.z, 0x04020400u), i3 = cvt(w.w, 0x04020400u);
+          const f16x2_t q0 = cvt(w.x, 0x04030401u), q1 = cvt(w.y, 0x04030401u);
+          const f16x2_t q2 = cvt(w.z, 0x04030401u), q3 = cvt(w.w, 0x04030401u);
+          const f16x8_t bi = {i0.x, i0.y, i1.x, i1.y, i2.x, i2.y, i3.x, i3.y};
+          const f16x8_t bq = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bi, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bq, acc[u][1], 0, 0, 0);
+          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bi, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bq, acc[u][1], 0, 0, 0);
+        }
+      }
+      __syncthreads(); // every wave is past raw: its outputs go to the (aliased) staging area
+      float4 *stg = reinterpret_cast<float4 *>(smem + LY::STG);
+      const float dc = D->dec_dc16, sc = D->dec_scale16;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
+        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g;
+        float yr[4], yi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          yr[i] = (acc[u][0][i] - dc) * sc;
+          yi[i] = (acc[u][1][i] - dc) * sc;
+        }
+        stg[o / 2] = make_float4(yr[0], yi[0], yr[1], yi[1]);
+        stg[o / 2 + 1] = make_float4(yr[2], yi[2], yr[3], yi[3]);
+      }
+      __syncthreads();
+      int myclip = 0;
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        const float4 v = stg[(j0 + r) / 2];
+        xv[r] = make_float2(v.x, v.y);
+        xv[r + 1] = make_float2(v.z, v.w);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (fabsf(xv[r].x) >= 0.995f || fabsf(xv[r].y) >= 0.995f) myclip++;
+      if (myclip) atomicAdd(&sh->clip, myclip);
+    }
+#else
     {
       // thread window: samples s = 0 .. 8G-1 from raw sample 8*M*tid; output
       // r uses s in [r*M + 1, r*M + L] with tap L + r*M - s
@@ -3214,6 +3328,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
       if (myclip) atomicAdd(&sh->clip, myclip);
     }
+#endif
     __syncthreads(); // raw is dead: xin / yb alias it from here on
     FE_STAMP(0)
     // IQ FIR history and the zero slack past the chunk (read with zero taps)

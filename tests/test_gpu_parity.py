@@ -8,10 +8,11 @@ The XDR pilot level (stereo_decoder.cpp pilotLevelTenthsKHz, 0.1 kHz steps)
 is exact wherever the pilot PLL is locked.  With a narrow IQ filter
 (W0 / XDR bandwidth < 100 kHz) the 19 kHz pilot is attenuated, the PLL free-
 runs, and the level becomes chaotic: the oracle against ITSELF moves by up to
-4 tenths when 1e-5 of noise is added to the MPX
-(tests/test_oracle_pinning.py::test_unlocked_pilot_level_is_chaotic), so
-those cases hold the level to PILOT_UNLOCKED_TOL instead.  Every test here
-runs on the GPU.
+13 tenths (4 channels x 12 blocks) when 1e-5 of noise is added to the MPX
+(tests/test_oracle_pinning.py::test_unlocked_pilot_level_is_chaotic), and
+the GPU (MPX within ~1e-6 RMS of the oracle) by up to 18 tenths, so those
+blocks hold the level to PILOT_UNLOCKED_TOL instead; their stereo flag,
+indicator, MPX and PCM keep the full bars.  Every test here runs on the GPU.
 """
 import json
 import os
@@ -47,7 +48,7 @@ def make_iq(fmx, kind, C, nblk, iq_rate=2_400_000, M=10, B=4096, noise=0.0, ch0=
     return iq, groups
 
 
-PILOT_UNLOCKED_TOL = 16   # tenths of kHz, free-running PLL only (see module doc)
+PILOT_UNLOCKED_TOL = 30   # tenths of kHz, free-running PLL only (see module doc)
 
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

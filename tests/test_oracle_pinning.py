@@ -239,3 +239,24 @@ def test_unlocked_pilot_level_is_chaotic(fmx, oracle):
     assert all(x == y for x, y in wide)
     narrow = _pilot_levels_with_perturbation(fmx, oracle, 42_000)
     assert max(abs(x - y) for x, y in narrow) >= 2
+    # over 12 blocks the self-deviation reaches 13 tenths on channel 1023
+    narrow = _pilot_levels_with_perturbation(fmx, oracle, 42_000, nblk=12, ch=1023)
+    assert max(abs(x - y) for x, y in narrow) >= 10
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_decimator_tap_tables(fmx, rates):
+    """k_fe8's MFMA decimator takes the decimator taps as f16 hi + lo pairs
+    (scaled by 2^16, FmxDesign::dec_q16): both table copies give the float
+    taps back to 22 significant bits."""
+    if rates["iq_rate"] == rates["dsp_rate"]:
+        pytest.skip("no decimator")
+    cfg = fmx.make_config(**rates)
+    raw = fmx.design_taps(cfg, 0).astype(np.float64)
+    q = fmx.design_taps(cfg, 9).astype(np.float64)
+    assert q.size == 2 * raw.size
+    scale = np.abs(raw).max()
+    for cp in range(2):
+        err = np.abs(q[cp * raw.size:(cp + 1) * raw.size] - raw)
+        # the taps pass through float32 (/127.5, then *127.5 here): a few ulp of the largest
+        assert err.max() <= scale * 2.0 ** -21, (cp, err.max() / scale)

@@ -21,3 +21,18 @@ if len(fe) > 4:
     for e in ev:
         if a[0] <= e[0] < b[0] + 1:
             print("  %9.1f %8.1f %s" % ((e[0] - a[0]) / 1e3, (e[1] - e[0]) / 1e3, e[2]))
+
+# per kernel: mean duration and mean idle gap between consecutive launches
+import statistics
+print("kernel            n    dur_us   median gap_us (start[k+1] - end[k])")
+for key in ("k_fe8", "k_pll", "k_rds", "k_audio"):
+    ks_ = [e for e in ev if key in e[2]]
+    if len(ks_) < 3:
+        continue
+    ks_ = ks_[2:]  # skip warmup
+    d = sum(e[1] - e[0] for e in ks_) / len(ks_) / 1e3
+    gp = [(b[0] - a[1]) / 1e3 for a, b in zip(ks_, ks_[1:])]
+    print("%-12s %5d %9.1f %8.1f" % (key, len(ks_), d, statistics.median(gp)))
+if len(fe) > 3:
+    print("step (front-end start to start, median) us: %.1f" % statistics.median(
+        (b[0] - a[0]) / 1e3 for a, b in zip(fe[2:], fe[3:])))
