@@ -2130,6 +2130,21 @@ __device__ __forceinline__ void rds_taps8(const float *__restrict__ p, float (&t
   t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w;
   t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
 }
+// One FIR product into a partial sum.  FMX_RDS_FMA (default): one packed
+// FMA (v_pk_fma_f32); 0: the reference's separate multiply and add (its
+// dotprod order, rounded twice).  The RDS path is held to bit-exact groups,
+// not to bit-exact floats (its mix-down sine is already the hardware one).
+#ifndef FMX_RDS_FMA
+#define FMX_RDS_FMA 1
+#endif
+__device__ __forceinline__ f32x2 rds_mac(float h, f32x2 m, f32x2 acc) {
+#if FMX_RDS_FMA
+  return __builtin_elementwise_fma(f32x2{h, h}, m, acc);
+#else
+  const f32x2 p = f32x2{h, h} * m;
+  return acc + p;
+#endif
+}
 struct RdsLds {
   // chunk taps by accumulator: tT[p][i][u] = h[J - u + 24 i] for the chunk
   // starting at period phase j0 = 1 + 8p (J = 24 - j0), zero past tap 254
@@ -2398,10 +2413,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
 #pragma unroll
     for (int i = 0; i < FMX_RDS_NACC; ++i) h[i] = tp[i];
 #pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC; ++i) {
-      const f32x2 p = f32x2{h[i], h[i]} * m;
-      acc[i] = acc[i] + p;
-    }
+    for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = rds_mac(h[i], m, acc[i]);
     ring_store(m, t);
   };
   auto mix = [&](float x, float ph) __attribute__((always_inline)) {
@@ -2651,10 +2663,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
         float tu[8];
         rds_taps8(&L.tT[p][i][0], tu);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const f32x2 pr = f32x2{tu[u], tu[u]} * mx[u];
-          acc[i] = acc[i] + pr;
-        }
+        for (int u = 0; u < U; ++u) acc[i] = rds_mac(tu[u], mx[u], acc[i]);
       }
     }
     RDS_STAMP(2)
