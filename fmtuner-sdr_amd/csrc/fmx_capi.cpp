@@ -98,6 +98,7 @@ struct Handle {
   std::vector<double> hsig;   // [C][4] gain*factor, bias, floor, ceil
   double *dsig = nullptr;
   float *sig_smooth = nullptr;
+  unsigned long long *sig_sums[FMX_NBUF] = {}; // [C][6] byte sums of step k (front end -> k_audio)
   bool sig_dirty = true;
   unsigned long long *dbg = nullptr;  // frontend stage clocks when FMX_STAMPS=1
   float2_t *iq_hist = nullptr;
@@ -660,6 +661,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     HIP_TRY(hipMemset(h->dbg, 0, 32 * sizeof(unsigned long long)));
   }
   if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
+  for (int b = 0; b < FMX_NBUF; ++b)
+    if ((rc = dalloc(h, &h->sig_sums[b], C * 6)) != FMX_OK) return rc;
   HIP_TRY(hipMemset(h->sig_smooth, 0, sizeof(float) * 2 * C));
   h->hsig.resize(static_cast<size_t>(C) * 4);
   for (int c = 0; c < C; ++c) {  // gain 0, config.h:27-29 defaults
@@ -730,9 +733,7 @@ static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   a.fd_prev = h->fd_prev;
   a.rds_hist = h->rds_hist;
   a.clip_out = h->clip;
-  a.sig_par = h->dsig;
   a.dbg = h->dbg;
-  a.sig_smooth = h->sig_smooth;
   a.rds_count = h->rds_count[buf];
   a.rds_sched = h->t_rds.d_sched[h->t_rds.cur];
   a.rds_sched_n = h->t_rds.d_count[h->t_rds.cur];
@@ -760,6 +761,17 @@ static AudioArgs audio_args(Handle *h, int n, int mode, TimingSet *t) {
     a.sched_stride = t->stride;
   }
   return a;
+}
+
+// k_audio of a process_block step evaluates the step's RF levels from the
+// front end's byte sums (computeSignalLevel over the call's n * M IQ samples)
+static void audio_signal_level(Handle *h, AudioArgs &a, const fmx_block_out *o, int buf, int n) {
+  if (!o->d_signal) return;
+  a.sig_out = o->d_signal;
+  a.sig_sums = h->sig_sums[buf];
+  a.sig_samples = static_cast<long>(n) * h->M;
+  a.sig_par = h->dsig;
+  a.sig_smooth = h->sig_smooth;
 }
 
 static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
@@ -862,7 +874,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.rds_stride = h->rds_stride;
     }
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
-    a.sig_out = o->d_signal;
+    a.sig_sums = o->d_signal ? h->sig_sums[buf] : nullptr;
     KTimer t(h, FMX_K_FRONTEND, h->sA);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
@@ -933,6 +945,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.clamp = 1;
     a.mute = h->mute;
     a.mute_fade = h->cfg.out_rate / 200;
+    audio_signal_level(h, a, o, buf, n);
     KTimer t(h, FMX_K_AUDIO, h->sD);
     if (!h->skip_audio && (rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
@@ -951,6 +964,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.clamp = 1;
     a.mute = h->mute;
     a.mute_fade = h->cfg.out_rate / 200;
+    audio_signal_level(h, a, o, buf, n);
     KTimer t(h, FMX_K_AUDIO, h->sD);
     if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";

@@ -56,9 +56,7 @@ struct FeArgs {
   int rds_stride;
   int *rds_count;    // [C]
   float *clip_out;   // [C]
-  fmx_signal_level *sig_out;  // [C] RF level (u8 inputs), may be null
-  const double *sig_par;      // [C][4] gain*factor, bias, floor, ceil
-  float *sig_smooth;          // [C][2] smoother value, initialized flag
+  unsigned long long *sig_sums; // [C][6] RF-level byte sums (u8 inputs; k_audio evaluates them), may be null
   unsigned long long *dbg;    // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
@@ -121,6 +119,13 @@ struct AudioArgs {
   int clamp;
   int *mute;       // [C][2] retune fade/mute {remaining, total} (main.cpp:1310-1337), may be null
   int mute_fade;   // OUTPUT_RATE / 200
+  // RF level of the step (computeSignalLevel / smoothSignalLevel) from the
+  // front end's byte sums, when sig_out is set
+  fmx_signal_level *sig_out;          // [C]
+  const unsigned long long *sig_sums; // [C][6]
+  long sig_samples;                   // IQ samples behind the sums
+  const double *sig_par;              // [C][4] gain*factor, bias, floor, ceil
+  float *sig_smooth;                  // [C][2] smoother value, initialized flag
 };
 
 struct RdsArgs {

@@ -392,11 +392,13 @@ struct SigAcc {
   }
 };
 
-// RF-level epilogue of a frontend workgroup (computeSignalLevel +
-// smoothSignalLevel, signal_level.cpp:145-214): block-reduce the exact byte
-// sums, then thread 0 evaluates the reference's formulas in double.
-__device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, unsigned long long *sgp, int c,
-                                                long samples, int lane, int wave, int tid) {
+// RF-level epilogue of a frontend workgroup: block-reduce the exact byte sums
+// of computeSignalLevel (signal_level.cpp:145-204) and store them; the
+// reference's double formulas run in k_audio (signal_level_eval), off the
+// front end's critical path (one f64 log10 per workgroup tail cost ~0.05 ms
+// per k_fe8 launch).
+__device__ __forceinline__ void fe_signal_sums(const FeArgs &a, SigAcc sig, unsigned long long *sgp, int c,
+                                               int lane, int wave, int tid) {
   sig.finish();
   unsigned long long v[6] = {sig.sI, sig.sQ, sig.sII, sig.sQQ, sig.hard, sig.nearc};
 #pragma unroll
@@ -405,9 +407,16 @@ __device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, uns
   if (lane == 0)
     for (int k = 0; k < 6; ++k) sgp[wave * 6 + k] = v[k];
   __syncthreads();
-  if (tid != 0) return;
+  if (tid < 6) a.sig_sums[6 * (size_t)c + tid] = sgp[tid] + sgp[6 + tid] + sgp[12 + tid] + sgp[18 + tid];
+}
+
+// computeSignalLevel + smoothSignalLevel (signal_level.cpp:145-214) of one
+// channel from its byte sums (t: sum I, sum Q, sum I^2, sum Q^2, hard-clip
+// and near-clip counts over `samples` IQ samples), in double as the reference
+__device__ __forceinline__ void signal_level_eval(const unsigned long long *sums, long samples, const double *sp,
+                                                  float *sm, fmx_signal_level *out) {
   double t[6];
-  for (int k = 0; k < 6; ++k) t[k] = (double)(sgp[k] + sgp[6 + k] + sgp[12 + k] + sgp[18 + k]);
+  for (int k = 0; k < 6; ++k) t[k] = (double)sums[k];
   fmx_signal_level r;
   r.level120 = 0.0f;
   r.dbfs = -120.0;
@@ -424,7 +433,7 @@ __device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, uns
     const double varI = fmax(0.0, (sumII / nn) - (meanI * meanI));
     const double varQ = fmax(0.0, (sumQQ / nn) - (meanQ * meanQ));
     const double rms = sqrt(fmax(1e-15, 0.5 * (varI + varQ)));
-    const double *sp = a.sig_par + 4 * (size_t)c;  // gain*factor, bias, floor, ceil
+    // sp: gain*factor, bias, floor, ceil
     r.dbfs = 20.0 * log10(rms + 1e-12);
     r.compensated_dbfs = r.dbfs - sp[0] + sp[1];
     const double safeCeil = fmax(sp[3], sp[2] + 1.0);
@@ -435,7 +444,6 @@ __device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, uns
     r.near_clip_ratio = t[5] / nn;
   }
   // smoothSignalLevel (signal_level.cpp:206-214)
-  float *sm = a.sig_smooth + 2 * (size_t)c;
   if (sm[1] == 0.0f) {
     sm[0] = r.level120;
     sm[1] = 1.0f;
@@ -444,7 +452,7 @@ __device__ __forceinline__ void fe_signal_level(const FeArgs &a, SigAcc sig, uns
     sm[0] += (r.level120 - sm[0]) * alpha;
   }
   r.level120_smoothed = sm[0];
-  a.sig_out[c] = r;
+  *out = r;
 }
 
 // LDS layout of k_frontend (shared with the launcher's size computation).
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
   float *rsh = reinterpret_cast<float *>(smem + LY::RSH);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
-  const bool want_sig = a.sig_out != nullptr && a.in_mode != FE_IN_CF && a.in_mode != FE_IN_MPX;
+  const bool want_sig = a.sig_sums != nullptr && a.in_mode != FE_IN_CF && a.in_mode != FE_IN_MPX;
   SigAcc sig;
   // diagnostic stage clock (thread 0's view, barrier waits included):
   // compiled only with -DFMX_STAMPS (make STAMPS=1) and read through
@@ -948,7 +956,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 #undef FE_STAMP
   if (tid == 0 && a.clip_out && a.in_mode != FE_IN_MPX)
     a.clip_out[c] = (n > 0) ? (float)sh->clip / (float)n : 0.0f;
-  if (want_sig) fe_signal_level(a, sig, sgp, c, (long)n * ((a.in_mode == FE_IN_U8_DECIM) ? M : 1), lane, wave, tid);
+  if (want_sig) fe_signal_sums(a, sig, sgp, c, lane, wave, tid);
 }
 
 /* ================================================================== */
@@ -1721,6 +1729,14 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const float dc_alpha = mono ? 0.0008f : 0.005f;
   const float de_a1 = -(1.0f - dalpha);
   const float dc_a1 = -1.0f + dc_alpha;
+  // the step's RF levels: workgroup b evaluates channels 256 b .. 256 b + 255
+  // from the front end's byte sums (one thread each)
+  if (a.sig_out && blockIdx.x * 256 < (unsigned)a.C) {
+    const int cs = blockIdx.x * 256 + tid;
+    if (cs < a.C)
+      signal_level_eval(a.sig_sums + 6 * (size_t)cs, a.sig_samples, a.sig_par + 4 * (size_t)cs,
+                        a.sig_smooth + 2 * (size_t)cs, a.sig_out + cs);
+  }
   // ---- carried state ----
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
@@ -3042,7 +3058,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const bool want_sig = a.sig_out != nullptr;
+  const bool want_sig = a.sig_sums != nullptr;
 #ifdef FMX_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
@@ -3151,7 +3167,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
-    FE_STAMP(7)
     // ================= decimator =================
 #if FMX_DEC_MFMA
     // the MFMA tap tables into the MPX image's chunk part (dead until the
@@ -3168,6 +3183,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
+    FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
     if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (full history)
       for (int h = tid; h < L; h += 256) {
         const int hh = h - 1;
@@ -3221,8 +3237,14 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         return __builtin_bit_cast(f16x2_t, __builtin_amdgcn_perm(0x64646464u, w, sel)) -
                f16x2_t{(_Float16)1152.0f, (_Float16)1152.0f};
       };
+#ifdef FMX_DIAG_DEC_KS
+      // diagnostic builds only: the MFMA loop cut to FMX_DIAG_DEC_KS steps (outputs invalid)
+#pragma unroll FMX_DEC_KS_UNROLL
+      for (int ks = 0; ks < FMX_DIAG_DEC_KS; ++ks) {
+#else
 #pragma unroll FMX_DEC_KS_UNROLL
       for (int ks = 0; ks < KS; ++ks) {
+#endif
         const u32x2 h0 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks);
         const u32x2 h1 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks + 2);
         const u32x2 l0 = *reinterpret_cast<const u32x2 *>(ta + FMX_DQ_N / 2 + 16 * ks);
@@ -3565,7 +3587,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, st_acc[k]);
 #endif
 #undef FE_STAMP
-  if (want_sig) fe_signal_level(a, sig, sgp, c, (long)n * M, lane, wave, tid);
+  if (want_sig) fe_signal_sums(a, sig, sgp, c, lane, wave, tid);
 }
 
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {

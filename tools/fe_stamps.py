@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 import fmx  # noqa: E402
 
-NAMES = ["decim", "dc", "iqfir+agc", "discrim", "pilot", "rds_rs", "carry", "tail"]
+NAMES = ["decim", "dc", "iqfir+agc", "discrim", "pilot", "rds_rs", "state_out", "setup+carry+dma_wait"]
 L = fmx.lib()
 L.fmx_debug_stamps.restype = C.c_int
 L.fmx_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
