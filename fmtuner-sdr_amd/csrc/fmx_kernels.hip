@@ -33,6 +33,14 @@
 #include "fmx_math.h"
 #include "fmx_synth.h"
 
+// k_rds's FIR partial sums: FMX_RDS_FMA (default) one packed FMA per product; 0 the
+// reference's separate multiply and add (its dotprod order, rounded twice).
+// The RDS path is held to bit-exact groups, not to bit-exact floats (its
+// mix-down sine is already the hardware one).
+#ifndef FMX_RDS_FMA
+#define FMX_RDS_FMA 1
+#endif
+
 namespace fmx {
 
 #define FE_T 768       // DSP samples per frontend chunk (256 threads x 3)
@@ -2146,13 +2154,7 @@ __device__ __forceinline__ void rds_taps8(const float *__restrict__ p, float (&t
   t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w;
   t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
 }
-// One FIR product into a partial sum.  FMX_RDS_FMA (default): one packed
-// FMA (v_pk_fma_f32); 0: the reference's separate multiply and add (its
-// dotprod order, rounded twice).  The RDS path is held to bit-exact groups,
-// not to bit-exact floats (its mix-down sine is already the hardware one).
-#ifndef FMX_RDS_FMA
-#define FMX_RDS_FMA 1
-#endif
+// One FIR product into a partial sum: FMX_RDS_FMA (fmx_kernels.hip top).
 __device__ __forceinline__ f32x2 rds_mac(float h, f32x2 m, f32x2 acc) {
 #if FMX_RDS_FMA
   return __builtin_elementwise_fma(f32x2{h, h}, m, acc);
@@ -3517,6 +3519,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #pragma unroll
           for (int m = 0; m < LY::RS_M; ++m) {
             const float v = xu[m];
+            // separate multiply and add (an FMA here measured no faster)
             const f32x2 p = hk[m] * f32x2{v, v};
             y = y + p;
           }
