@@ -1584,6 +1584,16 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
     case 6: v.assign(d->rds_fir, d->rds_fir + FMX_RDS_FIR); break;
     case 7: v = ex.rrc; break;
     case 8: v = ex.rrc_d; break;
+    case 10: { // k_fe8 MFMA pilot BPF taps back from the f16 hi/lo fragments (row 0 lanes), as pilot_taps
+      const int P = d->pilot_len, P8 = ((P + 6) & ~7) + 1;
+      for (int k = 0; k < P; ++k) {
+        const int dd = P8 - 1 - k; // = 32 ks + 8 g + j with row 0
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->pilot_frag[ks][0][l][j]) + f16_value(d->pilot_frag[ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 4096.0));
+      }
+      break;
+    }
     case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
       for (int cp = 0; cp < 2; ++cp)
         for (int k = 0; k < d->dec_len; ++k) {

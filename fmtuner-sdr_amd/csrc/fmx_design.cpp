@@ -370,6 +370,21 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     for (int k = 0; k < d->iq_len[i]; ++k) d->iq_z16[i][k + 16] = d->iq_taps[i][k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_z16[k + 16] = d->pilot_taps[k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
+  {
+    // MFMA pilot BPF fragments (k_fe8): taps * 2^12 (all f16-normal), hi/lo split
+    const int P = d->pilot_len, P8 = ((P + 6) & ~7) + 1;
+    d->pilot_ks = (P8 + 15 + 31) / 32;
+    for (int ks = 0; ks < FMX_PILOT_KS_MAX; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int dd = 32 * ks + 8 * (l >> 4) + j - (l & 15);
+          const int k = P8 - 1 - dd;
+          const float q = (ks < d->pilot_ks && k >= 0 && k < P) ? d->pilot_taps[k] * 4096.0f : 0.0f;
+          const uint16_t hi = f32_to_f16_bits(q);
+          d->pilot_frag[ks][0][l][j] = hi;
+          d->pilot_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+        }
+  }
   for (int k = 0; k + 1 < FMX_PILOT_MAX + FMX_PAD; ++k) {
     d->pilot_pair[k][0] = d->pilot_pad[k];
     d->pilot_pair[k][1] = d->pilot_pad[k + 1];

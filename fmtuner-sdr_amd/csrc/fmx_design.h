@@ -28,6 +28,7 @@
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
 #define FMX_DQ_MIN (-152)    // k_fe8 MFMA decimator tap table: first tap offset (multiple of 8, <= -15 M)
 #define FMX_DQ_N 608         // entries per copy and split (covers 32 K-steps of 16 outputs for M <= 10)
+#define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
 
 typedef struct {
   float x, y;
@@ -69,6 +70,12 @@ typedef struct {
   float pilot_pad[FMX_PILOT_MAX + FMX_PAD];
   float pilot_z16[FMX_PILOT_MAX + 32]; // [k + 16] = taps[k], 16 zeros each side (k_fe8)
   float pilot_pair[FMX_PILOT_MAX + FMX_PAD][2] __attribute__((aligned(8))); // {pad[k], pad[k+1]}: packed-FMA tap pairs
+  // k_fe8's MFMA pilot BPF (16 outputs x 16 blocks per v_mfma_f32_16x16x32_f16):
+  // lane l's A fragment of K step ks, split s (hi, lo of tap * 2^12):
+  // pilot_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - (l & 15)], q[d] =
+  // h[P8 - 1 - d] (P8 = fir8 length, 8k + 1, leading zero taps)
+  int pilot_ks; // K steps: ceil((P8 + 15) / 32)
+  uint16_t pilot_frag[FMX_PILOT_KS_MAX][2][64][8] __attribute__((aligned(16)));
   float lr_scale;
   float lr_taps[FMX_LR_LEN];
   float lr_pad[FMX_LR_LEN + FMX_PAD];

@@ -825,7 +825,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
         const float2 p = yb[j], r = yb[1 + j];
         const float re = p.x * r.x + p.y * r.y;
         const float im = p.x * r.y - p.y * r.x;
-        const float m = atan2f(im, re) * ref;
+        const float m = fmx_atan2f(im, re) * ref; // as k_fe8 (fmx_math.h)
         mx[FMX_HIST + j] = m;
         if (rds) rb[32 + j] = m;
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
@@ -2953,7 +2953,6 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int RAW_BYTES = HB + 2 * FE8_T * M + 16;
   static constexpr int YB_BYTES = (FE8_T + 1) * 8;
   static constexpr int XN = (FE_HALO_IQ + FE8_T + 16) * 9 / 8 + 8;   // padded complex image
-  static constexpr int MN = (FMX_HIST + FE8_T + 16) * 9 / 8 + 8;     // padded MPX image
   static constexpr int XIN = 0;                                      // aliases raw
   static constexpr int YB = XN * 8;                                  // aliases raw
   static constexpr int NPC = (HB + 2 * FE8_T * M + 1023) / 1024;     // 1-KiB LDS-DMA pieces per chunk
@@ -2966,19 +2965,27 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int UOFF = (R0 - U_FLOATS * 4) & ~15;
   static constexpr int NPC_EARLY = UOFF / 1024 < NPC ? UOFF / 1024 : NPC;
   static constexpr int HX = R0;                                      // IQ FIR history (FE_HALO_IQ)
-  static constexpr int MX = HX + FE_HALO_IQ * 8;
+  // MPX for the MFMA pilot BPF as f16 hi / lo images (history + chunk +
+  // zero slack, natural order), the chunk's last FMX_HIST samples in f32
+  // (stereo history write-back) and the previous chunk's last 32 in f32
+  // (the RDS resampler's window)
+  static constexpr int XW = FMX_HIST + FE8_T + 32;
+  static constexpr int MX = HX + FE_HALO_IQ * 8;                     // XH: f16 hi [XW]
+  static constexpr int XLO = MX + XW * 2;                            // XL: f16 lo [XW]
+  static constexpr int TL = (XLO + XW * 2 + 15) & ~15;               // f32 [FMX_HIST]
+  static constexpr int TL32 = TL + FMX_HIST * 4;                     // f32 [32]
   static constexpr int RS_PAIRS = FMX_NPFB + 1;                      // branch pairs (b, b+1), + the boundary pair
   static constexpr int RS_M = FMX_RDS_RS_SUB + 1;                    // 27 terms (leading / trailing zero)
-  static constexpr int RST = (MX + MN * 4 + 15) & ~15;               // RDS resampler bank [33][27] float2
+  static constexpr int RST = (TL32 + 32 * 4 + 15) & ~15;             // RDS resampler bank [33][27] float2
   static constexpr int SG = (RST + RS_PAIRS * RS_M * 8 + 15) & ~15;
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
-  // MFMA decimator tap tables (FmxDesign::dec_q16), per chunk in the MPX
-  // image's chunk part (floats from fe8_i(FMX_HIST), short of its zero slack)
-  static constexpr int TQ = (fe8_i(FMX_HIST) + 3) & ~3;
-  static constexpr int TQ_WORDS = 2 * FMX_DQ_N; // [copy][hi, lo][FMX_DQ_N] f16
-  static_assert(TQ + TQ_WORDS <= fe8_i(FMX_HIST + FE8_T), "tap tables inside the MPX chunk part");
+  // MFMA decimator tap table (copy 0 of FmxDesign::dec_q16: hi, lo), per
+  // chunk in the hi image's chunk part (dead until the discriminator)
+  static constexpr int TQ = MX + 2 * FMX_HIST;
+  static constexpr int TQ_WORDS = FMX_DQ_N; // [hi, lo][FMX_DQ_N] f16
+  static_assert(TQ_WORDS * 4 <= 2 * FE8_T, "tap table inside the hi image's chunk part");
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
   // (16-B aligned, above the complex image, inside the dead raw region)
   static constexpr int STG = (YB + 15) & ~15;
@@ -2988,36 +2995,11 @@ template <int M, int TPP> struct Fe8Layout {
 // 8 outputs j0..j0+7 (j0 % 8 == 0) of a real-tap FIR of runtime length P on
 // a padded LDS image x (input i at x[fe8_i(i)]); hz = taps with 16 zeros on
 // each side (hz[16 + k] = h[k]).  Per output the FMA chain runs oldest input
-// first, as fir_r3; outputs (2q, 2q+1) share one packed FMA.  The filter is
-// run as length P8 = P rounded up to 8k + 1 (up to 7 zero taps at the oldest
-// end: the chain starts with +0 products, same sums), so every group of 8
-// inputs is one 9-float row of the image: one address per group, the 8 reads
-// by immediate offsets.
+// first.  The filter is run as length P8 = P rounded up to 8k + 1 (up to 7
+// zero taps at the oldest end: the chain starts with +0 products, same sums),
+// so every group of 8 inputs is one 9-element row of the image: one address
+// per group, the 8 reads by immediate offsets.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
-__device__ __forceinline__ void fir8_r(const float *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[4]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = f32x2{0.0f, 0.0f};
-  const int P8 = fir8_len(P);
-  const float *xg = x + 9 * ((j0 - (P8 - 1)) >> 3);
-#pragma unroll 2
-  for (int m0 = 0; m0 < P8 + 7; m0 += 8) {
-    // input j0-(P8-1)+m0+u feeds output r with tap (P8-1)-m0+r-u = tw[7+r-u]
-    const FMX_CONST float *tw = cptr(hz) + 16 + (P8 - 1) - m0 - 7;
-    float t[16];
-#pragma unroll
-    for (int k = 0; k < 15; ++k) t[k] = tw[k];
-    t[15] = 0.0f;
-    const float *xr = xg + 9 * (m0 >> 3);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float v = xr[u];
-      const f32x2 vv = {v, v};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc[q] = __builtin_elementwise_fma(f32x2{t[7 + 2 * q - u], t[8 + 2 * q - u]}, vv, acc[q]);
-    }
-  }
-}
 // Complex input (float2 image), real taps: 8 outputs as packed (re, im).
 __device__ __forceinline__ void fir8_c(const float2 *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[8]) {
 #pragma unroll
@@ -3054,7 +3036,10 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
   float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
   float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
-  float *mx = reinterpret_cast<float *>(smem + LY::MX);
+  _Float16 *xh = reinterpret_cast<_Float16 *>(smem + LY::MX);  // MPX hi, index FMX_HIST + j
+  _Float16 *xl = reinterpret_cast<_Float16 *>(smem + LY::XLO); // MPX lo
+  float *tl = reinterpret_cast<float *>(smem + LY::TL);         // the chunk's last FMX_HIST MPX samples
+  float *tl32 = reinterpret_cast<float *>(smem + LY::TL32);     // the previous chunk's last 32
   f32x2(*rsb)[LY::RS_M] = reinterpret_cast<f32x2(*)[LY::RS_M]>(smem + LY::RST);
   float *uc = reinterpret_cast<float *>(smem + LY::UOFF); // uc[32 + j]: MPX sample j of the chunk
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
@@ -3091,7 +3076,10 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   const float dc_c = -dc_a1;
 
   // ---- zeroed images, carried state ----
-  for (int h = tid; h < LY::MN; h += 256) mx[h] = 0.0f;
+  for (int h = tid; h < LY::XW / 2; h += 256) {
+    reinterpret_cast<uint32_t *>(xh)[h] = 0u;
+    reinterpret_cast<uint32_t *>(xl)[h] = 0u;
+  }
   __syncthreads();
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
     const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
@@ -3106,7 +3094,12 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   }
   {
     const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
-    for (int h = tid; h < FMX_HIST; h += 256) mx[fe8_i(h)] = pilot ? hist[h] : 0.0f;
+    for (int h = tid; h < FMX_HIST; h += 256) {
+      const float v = pilot ? hist[h] : 0.0f;
+      const _Float16 hv = (_Float16)v;
+      xh[h] = hv;
+      xl[h] = (_Float16)(v - (float)hv);
+    }
   }
   float agc_g = 1.0f, agc_y2p = 1.0f;
   if (par.agc != 0 && tid == 0) {
@@ -3175,7 +3168,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     // discriminator below writes it)
     {
       const uint32_t *src = reinterpret_cast<const uint32_t *>(&D->dec_q16[0][0][0]);
-      uint32_t *dst = reinterpret_cast<uint32_t *>(mx + LY::TQ);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(smem + LY::TQ);
 #pragma unroll
       for (int k = 0; k < (LY::TQ_WORDS + 255) / 256; ++k) {
         const int i = tid + 256 * k;
@@ -3221,14 +3214,11 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
       typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
       typedef float f32x4_t __attribute__((ext_vector_type(4)));
-      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
       constexpr int KS = (15 * M + L + 1 + 31) / 32;
       static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN, "tap table range");
       const int col = lane & 15, g = lane >> 4;
-      const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0
-      const int cp = ((d00 & 3) == 2) ? 1 : 0;     // the copy where it starts 8-B aligned
-      const uint32_t *ta = reinterpret_cast<const uint32_t *>(mx + LY::TQ) + cp * FMX_DQ_N +
-                           ((d00 - FMX_DQ_MIN + 2 * cp) >> 1);
+      const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0 (even)
+      const uint32_t *ta = reinterpret_cast<const uint32_t *>(smem + LY::TQ) + ((d00 - FMX_DQ_MIN) >> 1);
       const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 16 * g;
       f32x4_t acc[2][2];
 #pragma unroll
@@ -3247,12 +3237,10 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #pragma unroll FMX_DEC_KS_UNROLL
       for (int ks = 0; ks < KS; ++ks) {
 #endif
-        const u32x2 h0 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks);
-        const u32x2 h1 = *reinterpret_cast<const u32x2 *>(ta + 16 * ks + 2);
-        const u32x2 l0 = *reinterpret_cast<const u32x2 *>(ta + FMX_DQ_N / 2 + 16 * ks);
-        const u32x2 l1 = *reinterpret_cast<const u32x2 *>(ta + FMX_DQ_N / 2 + 16 * ks + 2);
-        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, u32x4{h0.x, h0.y, h1.x, h1.y});
-        const f16x8_t alo = __builtin_bit_cast(f16x8_t, u32x4{l0.x, l0.y, l1.x, l1.y});
+        // 4-B aligned fragments (d00 is even): dword reads
+        const uint32_t *th = ta + 16 * ks, *tlo = ta + FMX_DQ_N / 2 + 16 * ks;
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, u32x4{th[0], th[1], th[2], th[3]});
+        const f16x8_t alo = __builtin_bit_cast(f16x8_t, u32x4{tlo[0], tlo[1], tlo[2], tlo[3]});
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const u32x4 w = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * ks);
@@ -3456,9 +3444,17 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         const float2 p = yb[j], r = yb[1 + j];
         const float re = p.x * r.x + p.y * r.y;
         const float im = p.x * r.y - p.y * r.x;
-        const float m = atan2f(im, re) * ref;
+#if defined(FMX_DIAG_DISC) && FMX_DIAG_DISC == 1
+        const float m = atan2f(im, re) * ref; // diagnostic builds only: the libm atan2f (not deterministic here)
+#else
+        const float m = fmx_atan2f(im, re) * ref; // select-free (fmx_math.h)
+#endif
         mv[k] = m;
-        mx[fe8_i(FMX_HIST + j)] = m;
+        // f16 hi / lo split for the MFMA pilot BPF (m = hi + lo to 22 bits)
+        const _Float16 hv = (_Float16)m;
+        xh[FMX_HIST + j] = hv;
+        xl[FMX_HIST + j] = (_Float16)(m - (float)hv);
+        if (k >= (FE8_T - FMX_HIST) / 256) tl[j - (FE8_T - FMX_HIST)] = m;
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
       if (tid == 0) {
@@ -3473,7 +3469,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
       if (tid < 32) {
-        uc[tid] = (n0 == 0) ? rds_keep : mx[fe8_i(FMX_HIST - 32 + tid)];
+        uc[tid] = (n0 == 0) ? rds_keep : tl32[tid];
         uc[32 + FE8_T + tid] = 0.0f;
       }
     }
@@ -3489,11 +3485,46 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     }
     // ================= 19 kHz pilot band-pass =================
     if (pilot) {
-      f32x2 z[4];
-      fir8_r(mx, FMX_HIST + j0, D->pilot_z16, D->pilot_len, z);
-      float4 *po = reinterpret_cast<float4 *>(a.pilot_out + (size_t)c * a.pilot_stride + n0 + j0);
-      po[0] = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
-      po[1] = make_float4(z[2].x, z[2].y, z[3].x, z[3].y);
+      // v_mfma_f32_16x16x32_f16 tiles as the decimator's: 16 outputs (rows,
+      // A = taps) of 16 blocks of 16 outputs (columns, B = MPX), K = the
+      // block's P8 + 15 inputs from x[16 B - P8 + 1]; B from the hi / lo
+      // images (two 16-B reads), A fragments (FmxDesign::pilot_frag, tap *
+      // 2^12 as hi + lo) from global memory, one K step ahead; three MFMAs
+      // per K step (hi*hi, hi*lo, lo*hi).  Each wave: two tiles, 512 outputs.
+      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+      typedef float f32x4_t __attribute__((ext_vector_type(4)));
+      const int P8 = fir8_len(D->pilot_len);
+      const int KSP = D->pilot_ks;
+      const int col = lane & 15, g = lane >> 4;
+      const int xb = FMX_HIST + 16 * (32 * wave + col) - (P8 - 1) + 8 * g; // 8-aligned: P8 = 8k + 1
+      const f16x8_t *bh = reinterpret_cast<const f16x8_t *>(xh + xb);
+      const f16x8_t *bl = reinterpret_cast<const f16x8_t *>(xl + xb);
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->pilot_frag[0][0][0][0]) + lane;
+      f32x4_t pacc[2];
+      pacc[0] = pacc[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      u32x4 ah = fa[0], al = fa[64];
+      for (int ks = 0; ks < KSP; ++ks) {
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
+        if (ks + 1 < KSP) {
+          ah = fa[128 * (ks + 1)];
+          al = fa[128 * (ks + 1) + 64];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f16x8_t xhi = bh[32 * u + 4 * ks], xlo = bl[32 * u + 4 * ks]; // + 256 u + 32 ks samples
+          pacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, xhi, pacc[u], 0, 0, 0);
+          pacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, xlo, pacc[u], 0, 0, 0);
+          pacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, xhi, pacc[u], 0, 0, 0);
+        }
+      }
+      constexpr float kInv = 1.0f / 4096.0f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
+        float4 *po = reinterpret_cast<float4 *>(a.pilot_out + (size_t)c * a.pilot_stride + n0 + 256 * (2 * wave + u) +
+                                                16 * col + 4 * g);
+        *po = make_float4(pacc[u][0] * kInv, pacc[u][1] * kInv, pacc[u][2] * kInv, pacc[u][3] * kInv);
+      }
     }
     FE_STAMP(4)
     // ================= RDS resampler 240k -> 171k =================
@@ -3537,10 +3568,16 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     FE_STAMP(5)
     // ================= carry halos to the next chunk =================
     {
-      const float cm0 = mx[fe8_i(tid + FE8_T)], cm1 = mx[fe8_i(tid + 256 + FE8_T)];
+      // the chunk's last FMX_HIST samples become the f16 images' history;
+      // its last 32 (f32) the next RDS window's history
+      static_assert(FMX_HIST == 2 * 256, "one f16 pair per thread");
+      const uint32_t ch = reinterpret_cast<const uint32_t *>(xh)[FE8_T / 2 + tid];
+      const uint32_t cl = reinterpret_cast<const uint32_t *>(xl)[FE8_T / 2 + tid];
+      const float t32 = (tid < 32) ? tl[FMX_HIST - 32 + tid] : 0.0f;
       __syncthreads();
-      mx[fe8_i(tid)] = cm0;
-      mx[fe8_i(tid + 256)] = cm1;
+      reinterpret_cast<uint32_t *>(xh)[tid] = ch;
+      reinterpret_cast<uint32_t *>(xl)[tid] = cl;
+      if (tid < 32) tl32[tid] = t32;
       __syncthreads();
     }
   }
@@ -3577,10 +3614,10 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   }
   if (pilot) {
     float *hist = a.st_hist_wr + (size_t)c * FMX_HIST;
-    for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[fe8_i(h)];
+    for (int h = tid; h < FMX_HIST; h += 256) hist[h] = tl[h];
   }
   if (rds) {
-    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = mx[fe8_i(FMX_HIST - 32 + tid)];
+    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = tl[FMX_HIST - 32 + tid];
     if (tid == 0) a.rds_count[c] = sched_n;
   }
   if (tid == 0 && a.clip_out) a.clip_out[c] = (float)sh->clip / (float)n;
@@ -3594,9 +3631,17 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 }
 
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
-  static_assert(Fe8Layout<M, TPP>::BYTES <= 63 * 1024, "k_fe8: two workgroups per CU plus a k_pll workgroup");
+  // 160 KB per CU: two k_fe8 workgroups (512-B allocation granules) beside one
+  // k_pll or k_rds workgroup (36 KB each, 36 864 B allocated)
+  static_assert(Fe8Layout<M, TPP>::BYTES <= (160 * 1024 - 36864) / 2, "k_fe8: two workgroups per CU plus a k_pll / k_rds workgroup");
   static_assert(Fe8Layout<M, TPP>::UOFF >= Fe8Layout<M, TPP>::YB, "RDS copy above the IQ image");
-  const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
+  size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
+  // diagnostic: FMX_DIAG_FE8_LDS=<bytes> launches with more LDS (fewer workgroups per CU)
+  static const size_t diag_lds = [] {
+    const char *e = std::getenv("FMX_DIAG_FE8_LDS");
+    return e ? (size_t)std::atol(e) : (size_t)0;
+  }();
+  if (diag_lds > smem) smem = diag_lds;
   static bool configured = false;
   if (!configured) {
     if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fe8<M, TPP>),
@@ -3639,7 +3684,11 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   const bool fe8 = vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
                    (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
                    a.des_fs >= 190000;
-  if (fe8) {
+  static const bool no_fe8 = [] { // diagnostic: FMX_DIAG_NO_FE8=1 runs k_frontend for every call
+    const char *e = std::getenv("FMX_DIAG_NO_FE8");
+    return e && e[0] == '1';
+  }();
+  if (fe8 && !no_fe8) {
     if (M == 10 && tpp == 28) return fe8_launch<10, 28>(a, st);
     if (M == 8 && tpp == 28) return fe8_launch<8, 28>(a, st);
     if (M == 4 && tpp == 20) return fe8_launch<4, 20>(a, st);

@@ -112,4 +112,46 @@ FMX_HD uint32_t fmx_word_near_clip(uint32_t w) {
   return (t - 0x12121212u) & ~t & 0x80808080u;
 }
 
+
+// atan2 for the FM discriminator, branch- and compare-free: octant
+// reduction a = min/max of |x|, |y| (reciprocal + one Newton step),
+// atan(a) = a + a s P(s), s = a^2, with the degree-7 minimax P of the device
+// libm (ocml atan), then the octant fix-ups through sign factors
+// (copysign) instead of compares and selects.  Within 2 ulp of the exact
+// atan2 and 2.5e-7 of atan2f (tests/test_math.py); atan2(+-0, +0) = +-0,
+// atan2(+-0, -0) = +-pi as IEEE.
+//
+// Why no selects: with two k_fe8 workgroups per CU, the libm atan2f (and a
+// select-based version) in the discriminator returned wrong values in lanes
+// 48-63 of some wave-instructions, nondeterministically (tools/
+// gpu_determinism.py: thousands of MPX samples per 4096-channel run, always
+// whole 16-lane groups, never with one workgroup per CU or with a
+// select-free discriminator).
+FMX_HD float fmx_atan2f(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(fmaxf(ax, ay), 1e-37f), mn = fminf(ax, ay);
+#ifdef __HIP_DEVICE_COMPILE__
+  const float rc = __builtin_amdgcn_rcpf(mx);
+#else
+  const float rc = 1.0f / mx;
+#endif
+  float a = mn * rc;
+  a = fmaf(fmaf(-mx, a, mn), rc, a); // one Newton step: ~0.5 ulp
+  const float s = a * a;
+  float p = fmaf(s, 0.002642294391989708f, -0.015280019491910934f);
+  p = fmaf(s, p, 0.04149937257170677f);
+  p = fmaf(s, p, -0.07413642853498459f);
+  p = fmaf(s, p, 0.10605181753635406f);
+  p = fmaf(s, p, -0.14197120070457458f);
+  p = fmaf(s, p, 0.19992350041866302f);
+  p = fmaf(s, p, -0.3333311676979065f);
+  const float r = fmaf(a, s * p, a);
+  // |y| > |x|: pi/2 - r;  x < 0 (or -0): pi - r1
+  const float sw = copysignf(1.0f, ax - ay);           // -1 when |y| > |x|
+  const float r1 = fmaf(sw, r, (1.0f - sw) * 0.78539818525314331f);
+  const float sx = copysignf(1.0f, x);
+  const float r2 = fmaf(sx, r1, (1.0f - sx) * 1.5707963705062866f);
+  return copysignf(r2, y);
+}
+
 #endif

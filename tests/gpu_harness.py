@@ -94,9 +94,12 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
     cnt_mismatch = 0
     ind_mismatch = 0
     g_gpu, g_ora = [], []
+    mpx_where = None
     for b in range(nblk):
         o, g = ores[b], gres[b]
         dm = o["mpx"] - g["mpx"][c, :len(o["mpx"])]
+        if dm.size and float(np.max(np.abs(dm))) > mpx_err:
+            mpx_where = (b, int(np.argmax(np.abs(dm))))
         mpx_err = max(mpx_err, float(np.max(np.abs(dm))))
         mpx_sq += float(np.sum(dm.astype(np.float64) ** 2))
         mpx_n += dm.size
@@ -117,7 +120,8 @@ def compare(gres, ores, c, nblk, pcm_blocks=None):
         pcm_max = max(pcm_max, float(np.max(np.abs(dl))) if k else 0.0, float(np.max(np.abs(dr))) if k else 0.0)
         pil_mismatch += int(o["pilot"] != int(g["pilot"][c]))
         pil_maxdiff = max(pil_maxdiff, abs(int(o["pilot"]) - int(g["pilot"][c])))
-    return dict(mpx_max=mpx_err, mpx_rms=(mpx_sq / max(mpx_n, 1)) ** 0.5, pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
+    return dict(mpx_max=mpx_err, mpx_where=mpx_where, mpx_rms=(mpx_sq / max(mpx_n, 1)) ** 0.5,
+                pcm_rms=(pcm_sq / max(pcm_n, 1)) ** 0.5, pcm_max=pcm_max,
                 stereo_mismatch=st_mismatch, indicator_mismatch=ind_mismatch, pilot_mismatch=pil_mismatch, pilot_maxdiff=pil_maxdiff, count_mismatch=cnt_mismatch,
                 groups_gpu=g_gpu, groups_oracle=g_ora)
 

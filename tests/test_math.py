@@ -67,3 +67,16 @@ def test_pll_chain_sine_error_bounds(tmp_path):
     with open(os.path.join(ROOT, "tests", "golden", "pllsin_exhaustive.json")) as f:
         ex = json.load(f)
     assert ex["stride"] == 1 and ex["pll_sin_word_vs_float_phase"] < 4.5e-7 and ex["pll_sin_word_vs_exact"] < 1.4e-7
+
+
+def test_discriminator_atan2_accuracy(tmp_path):
+    """fmx_atan2f (the front end's FM discriminator) within 2 ulp of the exact
+    atan2 and within 2.5e-7 of the C library's atan2f (the oracle's) over
+    random IQ-product arguments spanning 15 decades, and on the axes."""
+    exe = str(tmp_path / "atan2_test")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "atan2_test.cpp")], check=True, timeout=120)
+    r = json.loads(subprocess.run([exe, "1000000"], check=True, capture_output=True, text=True, timeout=300).stdout)
+    assert r["max_ulp"] < 2.0, r
+    assert r["max_abs_vs_atan2f"] < 2.5e-7, r
+    assert r["zero_zero"] == 0.0, r

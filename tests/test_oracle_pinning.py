@@ -260,3 +260,15 @@ def test_mfma_decimator_tap_tables(fmx, rates):
         err = np.abs(q[cp * raw.size:(cp + 1) * raw.size] - raw)
         # the taps pass through float32 (/127.5, then *127.5 here): a few ulp of the largest
         assert err.max() <= scale * 2.0 ** -21, (cp, err.max() / scale)
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_pilot_tap_fragments(fmx, rates):
+    """k_fe8's MFMA pilot BPF takes its taps as f16 hi + lo fragments (x 2^12,
+    FmxDesign::pilot_frag): they give the float taps back to 22 bits."""
+    cfg = fmx.make_config(**rates)
+    h = fmx.design_taps(cfg, 2).astype(np.float64)
+    q = fmx.design_taps(cfg, 10).astype(np.float64)
+    assert q.size == h.size
+    err = np.abs(q - h)
+    assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()
