@@ -80,6 +80,7 @@ struct Handle {
   hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr;
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
+  bool lr_rows = false; // raw L/R in rows instead of octet tiles (FMX_LR_ROWS=1)
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -582,6 +583,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   // k_pll / k_rds waves run at raised issue priority beside the front end's
   // (measured 1.39 -> 1.375 ms/step); FMX_SERIAL_PRIO=0 turns it off
   h->serial_prio = 1;
+  // FMX_LR_ROWS=1: raw L/R in [C][block] rows instead of octet tiles (A/B runs)
+  if (const char *e = std::getenv("FMX_LR_ROWS"); e && e[0] == '1') h->lr_rows = true;
   if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
@@ -690,8 +693,9 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->pilot[b], C * B)) != FMX_OK) return rc;
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
-    if ((rc = dalloc(h, &h->lraw[b], C * B)) != FMX_OK) return rc;
-    if ((rc = dalloc(h, &h->rraw[b], C * B)) != FMX_OK) return rc;
+    // octet tiles: whole groups of 8 channels
+    if ((rc = dalloc(h, &h->lraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
   }
   if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
@@ -774,6 +778,9 @@ static void audio_signal_level(Handle *h, AudioArgs &a, const fmx_block_out *o, 
   a.sig_smooth = h->sig_smooth;
 }
 
+// raw L/R (k_pll -> k_audio) in octet tiles when the block is whole 4-sample tiles
+static int lr_tiled(const Handle *h) { return (h->cfg.block % 4 == 0 && !h->lr_rows) ? 1 : 0; }
+
 static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
   PllArgs a{};
   a.des = h->ddes;
@@ -788,6 +795,7 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lraw = h->lraw[buf];
   a.rraw = h->rraw[buf];
   a.lr_stride = h->cfg.block;
+  a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
   a.prio = h->serial_prio;
@@ -937,6 +945,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.in_l = h->lraw[buf];
     a.in_r = h->rraw[buf];
     a.in_stride = h->cfg.block;
+    a.in_tiled = lr_tiled(h);
     a.out_l = o->d_pcm_l;
     a.out_r = o->d_pcm_r;
     a.out_stride = o->pcm_stride;
@@ -1311,6 +1320,7 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
     a.in_l = h->lraw[buf];
     a.in_r = h->rraw[buf];
     a.in_stride = h->cfg.block;
+    a.in_tiled = lr_tiled(h);
     a.lr_out_l = d_left;
     a.lr_out_r = d_right;
     a.lr_out_stride = lr_stride;

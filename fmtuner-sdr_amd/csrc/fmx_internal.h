@@ -88,6 +88,7 @@ struct PllArgs {
   const float *st_hist_rd; // [C][FMX_HIST] history the frontend of this call read
   float *lraw, *rraw;
   int lr_stride;
+  int lr_tiled;            // raw L/R in octet tiles (lr_tile_idx, fmx_kernels.hip), else [C][lr_stride]
   FmxStereoState *st;
   int *stereo_out, *pilot_tenths_out;
   int *indicator_out;      // [C] XDR stereo indicator (main.cpp:1298-1300), may be null
@@ -102,6 +103,7 @@ struct AudioArgs {
   int cap;
   const float *in_l, *in_r;
   int in_stride;
+  int in_tiled;    // in_l / in_r in octet tiles (raw L/R from k_pll), else [C][in_stride]
   float *out_l, *out_r;
   int out_stride;
   int *out_count;

@@ -71,13 +71,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 
 /* ------------------------------------------------------------------ */
 /* liquid NCO fixed-point helpers (nco.proto.c restated)               */
-__device__ __forceinline__ uint32_t d_nco_constrain(float x) {
-  const float p = (float)((double)x * 0.159154943091895);
-  float fpart = p - truncf(p);
-  if (fpart < 0.0f) fpart = (float)((double)fpart + 1.0);
-  const float s = fpart * 4294967296.0f;
-  return (s >= 4294967296.0f) ? 0u : (uint32_t)s;
-}
+// fmx_nco_constrain (fmx_math.h): one floor instead of trunc / compare / add,
+// bit-identical to the reference form for every float (exhaustive host check)
+__device__ __forceinline__ uint32_t d_nco_constrain(float x) { return fmx_nco_constrain(x); }
 __device__ __forceinline__ float d_nco_phase(uint32_t theta) {
   // (2pi * theta) / 2^32 in double: the power-of-two scaling is exact, so it
   // is folded into the constant (one v_mul_f64, same rounding)
@@ -94,6 +90,27 @@ __device__ __forceinline__ float d_unwrap(float x) {
 }
 __device__ __forceinline__ float d_clamp(float v, float lo, float hi) {
   return (v < lo) ? lo : ((hi < v) ? hi : v);
+}
+
+/* ------------------------------------------------------------------ */
+// Raw L/R between k_pll and k_audio in octet tiles: sample t of channel c at
+// ((c / 8) * (stride / 4) + t / 4) * 32 + (c % 8) * 4 + t % 4, i.e. one
+// 128-B line holds 4 consecutive samples of 8 consecutive channels.  k_pll's
+// lane = channel stores of a 4-sample tile then write whole lines (with one
+// row per channel every store instruction wrote a 16-B piece of 64 lines,
+// and HBM saw ~1.8x the bytes); stride % 4 == 0.
+__device__ __forceinline__ size_t lr_tile_idx(int c, int t, int stride) {
+  return ((size_t)(c >> 3) * (size_t)(stride >> 2) + (size_t)(t >> 2)) * 32 + (size_t)((c & 7) * 4 + (t & 3));
+}
+// k_audio's block -> channel order for tiled input: blocks b and b + 8 share
+// an XCD (observed round-robin dispatch, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so the 8 channels of one octet go to blocks 8 apart and their
+// reads of each shared line hit that XCD's L2 after the first.  Channels past
+// the last whole 64 keep b -> b.  Placement only: any order is correct.
+__device__ __forceinline__ int au_channel(int b, int C, bool tiled) {
+  if (!tiled || b >= (C & ~63)) return b;
+  const int x = b & 7, i = b >> 3;
+  return ((i >> 3) << 6) | (x << 3) | (i & 7);
 }
 
 /* ================================================================== */
@@ -1504,8 +1521,12 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
           }
         }
         if (act) {
-          float *ol = a.lraw + (size_t)c * a.lr_stride + kt * PLL_T;
-          float *orr = a.rraw + (size_t)c * a.lr_stride + kt * PLL_T;
+          // octet tiles (lr_tile_idx): the 8 lanes of a channel octet fill
+          // one 128-B line, a store instruction writes 8 whole lines
+          const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T, a.lr_stride)
+                                       : (size_t)c * a.lr_stride + kt * PLL_T;
+          float *ol = a.lraw + ob;
+          float *orr = a.rraw + ob;
           if (cnt == PLL_T && ((((uintptr_t)ol) | ((uintptr_t)orr)) & 15) == 0) {
 #pragma unroll
             for (int q = 0; q < PLL_T / 4; ++q) {
@@ -1722,7 +1743,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   // allocation from 111 to 129 (occupancy 3 by LDS)
   extern __shared__ __align__(16) unsigned char au_smem[];
   AuShared &S = *reinterpret_cast<AuShared *>(au_smem);
-  const int c = blockIdx.x;
+  const int c = au_channel(blockIdx.x, a.C, a.in_tiled != 0);
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
   const FmxChanParam par = a.par[c];
@@ -1780,8 +1801,11 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   }
   if (lrfir)
     for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
-  const float *inl = a.in_l + (size_t)c * a.in_stride;
-  const float *inr = mono ? nullptr : a.in_r + (size_t)c * a.in_stride;
+  // tiled input (raw L/R from k_pll): sample j of this channel at tin + ti(j)
+  const bool tiled = a.in_tiled != 0;
+  const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
+  const float *inr = mono ? nullptr : a.in_r + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
+  auto ti = [&](int j) __attribute__((always_inline)) { return tiled ? (j >> 2) * 32 + (j & 3) : j; };
   const float sc = D->lr_scale;
   // retune fade/mute of this call (main.cpp:1310-1337): outputs o < mrem
   // get the gain of position (mtot - mrem) + o of the fade-out/mute/fade-in
@@ -1810,8 +1834,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {
         const int j = tid + 256 * k;
-        vl[k] = (j < cnt) ? inl[n0 + j] : 0.0f;
-        vr[k] = (j < cnt && !mono) ? inr[n0 + j] : 0.0f;
+        vl[k] = (j < cnt) ? inl[ti(n0 + j)] : 0.0f;
+        vr[k] = (j < cnt && !mono) ? inr[ti(n0 + j)] : 0.0f;
       }
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {

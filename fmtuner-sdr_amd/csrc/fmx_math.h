@@ -76,6 +76,38 @@ FMX_HD float fmx_div_const(float x, float c, float rc) {
   return fmaf(r, rc, q);
 }
 
+// liquid's NCO constrain (nco.proto.c, as the oracle's lq::nco_constrain):
+//   p = (float)((double)x / 2pi);  f = p - truncf(p);  f < 0: f = (float)((double)f + 1);
+//   s = f * 2^32;  s >= 2^32 ? 0 : (uint32)s
+// restated with one floor: f = p - floorf(p) is the exact value of the
+// reference's fpart (+1 when negative) rounded once to float, which equals the
+// double add rounded to float (that add is exact unless |fpart| < 2^-29, where
+// both round to 1.0).  f == 1.0 is the only s >= 2^32 case and its compare is
+// off the dependency chain; the device's v_cvt_u32_f32 maps NaN to 0 as the
+// reference's conversion does on the GPU.  Checked bit for bit against the
+// reference form over all 2^32 inputs (tests/cpp/ncoconstrain_test.cpp).
+FMX_HD uint32_t fmx_cvt_u32(float s) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return (uint32_t)s;
+#else
+  return (s != s || s <= 0.0f) ? 0u : (s >= 4294967296.0f ? 0xFFFFFFFFu : (uint32_t)s);
+#endif
+}
+FMX_HD uint32_t fmx_nco_constrain(float x) {
+  const float p = (float)((double)x * 0.159154943091895);
+  const float f = p - floorf(p);
+  const uint32_t u = fmx_cvt_u32(f * 4294967296.0f);
+  return (f == 1.0f) ? 0u : u;
+}
+// the reference form, for the host check
+FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
+  const float p = (float)((double)x * 0.159154943091895);
+  float fpart = p - truncf(p);
+  if (fpart < 0.0f) fpart = (float)((double)fpart + 1.0);
+  const float s = fpart * 4294967296.0f;
+  return (s >= 4294967296.0f) ? 0u : fmx_cvt_u32(s);
+}
+
 // Quadrant count of an NCO phase word: round(theta / 2^30) in 0..4, the
 // quadrant of the exact phase 2 pi theta / 2^32.  The float phase the
 // reference computes from theta is within 0.5 ulp of it, so fmx_sincos_q of

@@ -1,0 +1,45 @@
+// ncoconstrain_test.cpp -- fmx_nco_constrain (fmtuner-sdr_amd/csrc/fmx_math.h,
+// the kernels' NCO phase-increment constrain: k_pll's PLL chain,
+// stereo_decoder.cpp:254-256, and k_rds's PSK loop, subcarrier.cpp:205-209)
+// against the reference form fmx_nco_constrain_ref (liquid nco.proto.c, as
+// oracle/fmx_oracle.cpp's lq::nco_constrain) for every float bit pattern
+// (NaN and Inf included; the conversion follows the device's v_cvt_u32_f32).
+// Prints JSON {"checked": N, "mismatches": M, "first": [...]}.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../fmtuner-sdr_amd/csrc/fmx_math.h"
+
+static float bits2f(uint32_t u) {
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+int main(int argc, char **argv) {
+  const long long stride = (argc > 1) ? std::atoll(argv[1]) : 1;
+  unsigned long long checked = 0, bad = 0;
+  uint32_t first[4] = {0, 0, 0, 0};
+#pragma omp parallel for reduction(+ : checked, bad) schedule(static)
+  for (long long i = 0; i < (1LL << 32); i += stride) {
+    const float x = bits2f((uint32_t)i);
+    checked++;
+    if (fmx_nco_constrain(x) != fmx_nco_constrain_ref(x)) {
+      bad++;
+#pragma omp critical
+      {
+        for (int k = 0; k < 4; ++k)
+          if (first[k] == 0) {
+            first[k] = (uint32_t)i;
+            break;
+          }
+      }
+    }
+  }
+  std::printf("{\"stride\": %lld, \"checked\": %llu, \"mismatches\": %llu, \"first\": [%u, %u, %u, %u]}\n", stride,
+              checked, bad, first[0], first[1], first[2], first[3]);
+  return 0;
+}
