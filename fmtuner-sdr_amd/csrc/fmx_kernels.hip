@@ -74,11 +74,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 // fmx_nco_constrain (fmx_math.h): one floor instead of trunc / compare / add,
 // bit-identical to the reference form for every float (exhaustive host check)
 __device__ __forceinline__ uint32_t d_nco_constrain(float x) { return fmx_nco_constrain(x); }
-__device__ __forceinline__ float d_nco_phase(uint32_t theta) {
-  // (2pi * theta) / 2^32 in double: the power-of-two scaling is exact, so it
-  // is folded into the constant (one v_mul_f64, same rounding)
-  return (float)((double)(float)theta * (6.283185307179586 / 4294967296.0));
-}
+// (2pi * theta) / 2^32 as the reference rounds it, in float (fmx_math.h)
+__device__ __forceinline__ float d_nco_phase(uint32_t theta) { return fmx_nco_phase(theta); }
 // x / c by fmx_div_const (fmx_math.h), for the divisors whose exactness
 // against IEEE x / c tests/cpp/divconst_test.cpp checks exhaustively
 __device__ __forceinline__ float d_div_const(float x, float c, float rc) { return fmx_div_const(x, c, rc); }

@@ -99,6 +99,21 @@ FMX_HD uint32_t fmx_nco_constrain(float x) {
   const uint32_t u = fmx_cvt_u32(f * 4294967296.0f);
   return (f == 1.0f) ? 0u : u;
 }
+// liquid's NCO phase of a word as the reference computes it,
+// (float)(2 pi (double)(float)theta / 2^32), in float arithmetic: the product
+// of (float)theta and the double constant K = 2 pi / 2^32 as Kh + Kl with the
+// exact FMA residual, rounded once.  Bit-identical to the double form for all
+// 2^32 words (tests/cpp/ncoconstrain_test.cpp); 5 full-rate VALU instead of
+// two double conversions and a double multiply.
+FMX_HD float fmx_nco_phase(uint32_t theta) {
+  const float t = (float)theta;
+  const float ph = t * 0x1.921fb6p-30f;
+  const float e = fmaf(t, 0x1.921fb6p-30f, -ph);
+  return ph + fmaf(t, -0x1.777a5cp-55f, e);
+}
+FMX_HD float fmx_nco_phase_ref(uint32_t theta) {
+  return (float)((double)(float)theta * (6.283185307179586 / 4294967296.0));
+}
 // the reference form, for the host check
 FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
   const float p = (float)((double)x * 0.159154943091895);

@@ -4,7 +4,9 @@
 // against the reference form fmx_nco_constrain_ref (liquid nco.proto.c, as
 // oracle/fmx_oracle.cpp's lq::nco_constrain) for every float bit pattern
 // (NaN and Inf included; the conversion follows the device's v_cvt_u32_f32).
-// Prints JSON {"checked": N, "mismatches": M, "first": [...]}.
+// Also fmx_nco_phase (the NCO phase of a word in float arithmetic) against
+// the reference's double form, for every word.
+// Prints JSON {"checked": N, "mismatches": M, "phase_mismatches": P, "first": [...]}.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -21,12 +23,14 @@ static float bits2f(uint32_t u) {
 
 int main(int argc, char **argv) {
   const long long stride = (argc > 1) ? std::atoll(argv[1]) : 1;
-  unsigned long long checked = 0, bad = 0;
+  unsigned long long checked = 0, bad = 0, bad_phase = 0;
   uint32_t first[4] = {0, 0, 0, 0};
-#pragma omp parallel for reduction(+ : checked, bad) schedule(static)
+#pragma omp parallel for reduction(+ : checked, bad, bad_phase) schedule(static)
   for (long long i = 0; i < (1LL << 32); i += stride) {
     const float x = bits2f((uint32_t)i);
     checked++;
+    const float pa = fmx_nco_phase((uint32_t)i), pb = fmx_nco_phase_ref((uint32_t)i);
+    if (std::memcmp(&pa, &pb, 4) != 0) bad_phase++;
     if (fmx_nco_constrain(x) != fmx_nco_constrain_ref(x)) {
       bad++;
 #pragma omp critical
@@ -39,7 +43,7 @@ int main(int argc, char **argv) {
       }
     }
   }
-  std::printf("{\"stride\": %lld, \"checked\": %llu, \"mismatches\": %llu, \"first\": [%u, %u, %u, %u]}\n", stride,
-              checked, bad, first[0], first[1], first[2], first[3]);
+  std::printf("{\"stride\": %lld, \"checked\": %llu, \"mismatches\": %llu, \"phase_mismatches\": %llu, \"first\": [%u, %u, %u, %u]}\n", stride,
+              checked, bad, bad_phase, first[0], first[1], first[2], first[3]);
   return 0;
 }

@@ -85,13 +85,14 @@ def test_discriminator_atan2_accuracy(tmp_path):
 def test_nco_constrain_floor_form_is_exact(tmp_path):
     """fmx_nco_constrain (the kernels' NCO constrain: one floor instead of the
     reference's trunc / compare / double add) returns the reference form's
-    word for every float.  Exhaustive over all 2^32 bit patterns:
+    word for every float, and fmx_nco_phase (the phase of a word in float
+    arithmetic) the reference's double-rounded phase for every word.  Exhaustive over all 2^32 bit patterns:
     tests/golden/ncoconstrain_exhaustive.json; this runs every 13th."""
     exe = str(tmp_path / "ncoconstrain_test")
     subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17", "-o", exe,
                     os.path.join(ROOT, "tests", "cpp", "ncoconstrain_test.cpp")], check=True, timeout=120)
     r = json.loads(subprocess.run([exe, "13"], check=True, capture_output=True, text=True, timeout=600).stdout)
-    assert r["mismatches"] == 0 and r["checked"] > 3 * 10**8, r
+    assert r["mismatches"] == 0 and r["phase_mismatches"] == 0 and r["checked"] > 3 * 10**8, r
     with open(os.path.join(ROOT, "tests", "golden", "ncoconstrain_exhaustive.json")) as f:
         ex = json.load(f)
-    assert ex["stride"] == 1 and ex["checked"] == 2**32 and ex["mismatches"] == 0
+    assert ex["stride"] == 1 and ex["checked"] == 2**32 and ex["mismatches"] == 0 and ex["phase_mismatches"] == 0
