@@ -1604,6 +1604,18 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
+    case 11: { // k_fe8 MFMA IQ FIR taps back from the f16 hi/lo fragments (row 0 lanes), as case 1
+      const int sel = bandwidth_select(cfg->bandwidth_hz, std::clamp(cfg->w0_bandwidth_hz, 0, 400000));
+      const int idx = (sel == 0) ? FMX_IQ_CTOR : sel;
+      const int P = d->iq_len[idx], P8 = ((P + 6) & ~7) + 1;
+      for (int k = 0; k < P; ++k) {
+        const int dd = P8 - 1 - k;
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->iq_frag[idx][ks][0][l][j]) + f16_value(d->iq_frag[idx][ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 4096.0));
+      }
+      break;
+    }
     case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
       for (int cp = 0; cp < 2; ++cp)
         for (int k = 0; k < d->dec_len; ++k) {

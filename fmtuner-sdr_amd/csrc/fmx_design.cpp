@@ -368,6 +368,21 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     for (int k = 0; k < d->iq_len[i]; ++k) d->iq_pad[i][k + 5] = d->iq_taps[i][k];
   for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
     for (int k = 0; k < d->iq_len[i]; ++k) d->iq_z16[i][k + 16] = d->iq_taps[i][k];
+  for (int i = 0; i < FMX_IQ_DESIGNS; ++i) {
+    // MFMA IQ FIR fragments (k_fe8), as the pilot BPF's below
+    const int P = d->iq_len[i], P8 = ((P + 6) & ~7) + 1;
+    d->iq_ks[i] = (P8 + 15 + 31) / 32;
+    for (int ks = 0; ks < FMX_IQ_KS_MAX; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int dd = 32 * ks + 8 * (l >> 4) + j - (l & 15);
+          const int k = P8 - 1 - dd;
+          const float q = (ks < d->iq_ks[i] && k >= 0 && k < P) ? d->iq_taps[i][k] * 4096.0f : 0.0f;
+          const uint16_t hi = f32_to_f16_bits(q);
+          d->iq_frag[i][ks][0][l][j] = hi;
+          d->iq_frag[i][ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+        }
+  }
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_z16[k + 16] = d->pilot_taps[k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
   {

@@ -29,6 +29,7 @@
 #define FMX_DQ_MIN (-152)    // k_fe8 MFMA decimator tap table: first tap offset (multiple of 8, <= -15 M)
 #define FMX_DQ_N 608         // entries per copy and split (covers 32 K-steps of 16 outputs for M <= 10)
 #define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
+#define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
 
 typedef struct {
   float x, y;
@@ -62,6 +63,10 @@ typedef struct {
   float iq_taps[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN];
   float iq_pad[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN + FMX_PAD]; // [k + 5] = taps[k], zeros around
   float iq_z16[FMX_IQ_DESIGNS][FMX_IQ_MAXLEN + 32]; // [k + 16] = taps[k], 16 zeros each side (k_fe8)
+  // k_fe8's MFMA IQ FIR, fragments as pilot_frag (below) per design: taps *
+  // 2^12 as f16 hi + lo, iq_ks[i] = ceil((P8 + 15) / 32) K steps
+  int iq_ks[FMX_IQ_DESIGNS];
+  uint16_t iq_frag[FMX_IQ_DESIGNS][FMX_IQ_KS_MAX][2][64][8] __attribute__((aligned(16)));
   float fd_ref;          // 1 / (2 pi kf), kf = 75 kHz / Fs
   float deemph_alpha[2]; // 50 us, 75 us at out_rate (fm_demod.cpp:119-131)
   // StereoDecoder (stereo_decoder.cpp:25-63)

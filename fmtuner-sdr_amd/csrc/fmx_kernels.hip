@@ -2961,6 +2961,9 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 #ifndef FMX_DEC_MFMA
 #define FMX_DEC_MFMA 1 // k_fe8 decimator on v_mfma_f32_16x16x32_f16 (0: packed-FMA VALU decimator, A/B runs)
 #endif
+#ifndef FMX_IQ_MFMA
+#define FMX_IQ_MFMA 1 // k_fe8 IQ FIR on v_mfma_f32_16x16x32_f16 (0: packed-FMA fir8_c, A/B runs)
+#endif
 #ifndef FMX_DEC_KS_UNROLL
 #define FMX_DEC_KS_UNROLL 7
 #endif
@@ -2975,6 +2978,9 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int YB_BYTES = (FE8_T + 1) * 8;
   static constexpr int XN = (FE_HALO_IQ + FE8_T + 16) * 9 / 8 + 8;   // padded complex image
   static constexpr int XIN = 0;                                      // aliases raw
+  // FMX_IQ_MFMA: the IQ FIR input instead of the complex image, as f16 hi / lo
+  // images of I and Q (x 2^10; history + chunk + zero slack) from XIN
+  static constexpr int IQW = FE_HALO_IQ + FE8_T + 32;
   static constexpr int YB = XN * 8;                                  // aliases raw
   static constexpr int NPC = (HB + 2 * FE8_T * M + 1023) / 1024;     // 1-KiB LDS-DMA pieces per chunk
   static constexpr int RAW_ALLOC = NPC * 1024 > RAW_BYTES ? NPC * 1024 : RAW_BYTES;
@@ -3011,6 +3017,8 @@ template <int M, int TPP> struct Fe8Layout {
   // (16-B aligned, above the complex image, inside the dead raw region)
   static constexpr int STG = (YB + 15) & ~15;
   static_assert(STG + FE8_T * 8 <= R0, "decimator staging inside the raw region");
+  static_assert(XIN + 4 * IQW * 2 <= YB && (IQW * 2) % 16 == 0 && (FE_HALO_IQ * 2) % 16 == 0,
+                "IQ images below yb, 16-B aligned rows");
 };
 
 // 8 outputs j0..j0+7 (j0 % 8 == 0) of a real-tap FIR of runtime length P on
@@ -3066,7 +3074,18 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   unsigned long long *sgp = reinterpret_cast<unsigned long long *>(smem + LY::SG);
   FeShared *sh = reinterpret_cast<FeShared *>(smem + LY::SH);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
   const bool want_sig = a.sig_sums != nullptr;
+#if FMX_IQ_MFMA
+  // IQ FIR input images (alias xin): I hi, I lo, Q hi, Q lo of the DC blockers'
+  // outputs x 2^10, sample i at [i] (i < FE_HALO_IQ: the carried history)
+  _Float16 *xih = reinterpret_cast<_Float16 *>(smem + LY::XIN);
+  _Float16 *xil = xih + LY::IQW;
+  _Float16 *xqh = xih + 2 * LY::IQW;
+  _Float16 *xql = xih + 3 * LY::IQW;
+  constexpr float kIqIn = 1024.0f;
+#endif
 #ifdef FMX_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
@@ -3374,8 +3393,24 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     __syncthreads(); // raw is dead: xin / yb alias it from here on
     FE_STAMP(0)
     // IQ FIR history and the zero slack past the chunk (read with zero taps)
+#if FMX_IQ_MFMA
+    if (tid < FE_HALO_IQ) {
+      const float2 v = hx[tid];
+      const float sI = v.x * kIqIn, sQ = v.y * kIqIn;
+      const _Float16 hI = (_Float16)sI, hQ = (_Float16)sQ;
+      xih[tid] = hI;
+      xil[tid] = (_Float16)(sI - (float)hI);
+      xqh[tid] = hQ;
+      xql[tid] = (_Float16)(sQ - (float)hQ);
+    }
+    if (tid < 32) {
+      const int i = FE_HALO_IQ + FE8_T + tid;
+      xih[i] = xil[i] = xqh[i] = xql[i] = (_Float16)0.0f;
+    }
+#else
     if (tid < FE_HALO_IQ) xin[fe8_i(tid)] = hx[tid];
     if (tid < 16) xin[fe8_i(FE_HALO_IQ + FE8_T + tid)] = make_float2(0.0f, 0.0f);
+#endif
     // ================= DC blockers: affine scan, 8 per thread =================
     {
       float A = 1.0f, BI = 0.0f, BQ = 0.0f;
@@ -3414,14 +3449,34 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       vI = eA * vI + eI;
       vQ = eA * vQ + eQ;
       // the state before this thread's first element, then the reference's op order
+#if FMX_IQ_MFMA
+      f16x8_t ih, il, qh, ql;
+#endif
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const float tI = dc_a1 * vI, tQ = dc_a1 * vQ;
         const float nI = xv[r].x - tI, nQ = xv[r].y - tQ;
+#if FMX_IQ_MFMA
+        const float oI = nI - vI, oQ = nQ - vQ;
+        const float sI = oI * kIqIn, sQ = oQ * kIqIn;
+        ih[r] = (_Float16)sI;
+        il[r] = (_Float16)(sI - (float)ih[r]);
+        qh[r] = (_Float16)sQ;
+        ql[r] = (_Float16)(sQ - (float)qh[r]);
+        // the next chunk's IQ FIR history (f32; read above before the scan's barrier)
+        if (j0 + r >= FE8_T - FE_HALO_IQ) hx[j0 + r - (FE8_T - FE_HALO_IQ)] = make_float2(oI, oQ);
+#else
         xin[fe8_i(FE_HALO_IQ + j0 + r)] = make_float2(nI - vI, nQ - vQ);
+#endif
         vI = nI;
         vQ = nQ;
       }
+#if FMX_IQ_MFMA
+      *reinterpret_cast<f16x8_t *>(xih + FE_HALO_IQ + j0) = ih;
+      *reinterpret_cast<f16x8_t *>(xil + FE_HALO_IQ + j0) = il;
+      *reinterpret_cast<f16x8_t *>(xqh + FE_HALO_IQ + j0) = qh;
+      *reinterpret_cast<f16x8_t *>(xql + FE_HALO_IQ + j0) = ql;
+#endif
       __syncthreads();
       if (tid == 255) {
         sh->carry_i = vI;
@@ -3431,6 +3486,55 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     __syncthreads();
     FE_STAMP(1)
     // ================= IQ FIR =================
+#if FMX_IQ_MFMA
+    {
+      // v_mfma_f32_16x16x32_f16 tiles as the pilot BPF's: 16 outputs (rows,
+      // A = taps, FmxDesign::iq_frag) of 16 blocks of 16 outputs (columns, B
+      // = the I or Q images), K = the block's P8 + 15 inputs; three MFMAs per
+      // K step and component (hi*hi, hi*lo, lo*hi) into f32 accumulators.
+      // Each wave: two tiles (512 outputs) of I and of Q.
+      const int P8 = fir8_len(iqL);
+      const int KSI = D->iq_ks[par.iqsel];
+      const int col = lane & 15, g = lane >> 4;
+      const int xb = FE_HALO_IQ + 16 * (32 * wave + col) - (P8 - 1) + 8 * g; // 8-aligned: P8 = 8k + 1
+      const f16x8_t *bih = reinterpret_cast<const f16x8_t *>(xih + xb);
+      const f16x8_t *bil = reinterpret_cast<const f16x8_t *>(xil + xb);
+      const f16x8_t *bqh = reinterpret_cast<const f16x8_t *>(xqh + xb);
+      const f16x8_t *bql = reinterpret_cast<const f16x8_t *>(xql + xb);
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->iq_frag[par.iqsel][0][0][0][0]) + lane;
+      f32x4_t ai[2], aq[2];
+      ai[0] = ai[1] = aq[0] = aq[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      u32x4 ah = fa[0], al = fa[64];
+      for (int ks = 0; ks < KSI; ++ks) {
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
+        if (ks + 1 < KSI) {
+          ah = fa[128 * (ks + 1)];
+          al = fa[128 * (ks + 1) + 64];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f16x8_t ihi = bih[32 * u + 4 * ks], ilo = bil[32 * u + 4 * ks]; // + 256 u + 32 ks samples
+          const f16x8_t qhi = bqh[32 * u + 4 * ks], qlo = bql[32 * u + 4 * ks];
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ihi, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, qhi, aq[u], 0, 0, 0);
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ilo, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, qlo, aq[u], 0, 0, 0);
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, ihi, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, qhi, aq[u], 0, 0, 0);
+        }
+      }
+      const float osc = iqscale * (1.0f / (4096.0f * kIqIn)); // exact: a power-of-two rescale
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
+        // (yb + 1 + even: 8-B aligned only, so float2 stores)
+        float2 *yo = yb + 1 + 256 * (2 * wave + u) + 16 * col + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) yo[i] = make_float2(ai[u][i] * osc, aq[u][i] * osc);
+      }
+      if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
+    }
+#else
     {
       f32x2 z[8];
       fir8_c(xin, FE_HALO_IQ + j0, iqz, iqL, z);
@@ -3438,6 +3542,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       for (int r = 0; r < 8; ++r) yb[1 + j0 + r] = make_float2(z[r].x * iqscale, z[r].y * iqscale);
       if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
     }
+#endif
     __syncthreads();
     // ================= AGC (serial, only when enabled) =================
     if (par.agc != 0) {
@@ -3482,7 +3587,9 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         sh->fd_re = yb[FE8_T].x;
         sh->fd_im = yb[FE8_T].y;
       }
+#if !FMX_IQ_MFMA
       if (tid < FE_HALO_IQ) hx[tid] = xin[fe8_i(tid + FE8_T)]; // IQ FIR history for the next chunk
+#endif
     }
     __syncthreads(); // xin / yb are dead: the next chunk may land in raw (below uc)
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});

@@ -272,3 +272,17 @@ def test_mfma_pilot_tap_fragments(fmx, rates):
     assert q.size == h.size
     err = np.abs(q - h)
     assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
+@pytest.mark.parametrize("bw", [-1, 0, 56000, 110000, 311000])
+def test_mfma_iq_fir_tap_fragments(fmx, rates, bw):
+    """k_fe8's MFMA IQ FIR takes the selected IQ filter's taps as f16 hi + lo
+    fragments (x 2^12, FmxDesign::iq_frag): they give the float taps back to
+    22 bits, for the 121-tap XDR filters and the 81-tap constructor filter."""
+    cfg = fmx.make_config(**rates, bandwidth_hz=bw)
+    h = fmx.design_taps(cfg, 1).astype(np.float64)
+    q = fmx.design_taps(cfg, 11).astype(np.float64)
+    assert q.size == h.size and h.size in (81, 121)
+    err = np.abs(q - h)
+    assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()

@@ -85,4 +85,24 @@ for k in range(RUNS):
             print("   ", [(int(a), int(b_), int(k)) for (a, b_), k in zip(u[:30], cnts[:30])])
             print("   offsets mod 2048 of run starts:", sorted(set(int(v) for v in (d[:, 2] - d[:, 2] % 16)[:200] % 2048))[:40])
         bad += len(d)
+# the RDS stage alone (fmx_rds: k_frontend's RDS resampler + k_rds) on the
+# reference run's MPX, twice in fresh handles: separates the front end's RDS
+# resampler in k_fe8 from k_rds
+if os.environ.get("RDS_STAGE", "1") == "1":
+    d_mpx = torch.from_numpy(ref).to(dev)
+    outs = []
+    for rep in range(2):
+        h = fmx.Handle(cfg, C)
+        g_all = torch.zeros((NBLK, C, 8, 4), dtype=torch.int32, device=dev)
+        c_all = torch.zeros((NBLK, C), dtype=torch.int32, device=dev)
+        for b in range(NBLK):
+            h.rds(d_mpx[b].data_ptr(), B, B, g_all[b].data_ptr(), 8, c_all[b].data_ptr())
+        h.sync()
+        outs.append((g_all.cpu().numpy(), c_all.cpu().numpy()))
+        h.close()
+    nd_g = int(np.sum(outs[0][0] != outs[1][0]))
+    nd_c = int(np.sum(outs[0][1] != outs[1][1]))
+    nd_x = int(np.sum(outs[0][0] != ref_other["groups"]))
+    print(f"rds stage twice: {nd_g} differing groups values, {nd_c} group counts; vs process_block: {nd_x}")
+    bad += nd_g + nd_c
 print("DETERMINISTIC" if bad == 0 else f"NONDETERMINISTIC ({bad} samples)")
