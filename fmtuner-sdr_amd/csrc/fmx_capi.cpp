@@ -81,6 +81,7 @@ struct Handle {
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
   bool lr_rows = false; // raw L/R in rows instead of octet tiles (FMX_LR_ROWS=1)
+  bool diag_rds_dump = false; // FMX_DIAG_RDS_DUMP=1: RDS-rate samples over the caller's MPX rows
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -585,6 +586,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   h->serial_prio = 1;
   // FMX_LR_ROWS=1: raw L/R in [C][block] rows instead of octet tiles (A/B runs)
   if (const char *e = std::getenv("FMX_LR_ROWS"); e && e[0] == '1') h->lr_rows = true;
+  if (const char *e = std::getenv("FMX_DIAG_RDS_DUMP"); e && e[0] == '1') h->diag_rds_dump = true;
   if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
@@ -889,6 +891,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       return rc;
     }
     dec_advance(h, n);
+  }
+  if (h->diag_rds_dump && o->d_mpx && rds) {
+    // diagnostic (FMX_DIAG_RDS_DUMP=1): the step's 171 kHz RDS-rate samples over the caller's MPX rows
+    const size_t w = static_cast<size_t>(std::min(h->rds_stride, o->mpx_stride)) * sizeof(float);
+    HIP_TRY(hipMemcpy2DAsync(o->d_mpx, sizeof(float) * static_cast<size_t>(o->mpx_stride), h->rds_in[buf],
+                             sizeof(float) * static_cast<size_t>(h->rds_stride), w, static_cast<size_t>(h->C),
+                             hipMemcpyDeviceToDevice, h->sA));
   }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC) ----
@@ -1616,6 +1625,14 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
+    case 12: // k_audio MFMA L/R FIR taps back from the f16 hi/lo fragments (row 0 lanes), as case 3
+      for (int k = 0; k < FMX_LR_LEN; ++k) {
+        const int dd = FMX_LR_LEN - 1 - k;
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->lr_frag[ks][0][l][j]) + f16_value(d->lr_frag[ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 4096.0));
+      }
+      break;
     case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
       for (int cp = 0; cp < 2; ++cp)
         for (int k = 0; k < d->dec_len; ++k) {

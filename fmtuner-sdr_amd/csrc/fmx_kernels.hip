@@ -1687,8 +1687,17 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 // FIR input image: pair i at i + i/8 (lanes 8 pairs apart land 9 apart:
 // conflict-free ds_read_b64)
 __device__ __forceinline__ int au_xi(int i) { return i + (i >> 3); }
+#ifndef FMX_AU_MFMA
+#define FMX_AU_MFMA 0 // 1: k_audio L/R FIR on v_mfma_f32_16x16x32_f16 (measured slower in the pipelined step)
+#endif
+#define AU_W (AU_HALO + AU2_T + 32) // FMX_AU_MFMA input image: history, chunk, zero slack
 struct AuShared {
+#if FMX_AU_MFMA
+  _Float16 xim[4][AU_W] __attribute__((aligned(16))); // raw L hi, L lo, R hi, R lo (x 2^10)
+  float2 hist[2][AU_HALO];                             // the last AU_HALO raw (L, R) in f32, by chunk parity
+#else
   float2 x[(AU_HALO + AU2_T + 8) * 9 / 8 + 8]; // raw (L, R), 120 of history first
+#endif
   float2 f[AU_RHALO + AU2_T];                  // resampler input (L, R), 32 of history first
   float2 o[AU2_MAXOUT];                        // resampler outputs of the chunk
   float hT[FMX_AF_SUB][FMX_NPFB];              // resampler bank transposed: hT[n][b] = h_b[n]
@@ -1766,8 +1775,13 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   // ---- carried state ----
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
+#if FMX_AU_MFMA
+  if (lrfir)
+    for (int h = tid; h < AU_HALO; h += 256) S.hist[0][h] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
+#else
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) S.x[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
+#endif
   if (af)
     for (int h = tid; h < AU_RHALO; h += 256) S.f[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
@@ -1796,8 +1810,10 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     S.eb = 0;
     S.count = 0;
   }
+#if !FMX_AU_MFMA
   if (lrfir)
     for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
+#endif
   // tiled input (raw L/R from k_pll): sample j of this channel at tin + ti(j)
   const bool tiled = a.in_tiled != 0;
   const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
@@ -1826,6 +1842,62 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       }
     }
     // ---- chunk input (all loads issued before the first LDS write) ----
+#if FMX_AU_MFMA
+    const int par_c = (n0 / AU2_T) & 1; // S.hist[par_c]: history before this chunk
+    if (lrfir) {
+      // 8 consecutive raw pairs per thread into the f16 hi / lo images (one
+      // 16-B write per image), the history images from the f32 copy, and the
+      // new history (the last AU_HALO pairs of history + chunk) into the other copy
+      float vl[8], vr[8];
+      const int jb = 8 * tid;
+      if (tiled && jb + 8 <= cnt) {
+        const float4 l0 = *reinterpret_cast<const float4 *>(inl + ti(n0 + jb));
+        const float4 l1 = *reinterpret_cast<const float4 *>(inl + ti(n0 + jb + 4));
+        const float4 r0 = *reinterpret_cast<const float4 *>(inr + ti(n0 + jb));
+        const float4 r1 = *reinterpret_cast<const float4 *>(inr + ti(n0 + jb + 4));
+        vl[0] = l0.x; vl[1] = l0.y; vl[2] = l0.z; vl[3] = l0.w; vl[4] = l1.x; vl[5] = l1.y; vl[6] = l1.z; vl[7] = l1.w;
+        vr[0] = r0.x; vr[1] = r0.y; vr[2] = r0.z; vr[3] = r0.w; vr[4] = r1.x; vr[5] = r1.y; vr[6] = r1.z; vr[7] = r1.w;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          vl[r] = (jb + r < cnt) ? inl[ti(n0 + jb + r)] : 0.0f;
+          vr[r] = (jb + r < cnt) ? inr[ti(n0 + jb + r)] : 0.0f;
+        }
+      }
+      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+      f16x8_t lh, ll, rh, rl;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float sl_ = vl[r] * 1024.0f, sr_ = vr[r] * 1024.0f;
+        lh[r] = (_Float16)sl_;
+        ll[r] = (_Float16)(sl_ - (float)lh[r]);
+        rh[r] = (_Float16)sr_;
+        rl[r] = (_Float16)(sr_ - (float)rh[r]);
+      }
+      *reinterpret_cast<f16x8_t *>(&S.xim[0][AU_HALO + jb]) = lh;
+      *reinterpret_cast<f16x8_t *>(&S.xim[1][AU_HALO + jb]) = ll;
+      *reinterpret_cast<f16x8_t *>(&S.xim[2][AU_HALO + jb]) = rh;
+      *reinterpret_cast<f16x8_t *>(&S.xim[3][AU_HALO + jb]) = rl;
+      float2 *hn = S.hist[par_c ^ 1];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j = jb + r;
+        if (j < cnt && j >= cnt - AU_HALO) hn[j - (cnt - AU_HALO)] = make_float2(vl[r], vr[r]);
+      }
+      if (tid < AU_HALO) {
+        const float2 v = S.hist[par_c][tid];
+        if (tid < AU_HALO - cnt) hn[tid] = S.hist[par_c][cnt + tid]; // short chunk: older history stays
+        const float sl_ = v.x * 1024.0f, sr_ = v.y * 1024.0f;
+        const _Float16 a0 = (_Float16)sl_, a1 = (_Float16)sr_;
+        S.xim[0][tid] = a0;
+        S.xim[1][tid] = (_Float16)(sl_ - (float)a0);
+        S.xim[2][tid] = a1;
+        S.xim[3][tid] = (_Float16)(sr_ - (float)a1);
+      }
+      if (tid < 32) S.xim[0][AU_HALO + AU2_T + tid] = S.xim[1][AU_HALO + AU2_T + tid] =
+          S.xim[2][AU_HALO + AU2_T + tid] = S.xim[3][AU_HALO + AU2_T + tid] = (_Float16)0.0f;
+    } else
+#endif
     {
       float vl[AU2_PT], vr[AU2_PT];
 #pragma unroll
@@ -1837,13 +1909,77 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {
         const int j = tid + 256 * k;
+#if FMX_AU_MFMA
+        if (j < cnt) S.f[AU_RHALO + j] = make_float2(vl[k], vr[k]);
+#else
         if (lrfir) S.x[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
         else if (j < cnt) S.f[AU_RHALO + j] = make_float2(vl[k], vr[k]);
+#endif
       }
     }
     if (tid == 0) S.ee = S.eb;
     __syncthreads();
     // ---- L/R FIR: outputs j0 .. j0+7, inputs j0-120 .. j0+7 ----
+#if FMX_AU_MFMA
+    if (lrfir) {
+      // v_mfma_f32_16x16x32_f16 tiles as k_fe8's IQ FIR: 16 outputs (rows,
+      // A = taps, FmxDesign::lr_frag) of 16 blocks of 16 outputs (columns, B
+      // = the L or R images), three MFMAs per K step and channel (hi*hi,
+      // hi*lo, lo*hi); each wave two tiles (512 outputs) of L and of R
+      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+      typedef float f32x4_t __attribute__((ext_vector_type(4)));
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      constexpr int P8 = FMX_LR_LEN; // 8k + 1: no leading zero taps
+      static_assert(((FMX_LR_LEN + 6) & ~7) + 1 == FMX_LR_LEN && FMX_LR_LEN - 1 == AU_HALO, "L/R FIR geometry");
+      const int lane = tid & 63, wave = tid >> 6;
+      const int col = lane & 15, g = lane >> 4;
+      const int xb = AU_HALO + 16 * (32 * wave + col) - (P8 - 1) + 8 * g;
+      const f16x8_t *blh = reinterpret_cast<const f16x8_t *>(&S.xim[0][xb]);
+      const f16x8_t *bll = reinterpret_cast<const f16x8_t *>(&S.xim[1][xb]);
+      const f16x8_t *brh = reinterpret_cast<const f16x8_t *>(&S.xim[2][xb]);
+      const f16x8_t *brl = reinterpret_cast<const f16x8_t *>(&S.xim[3][xb]);
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->lr_frag[0][0][0][0]) + lane;
+      f32x4_t al_[2], ar_[2];
+      al_[0] = al_[1] = ar_[0] = ar_[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      u32x4 ah = fa[0], alo_ = fa[64];
+#pragma unroll
+      for (int ks = 0; ks < FMX_LR_KS; ++ks) {
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, alo_);
+        if (ks + 1 < FMX_LR_KS) {
+          ah = fa[128 * (ks + 1)];
+          alo_ = fa[128 * (ks + 1) + 64];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f16x8_t lhi = blh[32 * u + 4 * ks], llo = bll[32 * u + 4 * ks];
+          const f16x8_t rhi = brh[32 * u + 4 * ks], rlo = brl[32 * u + 4 * ks];
+          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, lhi, al_[u], 0, 0, 0);
+          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rhi, ar_[u], 0, 0, 0);
+          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, llo, al_[u], 0, 0, 0);
+          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rlo, ar_[u], 0, 0, 0);
+          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, lhi, al_[u], 0, 0, 0);
+          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, rhi, ar_[u], 0, 0, 0);
+        }
+      }
+      const float osc = sc * (1.0f / (4096.0f * 1024.0f)); // exact power-of-two rescale
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g; // lane: outputs o .. o + 3
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = o + i;
+          if (j < cnt) {
+            const float2 y = make_float2(al_[u][i] * osc, ar_[u][i] * osc);
+            if (af) S.f[AU_RHALO + j] = y;
+            if (a.lr_out_l) {
+              a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
+              a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
+            }
+          }
+        }
+      }
+    }
+#else
     if (lrfir) {
       const int j0 = AU2_PT * tid;
       f32x2 acc[AU2_PT];
@@ -1881,6 +2017,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         }
       }
     }
+#endif
     __syncthreads();
     if (af) {
       // ---- resampler: one schedule entry per thread ----
@@ -2003,17 +2140,26 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     // ---- carry halos ----
     {
       float2 cx = make_float2(0.0f, 0.0f), cf = make_float2(0.0f, 0.0f);
+#if !FMX_AU_MFMA
       if (lrfir && tid < AU_HALO) cx = S.x[au_xi(tid + cnt)];
+#endif
       if (af && tid < AU_RHALO) cf = S.f[tid + cnt];
       __syncthreads();
+#if !FMX_AU_MFMA
       if (lrfir && tid < AU_HALO) S.x[au_xi(tid)] = cx;
+#endif
+      (void)cx;
       if (af && tid < AU_RHALO) S.f[tid] = cf;
       __syncthreads();
     }
   }
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) {
+#if FMX_AU_MFMA
+      const float2 v = S.hist[((n + AU2_T - 1) / AU2_T) & 1][h]; // after the last chunk
+#else
       const float2 v = S.x[au_xi(h)];
+#endif
       lrh[h] = v.x;
       lrh[(FMX_LR_LEN - 1) + h] = v.y;
     }
@@ -2964,6 +3110,9 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 #ifndef FMX_IQ_MFMA
 #define FMX_IQ_MFMA 1 // k_fe8 IQ FIR on v_mfma_f32_16x16x32_f16 (0: packed-FMA fir8_c, A/B runs)
 #endif
+#ifndef FMX_RS_PACKED
+#define FMX_RS_PACKED 0 // 1: k_fe8's RDS resampler on packed FP32 (v_pk_mul / v_pk_add), see the resampler
+#endif
 #ifndef FMX_DEC_KS_UNROLL
 #define FMX_DEC_KS_UNROLL 7
 #endif
@@ -3064,6 +3213,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
   float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
+  (void)xin;
   float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
   _Float16 *xh = reinterpret_cast<_Float16 *>(smem + LY::MX);  // MPX hi, index FMX_HIST + j
   _Float16 *xl = reinterpret_cast<_Float16 *>(smem + LY::XLO); // MPX lo
@@ -3109,6 +3259,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   const FmxChanParam par = a.par[c];
   const int iqL = D->iq_len[par.iqsel];
   const float *__restrict__ iqz = D->iq_z16[par.iqsel];
+  (void)iqz;
   const float iqscale = D->iq_scale[par.iqsel];
   const bool pilot = a.pilot_out != nullptr;
   const bool rds = a.rds_out != nullptr;
@@ -3674,6 +3825,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           asm volatile("" : "+v"(xa), "+v"(ha));
           const lds_f32 *xu = (const lds_f32 *)(uintptr_t)xa;
           const lds_f32x2 *hk = (const lds_f32x2 *)(uintptr_t)ha;
+#if FMX_RS_PACKED
           f32x2 y = {0.0f, 0.0f};
 #pragma unroll
           for (int m = 0; m < LY::RS_M; ++m) {
@@ -3682,6 +3834,25 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
             const f32x2 p = hk[m] * f32x2{v, v};
             y = y + p;
           }
+#else
+          // scalar multiplies and adds (same rounding): the packed-FP32 form
+          // (v_pk_mul / v_pk_add) returned wrong upper-32-lane results,
+          // nondeterministically, with two k_fe8 workgroups per CU issuing
+          // MFMAs (tools/gpu_determinism.py with FMX_DIAG_RDS_DUMP=1)
+          float y0 = 0.0f, y1 = 0.0f;
+#pragma unroll
+          for (int m = 0; m < LY::RS_M; ++m) {
+            const float v = xu[m];
+            const f32x2 hm = hk[m];
+            // as asm so that the vectorizer cannot pair them into v_pk_* again
+            float p0, p1;
+            asm("v_mul_f32 %0, %1, %2" : "=v"(p0) : "v"(hm.x), "v"(v));
+            asm("v_mul_f32 %0, %1, %2" : "=v"(p1) : "v"(hm.y), "v"(v));
+            asm("v_add_f32 %0, %1, %2" : "=v"(y0) : "v"(y0), "v"(p0));
+            asm("v_add_f32 %0, %1, %2" : "=v"(y1) : "v"(y1), "v"(p1));
+          }
+          const f32x2 y = {y0, y1};
+#endif
           const float w0f = (1.0f - en[k].mu) * y.x;
           const float w1f = en[k].mu * y.y;
           a.rds_out[(size_t)c * a.rds_stride + e] = w0f + w1f;
