@@ -36,3 +36,15 @@ for key in ("k_fe8", "k_pll", "k_rds", "k_audio"):
 if len(fe) > 3:
     print("step (front-end start to start, median) us: %.1f" % statistics.median(
         (b[0] - a[0]) / 1e3 for a, b in zip(fe[2:], fe[3:])))
+
+# per step (k-th launch of each kernel = step k): start / end of every kernel
+# relative to its front end's start, us -- which stream waits for which
+seq = {key: [e for e in ev if key in e[2]] for key in ("k_fe8", "k_pll", "k_rds", "k_audio")}
+nst = min(len(v) for v in seq.values())
+if nst > 6:
+    print("step  fe[s,e]        pll[s,e]        rds[s,e]        audio[s,e]   (us from fe start)")
+    for k in range(nst - 8, nst):
+        t0 = seq["k_fe8"][k][0]
+        row = " ".join("%6.0f,%6.0f " % ((seq[key][k][0] - t0) / 1e3, (seq[key][k][1] - t0) / 1e3)
+                       for key in ("k_fe8", "k_pll", "k_rds", "k_audio"))
+        print("%4d  %s" % (k, row))
