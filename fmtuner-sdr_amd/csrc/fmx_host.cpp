@@ -26,20 +26,24 @@
 
 namespace {
 
-// evaluatePiState (xdr_server.cpp:189-213)
+// PI confidence of `value` over the debounce buffer (the rule of
+// evaluatePiState, xdr_server.cpp:189-213): `seen` = buffered copies of the
+// value, `clean` = those received without block errors.  The XDR level is the
+// first rule that holds, best first:
+//   0  two clean copies            1  two copies, one of them clean
+//   2  three copies (any errors)   3  two copies, or one clean copy
+//   4  otherwise
 uint8_t pi_state(const fmx_xdr_pi_state *s, uint16_t value) {
-  uint8_t count = 0, correct = 0;
-  for (uint8_t i = 0; i < s->fill; i++) {
-    if (s->pi_buf[i] == value) {
-      count++;
-      if ((s->pi_err[i / 8] & (1 << (i % 8))) == 0) correct++;
-    }
+  int seen = 0, clean = 0;
+  for (int i = 0; i < s->fill; i++) {
+    if (s->pi_buf[i] != value) continue;
+    seen++;
+    clean += ((s->pi_err[i >> 3] >> (i & 7)) & 1) ? 0 : 1;
   }
-  if (correct >= 2) return 0;          // STATE_CORRECT
-  if (count >= 2 && correct) return 1; // STATE_VERY_LIKELY
-  if (count >= 3) return 2;            // STATE_LIKELY
-  if (count == 2 || correct) return 3; // STATE_UNLIKELY
-  return 4;                            // STATE_INVALID
+  const bool rule[4] = {clean >= 2, seen >= 2 && clean > 0, seen >= 3, seen == 2 || clean > 0};
+  for (uint8_t level = 0; level < 4; ++level)
+    if (rule[level]) return level;
+  return 4;
 }
 
 int emit(std::string &acc, const char *line) {
