@@ -50,4 +50,5 @@ def test_cfg3_outputs_bit_identical_across_runs(fmx, torch_cuda):
     print("determinism:", diffs)
     assert all(v == 0 for v in diffs.values()), diffs
     # the run decoded something (the comparison is not vacuous)
-    assert a["ints"][3].sum() > 300 and a["ints"][1][-1].mean() > 0.5, (a["ints"][3].sum(), a["ints"][1][-1].mean())
+    # (stereo detection needs 6 blocks of pilot presence: the level is checked instead)
+    assert a["ints"][3].sum() > 300 and a["ints"][2][-1].mean() > 10, (a["ints"][3].sum(), a["ints"][2][-1].mean())
