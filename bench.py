@@ -288,8 +288,11 @@ def main():
     h.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_call = []  # host time per process_block call (submission only): stalls show here
     for b in range(args.warmup, nblk):
+        tc = time.perf_counter()
         step(b)
+        host_call.append(time.perf_counter() - tc)
     h.sync()
     torch.cuda.synchronize()
     if world > 1:
@@ -415,6 +418,8 @@ def main():
         "dominant_kernel": dom,
         "cpu_baseline": cpu,
         "scan": scan,
+        "host_submit_ms": {"mean": round(1e3 * sum(host_call) / len(host_call), 4),
+                           "max": round(1e3 * max(host_call), 4)},
         "check": {"rds_groups_last_step": ngroups, "rds_groups_warmup": groups_warm,
                   "stereo_fraction": stereo_frac},
     }

@@ -42,6 +42,7 @@ namespace fmx {
 // the speculation back and uploads on sA as before.  On sA the uploads sat
 // between consecutive front-end kernels: 6 copies, ~0.1 ms per step
 // (rocprofv3 --memory-copy-trace).
+#define FMX_HSLOTS 8 // pinned schedule images per timing set
 struct TimingSet {
   float del = 1.0f;
   std::vector<ResampTiming> groups;
@@ -51,11 +52,18 @@ struct TimingSet {
   int cur = 0; // slot holding the schedules of the step being launched
   size_t slot_bytes = 0;
   unsigned char *d_slot[FMX_NBUF] = {};
-  unsigned char *h_slot[FMX_NBUF] = {}; // pinned
+  // pinned staging images, a ring deeper than the device slots: the image
+  // reused at step k was copied at step k - FMX_HSLOTS, long complete, so the
+  // host never blocks on it (with one image per device slot the host waited
+  // 0.66 ms per step on the copy of step k-3 and woke late, ms-long GPU gaps)
+  unsigned char *h_slot[FMX_HSLOTS] = {};
+  int hnext = 0, hcur = 0; // next image to fill, image of the last simulation
+  hipEvent_t ev_h[FMX_HSLOTS] = {}; // after the last copy out of h_slot[i]
+  bool ev_h_set[FMX_HSLOTS] = {};
   FmxSched *d_sched[FMX_NBUF] = {};
   int *d_count[FMX_NBUF] = {};
   int *d_group[FMX_NBUF] = {};
-  hipEvent_t ev_up[FMX_NBUF] = {}; // after the last copy out of h_slot[b]
+  hipEvent_t ev_up[FMX_NBUF] = {}; // after the last copy into d_slot[b]
   bool ev_up_set[FMX_NBUF] = {};
   // speculation: state before the speculative advance, its n and slot
   bool spec = false;
@@ -82,6 +90,12 @@ struct Handle {
   int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
   bool lr_rows = false; // raw L/R in rows instead of octet tiles (FMX_LR_ROWS=1)
   bool diag_rds_dump = false; // FMX_DIAG_RDS_DUMP=1: RDS-rate samples over the caller's MPX rows
+  // FMX_DIAG_HOST=1: host time per process_block part (printed at destroy)
+  bool diag_host = false;
+  double hd_sync = 0, hd_sync_max = 0, hd_sim = 0, hd_total = 0, hd_total_max = 0;
+  double hd_seg[10] = {}, hd_seg_max[10] = {};
+  std::chrono::steady_clock::time_point hd_last;
+  long hd_calls = 0;
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -193,6 +207,26 @@ struct KTimer {
   }
 };
 
+// the pending timings whose end event has completed, without blocking
+// (process_block, every step while timing is on): keeps the event pool
+// recycled, so the timed region never creates events -- creating them as the
+// pool ran dry stalled the host for 3-6 ms every 5-6 steps (rocprofv3
+// timeline: the GPU idle, the next step's work queued late)
+static void harvest_timing(Handle *h) {
+  size_t k = 0;
+  for (; k < h->pending.size(); ++k) {
+    auto &p = h->pending[k];
+    if (hipEventQuery(p.b) != hipSuccess) break;
+    float ms = 0.0f;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    h->kms[p.k] += ms;
+    h->klaunch[p.k]++;
+    h->pool.push_back(p.a);
+    h->pool.push_back(p.b);
+  }
+  h->pending.erase(h->pending.begin(), h->pending.begin() + static_cast<std::ptrdiff_t>(k));
+}
+
 static void collect_timing(Handle *h) {
   for (auto &p : h->pending) {
     float ms = 0.0f;
@@ -212,7 +246,7 @@ static size_t tset_sched_off(const Handle *h, const TimingSet &t) {
   return (sizeof(int) * (static_cast<size_t>(h->C) + t.cap_groups) + 15) & ~static_cast<size_t>(15);
 }
 static FmxSched *tset_hsched(const Handle *h, TimingSet &t, int b) {
-  return reinterpret_cast<FmxSched *>(t.h_slot[b] + tset_sched_off(h, t));
+  return reinterpret_cast<FmxSched *>(t.h_slot[b] + tset_sched_off(h, t)); // b: host image
 }
 static void tset_free_slots(Handle *h, TimingSet &t) {
   for (int b = 0; b < FMX_NBUF; ++b) {
@@ -221,8 +255,11 @@ static void tset_free_slots(Handle *h, TimingSet &t) {
                       h->allocs.end());
       hipFree(t.d_slot[b]);
     }
-    if (t.h_slot[b]) hipHostFree(t.h_slot[b]);
-    t.d_slot[b] = t.h_slot[b] = nullptr;
+    t.d_slot[b] = nullptr;
+  }
+  for (int i = 0; i < FMX_HSLOTS; ++i) {
+    if (t.h_slot[i]) hipHostFree(t.h_slot[i]);
+    t.h_slot[i] = nullptr;
   }
 }
 static int tset_alloc_slots(Handle *h, TimingSet &t) {
@@ -231,12 +268,16 @@ static int tset_alloc_slots(Handle *h, TimingSet &t) {
   int rc;
   for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &t.d_slot[b], t.slot_bytes)) != FMX_OK) return rc;
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.h_slot[b]), t.slot_bytes, hipHostMallocDefault));
-    std::memset(t.h_slot[b], 0, t.slot_bytes);
+
     t.d_group[b] = reinterpret_cast<int *>(t.d_slot[b]);
     t.d_count[b] = t.d_group[b] + h->C;
     t.d_sched[b] = reinterpret_cast<FmxSched *>(t.d_slot[b] + off);
     if (!t.ev_up[b]) HIP_TRY(hipEventCreateWithFlags(&t.ev_up[b], ev_flags(false)));
+  }
+  for (int i = 0; i < FMX_HSLOTS; ++i) {
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.h_slot[i]), t.slot_bytes, hipHostMallocDefault));
+    std::memset(t.h_slot[i], 0, t.slot_bytes);
+    if (!t.ev_h[i]) HIP_TRY(hipEventCreateWithFlags(&t.ev_h[i], ev_flags(false)));
   }
   return FMX_OK;
 }
@@ -315,13 +356,19 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
     tset_free_slots(h, t);
     t.cap_groups = G * 2;
     for (int b = 0; b < FMX_NBUF; ++b) t.ev_up_set[b] = false;
+    for (int i = 0; i < FMX_HSLOTS; ++i) t.ev_h_set[i] = false;
     int rc;
     if ((rc = tset_alloc_slots(h, t)) != FMX_OK) return rc;
   }
   // the previous copy out of this pinned image must have run
-  if (t.ev_up_set[buf]) HIP_TRY(hipEventSynchronize(t.ev_up[buf]));
-  FmxSched *hs = tset_hsched(h, t, buf);
-  int *hc = reinterpret_cast<int *>(t.h_slot[buf]) + h->C;
+  const auto ts0 = std::chrono::steady_clock::now();
+  const int hb = t.hnext;
+  t.hnext = (hb + 1) % FMX_HSLOTS;
+  t.hcur = hb;
+  if (t.ev_h_set[hb]) HIP_TRY(hipEventSynchronize(t.ev_h[hb]));
+  const auto ts1 = std::chrono::steady_clock::now();
+  FmxSched *hs = tset_hsched(h, t, hb);
+  int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
   int mx = 0;
   for (int g = 0; g < G; ++g) {
     const int k = timing_run(t.groups[static_cast<size_t>(g)], n, hs + static_cast<size_t>(g) * t.stride, t.stride);
@@ -332,16 +379,24 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
     hc[g] = k;
     mx = std::max(mx, k);
   }
-  std::memcpy(t.h_slot[buf], t.chan_group.data(), sizeof(int) * h->C);
+  std::memcpy(t.h_slot[hb], t.chan_group.data(), sizeof(int) * h->C);
   t.G = G;
+  if (h->diag_host) {
+    const double w = std::chrono::duration<double, std::milli>(ts1 - ts0).count();
+    h->hd_sync += w;
+    h->hd_sync_max = std::max(h->hd_sync_max, w);
+    h->hd_sim += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts1).count();
+  }
   if (max_count) *max_count = mx;
   return FMX_OK;
 }
 static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
-  HIP_TRY(hipMemcpyAsync(t.d_slot[buf], t.h_slot[buf], bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(t.d_slot[buf], t.h_slot[t.hcur], bytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(t.ev_up[buf], s));
   t.ev_up_set[buf] = true;
+  HIP_TRY(hipEventRecord(t.ev_h[t.hcur], s));
+  t.ev_h_set[t.hcur] = true;
   return FMX_OK;
 }
 // Simulate n inputs and upload the schedules into slot `buf` on sA.
@@ -524,6 +579,8 @@ static void destroy(Handle *h) {
     tset_free_slots(h, *t);
     for (hipEvent_t e : t->ev_up)
       if (e) hipEventDestroy(e);
+    for (hipEvent_t e : t->ev_h)
+      if (e) hipEventDestroy(e);
   }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
@@ -587,6 +644,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   // FMX_LR_ROWS=1: raw L/R in [C][block] rows instead of octet tiles (A/B runs)
   if (const char *e = std::getenv("FMX_LR_ROWS"); e && e[0] == '1') h->lr_rows = true;
   if (const char *e = std::getenv("FMX_DIAG_RDS_DUMP"); e && e[0] == '1') h->diag_rds_dump = true;
+  if (const char *e = std::getenv("FMX_DIAG_HOST"); e && e[0] == '1') h->diag_host = true;
   if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
     h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
@@ -833,6 +891,16 @@ static void step_done(Handle *h, bool stereo_hist_written) {
   h->step++;
 }
 
+// FMX_DIAG_HOST: host time of process_block's parts (0 prepare, 1 waits +
+// schedules, 2 front end, 3 RDS, 4 speculative uploads, 5 PLL, 6 audio)
+#define HD_MARK(i)                                                                               \
+  if (h->diag_host) {                                                                            \
+    const auto t_ = std::chrono::steady_clock::now();                                            \
+    const double w_ = std::chrono::duration<double, std::milli>(t_ - h->hd_last).count();        \
+    h->hd_seg[i] += w_;                                                                          \
+    h->hd_seg_max[i] = std::max(h->hd_seg_max[i], w_);                                           \
+    h->hd_last = t_;                                                                             \
+  }
 static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *o) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
@@ -842,6 +910,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   if (n == 0) return FMX_OK;
   if ((rc = prepare(h)) != FMX_OK) return rc;
+  if (h->diag_host) h->hd_last = std::chrono::steady_clock::now();
+  if (h->timing) harvest_timing(h);
+  HD_MARK(0);
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
   const int buf = static_cast<int>(h->step % FMX_NBUF);
@@ -865,6 +936,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if (rds && !hit_rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
   if (!hit_af && (rc = tset_advance(h, *tau, n, buf, nullptr)) != FMX_OK) return rc;
   if (hit_rds) HIP_TRY(hipStreamWaitEvent(h->sA, h->t_rds.ev_up[buf], 0)); // the front end reads it
+  HD_MARK(1);
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
   // ---- front end (sA) ----
@@ -900,6 +972,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
                              hipMemcpyDeviceToDevice, h->sA));
   }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
+  HD_MARK(2);
   // ---- RDS (sC) ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   if (rds) {
@@ -916,6 +989,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
   }
   HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
+  HD_MARK(3);
   h->evC_set[buf] = true;
   // ---- next step's schedules, one step early, on sB ahead of this step's
   // PLL (off the front end's stream).  Slot nb was last read by step
@@ -926,6 +1000,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     if (h->evD_set[nb]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[nb], 0));
     if (rds && (rc = tset_speculate(h, h->t_rds, n, nb, h->sB)) != FMX_OK) return rc;
     if ((rc = tset_speculate(h, *tau, n, nb, h->sB)) != FMX_OK) return rc;
+  HD_MARK(4);
   }
   // ---- stereo PLL (sB), audio (sD) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
@@ -947,6 +1022,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     if (o->d_stereo_indicator) HIP_TRY(hipMemsetAsync(o->d_stereo_indicator, 0, sizeof(int) * h->C, h->sB));
   }
   HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
+  HD_MARK(5);
   h->evB_set[buf] = true;
   HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0)); // after the PLL (stereo) / the frontend (mono)
   if (stereo) {
@@ -990,6 +1066,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
   }
   HIP_TRY(hipEventRecord(h->evD[buf], h->sD));
+  HD_MARK(6);
   h->evD_set[buf] = true;
   h->block_index++;
   step_done(h, stereo);
@@ -1039,6 +1116,13 @@ int fmx_create(const fmx_config *cfg, int n_channels, int device, void **handle)
 }
 
 int fmx_destroy(void *handle) {
+  if (Handle *h = H(handle); h && h->diag_host && h->hd_calls)
+    std::fprintf(stderr, "fmx host: %ld process_block calls, mean %.3f ms (max %.3f); schedule-slot waits %.3f ms/call "
+                 "(max %.3f), simulation %.3f ms/call\n", h->hd_calls, h->hd_total / h->hd_calls, h->hd_total_max,
+                 h->hd_sync / h->hd_calls, h->hd_sync_max, h->hd_sim / h->hd_calls);
+  if (Handle *h = H(handle); h && h->diag_host && h->hd_calls)
+    for (int i = 0; i < 7; ++i)
+      std::fprintf(stderr, "fmx host part %d: mean %.3f ms max %.3f\n", i, h->hd_seg[i] / h->hd_calls, h->hd_seg_max[i]);
   destroy(H(handle));
   return FMX_OK;
 }
@@ -1172,7 +1256,14 @@ int fmx_set_signal_params(void *handle, int channel, int applied_gain_db, double
 int fmx_process_block(void *handle, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *out) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  return process_block(h, d_iq, iq_stride, n, out);
+  if (!h->diag_host) return process_block(h, d_iq, iq_stride, n, out);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = process_block(h, d_iq, iq_stride, n, out);
+  const double w = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  h->hd_total += w;
+  h->hd_total_max = std::max(h->hd_total_max, w);
+  h->hd_calls++;
+  return rc;
 }
 
 int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, float *d_out, int out_stride) {
@@ -1460,6 +1551,12 @@ int fmx_timing_enable(void *handle, int enable) {
     collect_timing(h);
   }
   h->timing = enable != 0;
+  // events for the timed region up front (creating them on the way stalls the host)
+  while (h->timing && h->pool.size() < 256) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, ev_flags(true)));
+    h->pool.push_back(e);
+  }
   for (int k = 0; k < FMX_K_COUNT; ++k) {
     h->kms[k] = 0.0;
     h->klaunch[k] = 0;

@@ -1,6 +1,5 @@
 #!/bin/bash
-# scratch GPU step (edited per experiment)
 set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
-bash tools/gpu_step2.sh
-bash tools/gpu_trace.sh trace_r02d > gpurun_out/trace_r02d.txt 2>&1; tail -24 gpurun_out/trace_r02d.txt
+FMX_DIAG_HOST=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 > gpurun_out/hd.json 2> gpurun_out/hd.err
+grep "fmx host" gpurun_out/hd.err; python3 -c "import json;d=json.load(open('gpurun_out/hd.json'));print(d['ms_per_step'], d['host_submit_ms'])"
