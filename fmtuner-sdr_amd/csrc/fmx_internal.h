@@ -191,6 +191,7 @@ enum ResetParts {
 };
 int launch_reset(const ResetArgs &a, void *stream);
 int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, size_t out_stride, void *stream);
+int launch_copy16(const void *src, void *dst, size_t n16, void *stream); // 16-B words, any memory the device maps
 
 } // namespace fmx
 

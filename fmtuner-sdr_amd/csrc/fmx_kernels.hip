@@ -4015,6 +4015,17 @@ int launch_rds(const RdsArgs &a, void *stream) {
   hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
+// 16-B words src -> dst (the schedule upload from mapped pinned memory)
+__global__ void k_copy16(const uint4 *src, uint4 *dst, size_t n16) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+}
+int launch_copy16(const void *src, void *dst, size_t n16, void *stream) {
+  if (n16 == 0) return FMX_OK;
+  hipLaunchKernelGGL(k_copy16, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4 *>(src), static_cast<uint4 *>(dst), n16);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
 int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, size_t out_stride, void *stream) {
   if (C <= 0 || n <= 0) return FMX_OK;
   hipLaunchKernelGGL(k_iq_to_u8, dim3((n + 255) / 256, C), dim3(256), 0, static_cast<hipStream_t>(stream), in,
