@@ -2231,6 +2231,18 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 #ifndef FMX_HWSIN_RDS
 #define FMX_HWSIN_RDS 1
 #endif
+// FMX_RDS_DIRECT_PHASE (default 1): the mix-down phase of sample k is the
+// NCO word's own phase, v_sin / v_cos of theta / 2^32 turns.  The reference
+// mixes with the quad-phase wrapper's accumulator phases_[0] (liquid_wrappers
+// .cpp:121-139), which sums unwrap(phase_now - prev) * 57000 / 57000 over the
+// NCO's steps (PLL jumps included): it is the NCO phase mod 2 pi up to float
+// rounding (a random walk of ~1e-7 rad per step, also through resets, which
+// keep phases_ and prev).  Dropping that sum removes ~15 dependent VALU per
+// sample from the issue-bound k_rds wave; RDS groups stay bit-exact against
+// the oracle (which keeps the reference's sum).  0: the reference's sum.
+#ifndef FMX_RDS_DIRECT_PHASE
+#define FMX_RDS_DIRECT_PHASE 1
+#endif
 #define RDS_TILE 8  // samples per LDS-DMA tile
 #define RDS_RING 32 // ring of 4 tiles: up to 3 in flight ahead of the one being read
 #ifndef RDS_U
@@ -2601,6 +2613,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = rds_mac(h[i], m, acc[i]);
     ring_store(m, t);
   };
+#if !FMX_RDS_DIRECT_PHASE
   auto mix = [&](float x, float ph) __attribute__((always_inline)) {
     float sn, cs;
 #if FMX_HWSIN_RDS
@@ -2615,9 +2628,21 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
 #endif
     return f32x2{x, x} * f32x2{cs, sn};
   };
+#endif
+  // x * polar(1, -phase(w)) from the NCO word: v_sin / v_cos take turns
+  auto mix_word = [&](float x, uint32_t w) __attribute__((always_inline)) {
+    const float r = (float)(int32_t)w * 2.3283064365386963e-10f; // w / 2^32 turns, in [-0.5, 0.5)
+    const float sn = -__builtin_amdgcn_sinf(r);
+    const float cs = __builtin_amdgcn_cosf(r);
+    return f32x2{x, x} * f32x2{cs, sn};
+  };
   // NCO step + quad-phase wrapper (liquid_wrappers.cpp:271-312)
   auto nco_step = [&]() __attribute__((always_inline)) {
     theta += dtheta;
+#if FMX_RDS_DIRECT_PHASE
+    ssr++;
+    return;
+#endif
     const float now = d_nco_phase(theta);
     float delta = now - prev_f0;
     delta = d_unwrap(delta);
@@ -2786,7 +2811,11 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     if (act && t < count) {
       const int j = (int)(ssr % FMX_RDS_DECIM);
       const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
+#if FMX_RDS_DIRECT_PHASE
+      acc_add(mix_word(read1(t), theta), t, &D->rds_rows[jp][0]);
+#else
       acc_add(mix(read1(t), phase0), t, &D->rds_rows[jp][0]);
+#endif
       if (j == 0) fir_output();
       nco_step();
     }
@@ -2807,6 +2836,16 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     t = __builtin_amdgcn_readfirstlane(t); // wave-uniform
     need(t, U);
     const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;
+#if FMX_RDS_DIRECT_PHASE
+    float xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xs[u] = read1(t + u);
+    f32x2 mx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) mx[u] = mix_word(xs[u], theta + (uint32_t)u * dtheta);
+    theta += (uint32_t)(U - 1) * dtheta;
+    ssr += U - 1;
+#else
     float ph[U];
     ph[0] = phase0;
     {
@@ -2833,6 +2872,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     f32x2 mx[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) mx[u] = mix(xs[u], ph[u]);
+#endif
     // accumulator by accumulator, the chunk's samples oldest first: every
     // partial sum sees the same products in the same order as the
     // per-sample push (h[jp + 24 i] * mix, jp = 24 - j); the 8 taps of one
@@ -2889,8 +2929,14 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   FmxRdsState *out = a.st + c;
   out->theta = theta;
   out->dtheta = dtheta;
+#if FMX_RDS_DIRECT_PHASE
+  // the wrapper's phases as the reference would hold them (= the NCO phase)
+  out->prev_f0 = d_nco_phase(theta);
+  out->phase0 = d_unwrap(d_nco_phase(theta));
+#else
   out->prev_f0 = prev_f0;
   out->phase0 = phase0;
+#endif
   out->sample_since_reset = ssr;
   out->ring_pos = ring0 + (uint32_t)count;
   out->rebuild = 0;
