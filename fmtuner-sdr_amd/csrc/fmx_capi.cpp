@@ -1737,6 +1737,14 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
         v.push_back(static_cast<float>(q / 4096.0));
       }
       break;
+    case 13: // k_fe8 MFMA decimator taps back from the A fragments (row 0 lanes), as dec_taps_raw
+      for (int k = 0; k < d->dec_len; ++k) {
+        const int dd = d->dec_len - k;
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->dec_frag[ks][0][l][j]) + f16_value(d->dec_frag[ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 65536.0 * 127.5));
+      }
+      break;
     case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
       for (int cp = 0; cp < 2; ++cp)
         for (int k = 0; k < d->dec_len; ++k) {

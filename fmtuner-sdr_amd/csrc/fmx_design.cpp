@@ -232,6 +232,20 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
         d->dec_q16[cp][0][x] = hi;
         d->dec_q16[cp][1][x] = lo;
       }
+    const int KS = (15 * M + L + 1 + 31) / 32;
+    if (KS > FMX_DEC_KS_MAX) {
+      *err = "decimator too long for the MFMA fragment table";
+      return FMX_E_INVALID;
+    }
+    for (int ks = 0; ks < FMX_DEC_KS_MAX; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int dd = 32 * ks + 8 * (l >> 4) + j - M * (l & 15);
+          const float q = (ks < KS && dd >= 1 && dd <= L) ? d->dec_taps[L - dd] * 65536.0f : 0.0f;
+          const uint16_t hi = f32_to_f16_bits(q);
+          d->dec_frag[ks][0][l][j] = hi;
+          d->dec_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+        }
     d->dec_dc16 = static_cast<float>(-0.5 * 65536.0 * dc);
     d->dec_scale16 = d->dec_scale * (1.0f / 65536.0f);
   } else {

@@ -29,6 +29,7 @@
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
 #define FMX_DQ_MIN (-152)    // k_fe8 MFMA decimator tap table: first tap offset (multiple of 8, <= -15 M)
 #define FMX_DQ_N 608         // entries per copy and split (covers 32 K-steps of 16 outputs for M <= 10)
+#define FMX_DEC_KS_MAX 16    // K steps of the MFMA decimator: ceil((15 M + L + 1) / 32) for M <= 10
 #define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
 #define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
 
@@ -57,6 +58,9 @@ typedef struct {
   // fragment starts 8-B aligned in one of the copies.  Output y = (acc -
   // dec_dc16) * dec_scale16 with acc = sum (byte - 128) * q.
   uint16_t dec_q16[2][2][FMX_DQ_N] __attribute__((aligned(16))); // [copy][hi, lo][d - FMX_DQ_MIN + 2 * copy]
+  // the same taps as per-lane A fragments (as pilot_frag):
+  // dec_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - M (l & 15)]
+  uint16_t dec_frag[FMX_DEC_KS_MAX][2][64][8] __attribute__((aligned(16)));
   float dec_dc16, dec_scale16;
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
   int iq_len[FMX_IQ_DESIGNS];

@@ -3156,6 +3156,9 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 #ifndef FMX_IQ_MFMA
 #define FMX_IQ_MFMA 1 // k_fe8 IQ FIR on v_mfma_f32_16x16x32_f16 (0: packed-FMA fir8_c, A/B runs)
 #endif
+#ifndef FMX_DEC_FRAG
+#define FMX_DEC_FRAG 1 // MFMA decimator A fragments from FmxDesign::dec_frag (0: per-chunk LDS tap table)
+#endif
 #ifndef FMX_RS_PACKED
 #define FMX_RS_PACKED 0 // 1: k_fe8's RDS resampler on packed FP32 (v_pk_mul / v_pk_add), see the resampler
 #endif
@@ -3400,7 +3403,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
     // ================= decimator =================
-#if FMX_DEC_MFMA
+#if FMX_DEC_MFMA && !FMX_DEC_FRAG
     // the MFMA tap tables into the MPX image's chunk part (dead until the
     // discriminator below writes it)
     {
@@ -3452,10 +3455,18 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
       typedef float f32x4_t __attribute__((ext_vector_type(4)));
       constexpr int KS = (15 * M + L + 1 + 31) / 32;
-      static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN, "tap table range");
+      static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN && KS <= FMX_DEC_KS_MAX, "tap table range");
       const int col = lane & 15, g = lane >> 4;
       const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0 (even)
+#if FMX_DEC_FRAG
+      // A fragments from the design (FmxDesign::dec_frag, 16-B per lane, one
+      // K step ahead) instead of 8 dword LDS reads per K step
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag[0][0][0][0]) + lane;
+      u32x4 fh = fa[0], fl = fa[64];
+      (void)d00;
+#else
       const uint32_t *ta = reinterpret_cast<const uint32_t *>(smem + LY::TQ) + ((d00 - FMX_DQ_MIN) >> 1);
+#endif
       const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 16 * g;
       f32x4_t acc[2][2];
 #pragma unroll
@@ -3474,10 +3485,18 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #pragma unroll FMX_DEC_KS_UNROLL
       for (int ks = 0; ks < KS; ++ks) {
 #endif
+#if FMX_DEC_FRAG
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, fh), alo = __builtin_bit_cast(f16x8_t, fl);
+        if (ks + 1 < KS) {
+          fh = fa[128 * (ks + 1)];
+          fl = fa[128 * (ks + 1) + 64];
+        }
+#else
         // 4-B aligned fragments (d00 is even): dword reads
         const uint32_t *th = ta + 16 * ks, *tlo = ta + FMX_DQ_N / 2 + 16 * ks;
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, u32x4{th[0], th[1], th[2], th[3]});
         const f16x8_t alo = __builtin_bit_cast(f16x8_t, u32x4{tlo[0], tlo[1], tlo[2], tlo[3]});
+#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const u32x4 w = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * ks);

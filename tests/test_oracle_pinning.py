@@ -260,6 +260,10 @@ def test_mfma_decimator_tap_tables(fmx, rates):
         err = np.abs(q[cp * raw.size:(cp + 1) * raw.size] - raw)
         # the taps pass through float32 (/127.5, then *127.5 here): a few ulp of the largest
         assert err.max() <= scale * 2.0 ** -21, (cp, err.max() / scale)
+    # the per-lane A fragments k_fe8 reads (FmxDesign::dec_frag)
+    fr = fmx.design_taps(cfg, 13).astype(np.float64)
+    assert fr.size == raw.size
+    assert np.abs(fr - raw).max() <= scale * 2.0 ** -21
 
 
 @pytest.mark.parametrize("rates", CONFIGS)

@@ -101,3 +101,40 @@ def test_gpu_signal_level(fmx, oracle, torch_cuda, iq_rate, n, noise):
             assert abs(got.level120 - r["level120"]) <= 1e-4
             assert got.hard_clip_ratio == r["hard_clip_ratio"] and got.near_clip_ratio == r["near_clip_ratio"]
             assert abs(got.level120_smoothed - sm(r["level120"])) <= 1e-4
+
+
+@pytest.mark.gpu
+def test_gpu_scan_line_three_reads(fmx, oracle, torch_cuda):
+    """SURVEY 8f row 2, the multi-channel scan (main.cpp:1064-1121): every
+    channel is one scan point; three process_block reads give three
+    level120 values per point (computeSignalLevel of each read), averaged in
+    double and formatted by fmx_xdr_scan_line.  The expected line applies the
+    reference's signal_level.cpp (oracle/_ref) to the same IQ reads."""
+    C_, nblk, n = 16, 3, 4096
+    # a spread of signal strengths and noise over the points
+    rows = []
+    for c in range(C_):
+        scfg = fmx.make_synth(kind=2, noise_std=0.02 * (c % 4), amplitude=0.05 + 0.06 * c, n_bits=4096)
+        bits, _ = fmx.synth_rds_bits(scfg, c, 1)
+        rows.append(fmx.synth_host(scfg, c, 1, 0, n * 10 * nblk, bits)[0])
+    iq = np.stack(rows)
+    cfg = fmx.make_config()
+    params = (20, 0.5, -2.0, -60.0, -15.0)
+    g = _run_gpu(fmx, torch_cuda, cfg, iq, nblk, n, params)
+    freqs = [87500 + 100 * c for c in range(C_)]
+    gpu_sum = [sum(float(g[b][c].level120) for b in range(nblk)) for c in range(C_)]
+    checker = O.ref_signal_level if O.ref_available() else O.signal_level
+    ref_sum = [sum(float(np.float32(checker(iq[c, b * 2 * n * 10:(b + 1) * 2 * n * 10], *params)["level120"]))
+                   for b in range(nblk)) for c in range(C_)]
+    line = fmx.xdr_scan_line(freqs, gpu_sum, [nblk] * C_)
+    want = "U" + ",".join("%d=%.1f" % (f, float(np.float32(s / nblk))) for f, s in zip(freqs, ref_sum))
+    print(line)
+    print(want)
+    assert line.startswith("U") and len(line[1:].split(",")) == C_
+    for pg, pw, sg, sw in zip(line[1:].split(","), want[1:].split(","), gpu_sum, ref_sum):
+        fg, vg = pg.split("=")
+        fw, vw = pw.split("=")
+        # per-read levels agree to 1e-4 (test_gpu_signal_level); the one-decimal
+        # text can differ by one display step only at a rounding boundary
+        assert fg == fw and abs(sg - sw) <= 3e-4 and abs(float(vg) - float(vw)) <= 0.1 + 1e-9, (pg, pw, sg, sw)
+    assert len(set(v.split("=")[1] for v in line[1:].split(","))) > C_ // 2  # a spread of levels

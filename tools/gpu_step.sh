@@ -1,7 +1,9 @@
 #!/bin/bash
+set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
-L=$PWD/fmtuner-sdr_amd
-STEREO=0 RDS_STAGE=0 FMX_DIAG_RDS_DUMP=1 FMX_LIB=$L/libfmx_pk2.so timeout -k 10 200 python tools/gpu_determinism.py 4096 8 1 > gpurun_out/det_pk2.log 2>&1; echo "pk2 dump rc=$? $(tail -1 gpurun_out/det_pk2.log)"
-FMX_LIB=$L/libfmx_pk2.so FMX_SERIAL=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/iso_pk2.json 2>/dev/null && python3 -c "import json;d=json.load(open('gpurun_out/iso_pk2.json'));print('pk2 iso', {k:v['avg_ms'] for k,v in d['kernels'].items()})"
-FMX_SERIAL=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/iso_cur.json 2>/dev/null && python3 -c "import json;d=json.load(open('gpurun_out/iso_cur.json'));print('cur iso', {k:v['avg_ms'] for k,v in d['kernels'].items()})"
-exit 0
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -s --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log; grep -E "^U8" gpurun_out/gpu_tests.log | head -2 | cut -c1-200
+bash tools/gpu_iso.sh 20 base cur
+bash tools/gpu_abn.sh 3 100 base cur > gpurun_out/abn.log 2>&1; tail -2 gpurun_out/abn.log
+FMX_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_g2.json 2> gpurun_out/bench_g2.err || { tail -20 gpurun_out/bench_g2.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/bench_g2.json'));print(d['n_gpus'], d['value'], d['ms_per_step'], d['config']['channels_rank0'], d['config']['total_channels'], d.get('scan',{}).get('points'))"
