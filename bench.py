@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=None,
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc (tools/pmc_traffic.py); "
                          "default: the newest profiles/r*_pmc*.json")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no per-kernel HIP-event timing in the timed region (no roofline / kernels)")
     ap.add_argument("--no-signal-level", action="store_true",
                     help="diagnostic: skip the per-block RF level (computeSignalLevel) output")
     ap.add_argument("--dry-run", action="store_true",
@@ -282,7 +284,7 @@ def main():
         step(b)
     h.sync()
     groups_warm = int(gcnt.sum().item())
-    h.timing_enable(True)
+    h.timing_enable(not args.no_kernel_timing)
     if world > 1:
         dist.barrier()
     h.sync()
@@ -334,6 +336,8 @@ def main():
     # its own stream over the timed region), against SURVEY 8(d)'s 2.107 B/IQ ----
     units = C * n_iq  # IQ samples one launch of each kernel processes on this rank
     avg = {k: v[0] / max(v[1], 1) * 1e-3 for k, v in ktimes.items() if v[1] > 0}
+    if not avg:  # --no-kernel-timing (diagnostic): no per-kernel figures
+        avg = {k: float("nan") for k in ktimes}
     dom = max(avg, key=avg.get)
     dom_s = avg[dom]
     pmc_path = args.pmc_json or newest_pmc()
