@@ -1,14 +1,13 @@
 #!/bin/bash
 set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
-for r in 1 2; do
-timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 > gpurun_out/t_on.json 2>/dev/null
-timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --no-kernel-timing > gpurun_out/t_off.json 2>/dev/null || true
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; tail -1 gpurun_out/smoke.log
+bash tools/gpu_prof2.sh r02f > gpurun_out/prof2_r02f.log 2>&1 || { tail -20 gpurun_out/prof2_r02f.log; exit 1; }
+timeout -k 10 300 python bench.py --pmc-json gpurun_out/prof_r02f/pmc_frontend.json > gpurun_out/bench_r02f.json 2> gpurun_out/bench_r02f.err
+timeout -k 10 300 python bench.py --no-cpu-baseline --pmc-json gpurun_out/prof_r02f/pmc_frontend.json > gpurun_out/bench_r02f_repeat.json 2>> gpurun_out/bench_r02f.err
 python3 -c "
 import json
-a=json.load(open('gpurun_out/t_on.json'));print('timing on ', a['ms_per_step'], a['host_submit_ms'])
-" ; python3 -c "
-import json
-b=json.loads(open('gpurun_out/t_off.json').read().strip().splitlines()[-1]);print('timing off', b['ms_per_step'], b['host_submit_ms'])
-" || tail -5 gpurun_out/t_off.json
-done
+for f in ('bench_r02f','bench_r02f_repeat'):
+    d=json.load(open('gpurun_out/%s.json'%f)); print(f, d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], d['roofline']['valu_path']['frac'])"
