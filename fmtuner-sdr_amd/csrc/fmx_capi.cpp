@@ -90,6 +90,7 @@ struct Handle {
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
   bool lr_rows = false; // raw L/R in rows instead of octet tiles (FMX_LR_ROWS=1)
+  int fe_prio = 0;       // k_fe8 issue priority (FMX_FE_PRIO=0..3)
   bool diag_rds_dump = false; // FMX_DIAG_RDS_DUMP=1: RDS-rate samples over the caller's MPX rows
   // FMX_DIAG_HOST=1: host time per process_block part (printed at destroy)
   bool diag_host = false;
@@ -650,6 +651,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   h->serial_prio = 1;
   // FMX_LR_ROWS=1: raw L/R in [C][block] rows instead of octet tiles (A/B runs)
   if (const char *e = std::getenv("FMX_LR_ROWS"); e && e[0] == '1') h->lr_rows = true;
+  if (const char *e = std::getenv("FMX_FE_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->fe_prio = e[0] - '0';
   if (const char *e = std::getenv("FMX_DIAG_RDS_DUMP"); e && e[0] == '1') h->diag_rds_dump = true;
   if (const char *e = std::getenv("FMX_DIAG_HOST"); e && e[0] == '1') h->diag_host = true;
   if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
@@ -810,6 +812,7 @@ static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   a.rds_sched_n = h->t_rds.d_count[h->t_rds.cur];
   a.rds_group = h->t_rds.d_group[h->t_rds.cur];
   a.rds_sched_stride = h->t_rds.stride;
+  a.prio = h->fe_prio;
   return a;
 }
 

@@ -60,6 +60,7 @@ struct FeArgs {
   unsigned long long *dbg;    // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
+  int prio;          // k_fe8 waves' issue priority (s_setprio 0..3; FMX_FE_PRIO, A/B runs)
   // state
   uint8_t *dec_hist;
   int *dec_valid;

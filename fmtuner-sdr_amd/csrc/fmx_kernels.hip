@@ -3258,6 +3258,9 @@ template <int M, int TPP>
 __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP>;
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);

@@ -1,13 +1,4 @@
 #!/bin/bash
 set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -1 gpurun_out/gpu_tests.log
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; tail -1 gpurun_out/smoke.log
-bash tools/gpu_prof2.sh r02f > gpurun_out/prof2_r02f.log 2>&1 || { tail -20 gpurun_out/prof2_r02f.log; exit 1; }
-timeout -k 10 300 python bench.py --pmc-json gpurun_out/prof_r02f/pmc_frontend.json > gpurun_out/bench_r02f.json 2> gpurun_out/bench_r02f.err
-timeout -k 10 300 python bench.py --no-cpu-baseline --pmc-json gpurun_out/prof_r02f/pmc_frontend.json > gpurun_out/bench_r02f_repeat.json 2>> gpurun_out/bench_r02f.err
-python3 -c "
-import json
-for f in ('bench_r02f','bench_r02f_repeat'):
-    d=json.load(open('gpurun_out/%s.json'%f)); print(f, d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], d['roofline']['valu_path']['frac'])"
+bash tools/gpu_abn.sh 2 100 cur f1:FMX_FE_PRIO=1 f2:FMX_FE_PRIO=2 f3:FMX_FE_PRIO=3 s0:FMX_SERIAL_PRIO=0 > gpurun_out/abn.log 2>&1; tail -5 gpurun_out/abn.log
