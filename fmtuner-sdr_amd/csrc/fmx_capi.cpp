@@ -1732,14 +1732,6 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
-    case 12: // k_audio MFMA L/R FIR taps back from the f16 hi/lo fragments (row 0 lanes), as case 3
-      for (int k = 0; k < FMX_LR_LEN; ++k) {
-        const int dd = FMX_LR_LEN - 1 - k;
-        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
-        const double q = f16_value(d->lr_frag[ks][0][l][j]) + f16_value(d->lr_frag[ks][1][l][j]);
-        v.push_back(static_cast<float>(q / 4096.0));
-      }
-      break;
     case 13: // k_fe8 MFMA decimator taps back from the A fragments (row 0 lanes), as dec_taps_raw
       for (int k = 0; k < d->dec_len; ++k) {
         const int dd = d->dec_len - k;

@@ -16,7 +16,6 @@
 #define FMX_IQ_MAXLEN 121
 #define FMX_PILOT_MAX 511    // stereo_decoder.cpp:98 clamp
 #define FMX_LR_LEN 121       // stereo_decoder.cpp:110-111
-#define FMX_LR_KS 5          // K steps of k_audio's MFMA L/R FIR: (121 + 15) / 32 rounded up
 #define FMX_NPFB 32          // resamp_rrrf / symsync filter-bank size
 #define FMX_AF_SUB 24        // 2*m, m = 12 (liquid_primitives.h:145)
 #define FMX_RDS_RS_SUB 26    // 2*m, m = 13 (subcarrier.cpp:45)
@@ -90,8 +89,6 @@ typedef struct {
   float lr_taps[FMX_LR_LEN];
   float lr_pad[FMX_LR_LEN + FMX_PAD];
   float lr_pair[FMX_LR_LEN + FMX_PAD][2] __attribute__((aligned(8)));
-  // k_audio's MFMA L/R FIR, fragments as pilot_frag (taps * 2^12, hi / lo)
-  uint16_t lr_frag[FMX_LR_KS][2][64][8] __attribute__((aligned(16)));
   float nominal, pll_min, pll_max, pll_alpha, pll_beta;
   uint32_t pll_dtheta0;
   float blend_attack[3], blend_release[3], gate[3];

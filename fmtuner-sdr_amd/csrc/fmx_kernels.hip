@@ -1687,18 +1687,15 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 // FIR input image: pair i at i + i/8 (lanes 8 pairs apart land 9 apart:
 // conflict-free ds_read_b64)
 __device__ __forceinline__ int au_xi(int i) { return i + (i >> 3); }
-#ifndef FMX_AU_MFMA
-#define FMX_AU_MFMA 0 // 1: k_audio L/R FIR on v_mfma_f32_16x16x32_f16 (measured slower in the pipelined step)
-#endif
-#define AU_W (AU_HALO + AU2_T + 32) // FMX_AU_MFMA input image: history, chunk, zero slack
+#define AU_XN ((AU_HALO + AU2_T + 8) * 9 / 8 + 8)
 struct AuShared {
-#if FMX_AU_MFMA
-  _Float16 xim[4][AU_W] __attribute__((aligned(16))); // raw L hi, L lo, R hi, R lo (x 2^10)
-  float2 hist[2][AU_HALO];                             // the last AU_HALO raw (L, R) in f32, by chunk parity
-#else
-  float2 x[(AU_HALO + AU2_T + 8) * 9 / 8 + 8]; // raw (L, R), 120 of history first
-#endif
-  float2 f[AU_RHALO + AU2_T];                  // resampler input (L, R), 32 of history first
+  // one region, two lives per chunk: the raw (L, R) FIR image x (au_xi
+  // order, 120 of history first) until the FIR has read it, then the
+  // resampler input f (32 of history first, natural order).  Sharing it
+  // takes the workgroup from 45.6 to 29 KB of LDS: four workgroups per CU
+  // instead of three (isolated 0.206 ms at three, 0.263 at two).
+  float2 xf[AU_XN > AU_RHALO + AU2_T ? AU_XN : AU_RHALO + AU2_T];
+  float2 fh[AU_RHALO];                         // f's history between chunks
   float2 o[AU2_MAXOUT];                        // resampler outputs of the chunk
   float hT[FMX_AF_SUB][FMX_NPFB];              // resampler bank transposed: hT[n][b] = h_b[n]
   float lt[136] __attribute__((aligned(16)));  // L/R FIR taps, lt[k + 7] = h[k], zeros around
@@ -1775,15 +1772,12 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   // ---- carried state ----
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
-#if FMX_AU_MFMA
+  float2 *const X = S.xf; // FIR image (au_xi order)
+  float2 *const F = S.xf; // resampler input, after the FIR
   if (lrfir)
-    for (int h = tid; h < AU_HALO; h += 256) S.hist[0][h] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
-#else
-  if (lrfir)
-    for (int h = tid; h < AU_HALO; h += 256) S.x[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
-#endif
+    for (int h = tid; h < AU_HALO; h += 256) X[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
   if (af)
-    for (int h = tid; h < AU_RHALO; h += 256) S.f[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
+    for (int h = tid; h < AU_RHALO; h += 256) S.fh[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
   if (af && tid == 0) {
     if (mono) {
@@ -1810,10 +1804,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     S.eb = 0;
     S.count = 0;
   }
-#if !FMX_AU_MFMA
   if (lrfir)
     for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
-#endif
   // tiled input (raw L/R from k_pll): sample j of this channel at tin + ti(j)
   const bool tiled = a.in_tiled != 0;
   const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
@@ -1842,62 +1834,6 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       }
     }
     // ---- chunk input (all loads issued before the first LDS write) ----
-#if FMX_AU_MFMA
-    const int par_c = (n0 / AU2_T) & 1; // S.hist[par_c]: history before this chunk
-    if (lrfir) {
-      // 8 consecutive raw pairs per thread into the f16 hi / lo images (one
-      // 16-B write per image), the history images from the f32 copy, and the
-      // new history (the last AU_HALO pairs of history + chunk) into the other copy
-      float vl[8], vr[8];
-      const int jb = 8 * tid;
-      if (tiled && jb + 8 <= cnt) {
-        const float4 l0 = *reinterpret_cast<const float4 *>(inl + ti(n0 + jb));
-        const float4 l1 = *reinterpret_cast<const float4 *>(inl + ti(n0 + jb + 4));
-        const float4 r0 = *reinterpret_cast<const float4 *>(inr + ti(n0 + jb));
-        const float4 r1 = *reinterpret_cast<const float4 *>(inr + ti(n0 + jb + 4));
-        vl[0] = l0.x; vl[1] = l0.y; vl[2] = l0.z; vl[3] = l0.w; vl[4] = l1.x; vl[5] = l1.y; vl[6] = l1.z; vl[7] = l1.w;
-        vr[0] = r0.x; vr[1] = r0.y; vr[2] = r0.z; vr[3] = r0.w; vr[4] = r1.x; vr[5] = r1.y; vr[6] = r1.z; vr[7] = r1.w;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          vl[r] = (jb + r < cnt) ? inl[ti(n0 + jb + r)] : 0.0f;
-          vr[r] = (jb + r < cnt) ? inr[ti(n0 + jb + r)] : 0.0f;
-        }
-      }
-      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-      f16x8_t lh, ll, rh, rl;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float sl_ = vl[r] * 1024.0f, sr_ = vr[r] * 1024.0f;
-        lh[r] = (_Float16)sl_;
-        ll[r] = (_Float16)(sl_ - (float)lh[r]);
-        rh[r] = (_Float16)sr_;
-        rl[r] = (_Float16)(sr_ - (float)rh[r]);
-      }
-      *reinterpret_cast<f16x8_t *>(&S.xim[0][AU_HALO + jb]) = lh;
-      *reinterpret_cast<f16x8_t *>(&S.xim[1][AU_HALO + jb]) = ll;
-      *reinterpret_cast<f16x8_t *>(&S.xim[2][AU_HALO + jb]) = rh;
-      *reinterpret_cast<f16x8_t *>(&S.xim[3][AU_HALO + jb]) = rl;
-      float2 *hn = S.hist[par_c ^ 1];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int j = jb + r;
-        if (j < cnt && j >= cnt - AU_HALO) hn[j - (cnt - AU_HALO)] = make_float2(vl[r], vr[r]);
-      }
-      if (tid < AU_HALO) {
-        const float2 v = S.hist[par_c][tid];
-        if (tid < AU_HALO - cnt) hn[tid] = S.hist[par_c][cnt + tid]; // short chunk: older history stays
-        const float sl_ = v.x * 1024.0f, sr_ = v.y * 1024.0f;
-        const _Float16 a0 = (_Float16)sl_, a1 = (_Float16)sr_;
-        S.xim[0][tid] = a0;
-        S.xim[1][tid] = (_Float16)(sl_ - (float)a0);
-        S.xim[2][tid] = a1;
-        S.xim[3][tid] = (_Float16)(sr_ - (float)a1);
-      }
-      if (tid < 32) S.xim[0][AU_HALO + AU2_T + tid] = S.xim[1][AU_HALO + AU2_T + tid] =
-          S.xim[2][AU_HALO + AU2_T + tid] = S.xim[3][AU_HALO + AU2_T + tid] = (_Float16)0.0f;
-    } else
-#endif
     {
       float vl[AU2_PT], vr[AU2_PT];
 #pragma unroll
@@ -1909,77 +1845,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {
         const int j = tid + 256 * k;
-#if FMX_AU_MFMA
-        if (j < cnt) S.f[AU_RHALO + j] = make_float2(vl[k], vr[k]);
-#else
-        if (lrfir) S.x[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
-        else if (j < cnt) S.f[AU_RHALO + j] = make_float2(vl[k], vr[k]);
-#endif
+        if (lrfir) X[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
+        else if (j < cnt) F[AU_RHALO + j] = make_float2(vl[k], vr[k]);
       }
+      if (!lrfir && af && tid < AU_RHALO) F[tid] = S.fh[tid];
     }
     if (tid == 0) S.ee = S.eb;
     __syncthreads();
     // ---- L/R FIR: outputs j0 .. j0+7, inputs j0-120 .. j0+7 ----
-#if FMX_AU_MFMA
-    if (lrfir) {
-      // v_mfma_f32_16x16x32_f16 tiles as k_fe8's IQ FIR: 16 outputs (rows,
-      // A = taps, FmxDesign::lr_frag) of 16 blocks of 16 outputs (columns, B
-      // = the L or R images), three MFMAs per K step and channel (hi*hi,
-      // hi*lo, lo*hi); each wave two tiles (512 outputs) of L and of R
-      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-      typedef float f32x4_t __attribute__((ext_vector_type(4)));
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      constexpr int P8 = FMX_LR_LEN; // 8k + 1: no leading zero taps
-      static_assert(((FMX_LR_LEN + 6) & ~7) + 1 == FMX_LR_LEN && FMX_LR_LEN - 1 == AU_HALO, "L/R FIR geometry");
-      const int lane = tid & 63, wave = tid >> 6;
-      const int col = lane & 15, g = lane >> 4;
-      const int xb = AU_HALO + 16 * (32 * wave + col) - (P8 - 1) + 8 * g;
-      const f16x8_t *blh = reinterpret_cast<const f16x8_t *>(&S.xim[0][xb]);
-      const f16x8_t *bll = reinterpret_cast<const f16x8_t *>(&S.xim[1][xb]);
-      const f16x8_t *brh = reinterpret_cast<const f16x8_t *>(&S.xim[2][xb]);
-      const f16x8_t *brl = reinterpret_cast<const f16x8_t *>(&S.xim[3][xb]);
-      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->lr_frag[0][0][0][0]) + lane;
-      f32x4_t al_[2], ar_[2];
-      al_[0] = al_[1] = ar_[0] = ar_[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-      u32x4 ah = fa[0], alo_ = fa[64];
-#pragma unroll
-      for (int ks = 0; ks < FMX_LR_KS; ++ks) {
-        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, alo_);
-        if (ks + 1 < FMX_LR_KS) {
-          ah = fa[128 * (ks + 1)];
-          alo_ = fa[128 * (ks + 1) + 64];
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const f16x8_t lhi = blh[32 * u + 4 * ks], llo = bll[32 * u + 4 * ks];
-          const f16x8_t rhi = brh[32 * u + 4 * ks], rlo = brl[32 * u + 4 * ks];
-          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, lhi, al_[u], 0, 0, 0);
-          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rhi, ar_[u], 0, 0, 0);
-          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, llo, al_[u], 0, 0, 0);
-          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rlo, ar_[u], 0, 0, 0);
-          al_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, lhi, al_[u], 0, 0, 0);
-          ar_[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, rhi, ar_[u], 0, 0, 0);
-        }
-      }
-      const float osc = sc * (1.0f / (4096.0f * 1024.0f)); // exact power-of-two rescale
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g; // lane: outputs o .. o + 3
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int j = o + i;
-          if (j < cnt) {
-            const float2 y = make_float2(al_[u][i] * osc, ar_[u][i] * osc);
-            if (af) S.f[AU_RHALO + j] = y;
-            if (a.lr_out_l) {
-              a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
-              a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
-            }
-          }
-        }
-      }
-    }
-#else
+    float2 cx = make_float2(0.0f, 0.0f); // the next chunk's FIR history (X is overwritten by F)
     if (lrfir) {
       const int j0 = AU2_PT * tid;
       f32x2 acc[AU2_PT];
@@ -1995,7 +1869,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
                              t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w};
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const float2 v = S.x[au_xi(j0 + m0 + u)]; // input j0 - 120 + m0 + u
+          const float2 v = X[au_xi(j0 + m0 + u)]; // input j0 - 120 + m0 + u
           const f32x2 vv = f32x2{v.x, v.y};
 #pragma unroll
           for (int r = 0; r < AU2_PT; ++r) {
@@ -2004,12 +1878,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
           }
         }
       }
+      if (tid < AU_HALO) cx = X[au_xi(tid + cnt)];
+      __syncthreads(); // X is read: F takes its place
+      if (af && tid < AU_RHALO) F[tid] = S.fh[tid];
 #pragma unroll
       for (int r = 0; r < AU2_PT; ++r) {
         const int j = j0 + r;
         if (j < cnt) {
           const float2 y = make_float2(acc[r].x * sc, acc[r].y * sc);
-          if (af) S.f[AU_RHALO + j] = y;
+          if (af) F[AU_RHALO + j] = y;
           if (a.lr_out_l) {
             a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
             a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
@@ -2017,7 +1894,6 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         }
       }
     }
-#endif
     __syncthreads();
     if (af) {
       // ---- resampler: one schedule entry per thread ----
@@ -2035,8 +1911,8 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
           f32x2 y0 = f32x2{0.0f, 0.0f}, y1 = f32x2{0.0f, 0.0f};
 #pragma unroll
           for (int m = 0; m < FMX_AF_SUB; ++m) {
-            const float2 v0 = S.f[AU_RHALO + i0 - (FMX_AF_SUB - 1) + m];
-            const float2 v1 = S.f[AU_RHALO + i - (FMX_AF_SUB - 1) + m];
+            const float2 v0 = F[AU_RHALO + i0 - (FMX_AF_SUB - 1) + m];
+            const float2 v1 = F[AU_RHALO + i - (FMX_AF_SUB - 1) + m];
             const float h0 = S.hT[FMX_AF_SUB - 1 - m][b0], h1 = S.hT[FMX_AF_SUB - 1 - m][b1];
             const f32x2 p0 = f32x2{h0, h0} * f32x2{v0.x, v0.y};
             const f32x2 p1 = f32x2{h1, h1} * f32x2{v1.x, v1.y};
@@ -2139,33 +2015,23 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     }
     // ---- carry halos ----
     {
-      float2 cx = make_float2(0.0f, 0.0f), cf = make_float2(0.0f, 0.0f);
-#if !FMX_AU_MFMA
-      if (lrfir && tid < AU_HALO) cx = S.x[au_xi(tid + cnt)];
-#endif
-      if (af && tid < AU_RHALO) cf = S.f[tid + cnt];
-      __syncthreads();
-#if !FMX_AU_MFMA
-      if (lrfir && tid < AU_HALO) S.x[au_xi(tid)] = cx;
-#endif
-      (void)cx;
-      if (af && tid < AU_RHALO) S.f[tid] = cf;
+      float2 cf = make_float2(0.0f, 0.0f);
+      if (af && tid < AU_RHALO) cf = F[tid + cnt];
+      __syncthreads(); // F is dead: X takes its place again
+      if (lrfir && tid < AU_HALO) X[au_xi(tid)] = cx;
+      if (af && tid < AU_RHALO) S.fh[tid] = cf;
       __syncthreads();
     }
   }
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) {
-#if FMX_AU_MFMA
-      const float2 v = S.hist[((n + AU2_T - 1) / AU2_T) & 1][h]; // after the last chunk
-#else
-      const float2 v = S.x[au_xi(h)];
-#endif
+      const float2 v = X[au_xi(h)];
       lrh[h] = v.x;
       lrh[(FMX_LR_LEN - 1) + h] = v.y;
     }
   if (af) {
     for (int h = tid; h < AU_RHALO; h += 256) {
-      const float2 v = S.f[h];
+      const float2 v = S.fh[h];
       win[h] = v.x;
       if (!mono) win[32 + h] = v.y;
     }
@@ -4073,7 +3939,15 @@ int launch_pll(const PllArgs &a, void *stream) {
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
+  // diagnostic: FMX_DIAG_AU_LDS=<bytes> launches with more LDS (fewer workgroups per CU)
+  static const size_t au_lds = [] {
+    const char *e = std::getenv("FMX_DIAG_AU_LDS");
+    const size_t v = e ? (size_t)std::atol(e) : (size_t)0;
+    if (v > sizeof(AuShared))
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_audio), hipFuncAttributeMaxDynamicSharedMemorySize, (int)v);
+    return v > sizeof(AuShared) ? v : sizeof(AuShared);
+  }();
+  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), au_lds, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_rds(const RdsArgs &a, void *stream) {

@@ -290,14 +290,3 @@ def test_mfma_iq_fir_tap_fragments(fmx, rates, bw):
     assert q.size == h.size and h.size in (81, 121)
     err = np.abs(q - h)
     assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()
-
-
-def test_mfma_lr_fir_tap_fragments(fmx):
-    """k_audio's MFMA L/R FIR takes the 121 L/R LPF taps as f16 hi + lo
-    fragments (x 2^12, FmxDesign::lr_frag): they give the taps back to 22 bits."""
-    cfg = fmx.make_config()
-    h = fmx.design_taps(cfg, 3).astype(np.float64)
-    q = fmx.design_taps(cfg, 12).astype(np.float64)
-    assert q.size == h.size == 121
-    err = np.abs(q - h)
-    assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()
