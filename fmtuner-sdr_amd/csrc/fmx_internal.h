@@ -174,8 +174,11 @@ struct ResetArgs {
   float *rds_hist;
   int *mute;      // [C][2]
 };
-#define FMX_NBUF 3                // per-step intermediates (MPX, pilot, RDS-rate, raw L/R): front end k
-                                  // runs while stereo/RDS/audio of steps k-1, k-2 drain
+// per-step intermediates (MPX, pilot, RDS-rate, raw L/R): front end k runs
+// while stereo/RDS/audio of steps k-1, k-2 drain
+#ifndef FMX_NBUF
+#define FMX_NBUF 3
+#endif
 #define FMX_ST_BUFS (FMX_NBUF + 1) // rotating stereo-history buffers
 enum ResetParts {
   RS_DECIM = 1,    // ComplexDecimator::reset
