@@ -1615,9 +1615,16 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
           const float mag2 = sh->s1[sb][F_MAG2][row[j]][tt[j]];
           const float pf = sh->s1[sb][F_FREQ][row[j]][tt[j]];
           const float gate = sh->s2_gate[row[j]];
+#if FMX_PLL_FAST_DIV
+          // hardware sqrt / reciprocal (~1 ulp) instead of the IEEE sequences
+          const float magNow = __builtin_amdgcn_sqrtf(mag2);
+          const float ratioNow = pbm * __builtin_amdgcn_rcpf(fmaxf(mm, 1e-3f));
+          const float cohNow = magNow * __builtin_amdgcn_rcpf(fmaxf(pbm, 1e-4f));
+#else
           const float magNow = sqrtf(mag2);
           const float ratioNow = pbm / fmaxf(mm, 1e-3f);
           const float cohNow = magNow / fmaxf(pbm, 1e-4f);
+#endif
           const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
           // blend_target(ratioNow, cohNow, errHzNow, mode, false, false, true, gate)
           constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cP = 320.0f - 180.0f;
@@ -3024,6 +3031,9 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 #endif
 #ifndef FMX_DEC_FRAG
 #define FMX_DEC_FRAG 1 // MFMA decimator A fragments from FmxDesign::dec_frag (0: per-chunk LDS tap table)
+#endif
+#ifndef FMX_PLL_FAST_DIV
+#define FMX_PLL_FAST_DIV 1 // k_pll W2: blend-target sqrt / divisions on v_sqrt / v_rcp (~1 ulp); 0: IEEE (A/B)
 #endif
 #ifndef FMX_RS_PACKED
 #define FMX_RS_PACKED 0 // 1: k_fe8's RDS resampler on packed FP32 (v_pk_mul / v_pk_add), see the resampler
