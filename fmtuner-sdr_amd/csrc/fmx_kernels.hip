@@ -1045,6 +1045,9 @@ __device__ __forceinline__ float blend_target(float ratio, float coh, float errH
 // The chain's sine: pll_sin_word (fmx_math.h) straight from the phase word
 // (11 VALU), or with FMX_PLL_SIN_WORD=0 the reference's float phase and
 // fmx_sincos_q (the outputs' arithmetic) for A/B parity runs.
+#ifndef FMX_PLL_FAST_DIV
+#define FMX_PLL_FAST_DIV 1 // k_pll W2: blend-target sqrt / divisions on v_sqrt / v_rcp (~1 ulp); 0: IEEE (A/B)
+#endif
 #ifndef FMX_PLL_SIN_WORD
 #define FMX_PLL_SIN_WORD 1
 #endif
@@ -3032,8 +3035,8 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 #ifndef FMX_DEC_FRAG
 #define FMX_DEC_FRAG 1 // MFMA decimator A fragments from FmxDesign::dec_frag (0: per-chunk LDS tap table)
 #endif
-#ifndef FMX_PLL_FAST_DIV
-#define FMX_PLL_FAST_DIV 1 // k_pll W2: blend-target sqrt / divisions on v_sqrt / v_rcp (~1 ulp); 0: IEEE (A/B)
+#ifndef FMX_RS_FMA
+#define FMX_RS_FMA 0 // 1: k_fe8's RDS resampler terms as scalar FMAs (k_fe8 isolated -1.7 %, step unchanged)
 #endif
 #ifndef FMX_RS_PACKED
 #define FMX_RS_PACKED 0 // 1: k_fe8's RDS resampler on packed FP32 (v_pk_mul / v_pk_add), see the resampler
@@ -3789,11 +3792,18 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
             const float v = xu[m];
             const f32x2 hm = hk[m];
             // as asm so that the vectorizer cannot pair them into v_pk_* again
+#if FMX_RS_FMA
+            // one FMA per term (one rounding instead of two; RDS groups stay
+            // bit-exact against the oracle, as k_rds's FMA partial sums)
+            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(y0) : "v"(hm.x), "v"(v), "v"(y0));
+            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(y1) : "v"(hm.y), "v"(v), "v"(y1));
+#else
             float p0, p1;
             asm("v_mul_f32 %0, %1, %2" : "=v"(p0) : "v"(hm.x), "v"(v));
             asm("v_mul_f32 %0, %1, %2" : "=v"(p1) : "v"(hm.y), "v"(v));
             asm("v_add_f32 %0, %1, %2" : "=v"(y0) : "v"(y0), "v"(p0));
             asm("v_add_f32 %0, %1, %2" : "=v"(y1) : "v"(y1), "v"(p1));
+#endif
           }
           const f32x2 y = {y0, y1};
 #endif
