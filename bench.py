@@ -254,6 +254,7 @@ def main():
     row = 2 * n_iq * nblk
     d_iq = torch.empty((C, row), dtype=torch.uint8, device=dev)
     h.synth_device(scfg, ch0, C, 0, n_iq * nblk, d_bits.data_ptr(), d_iq.data_ptr(), row)
+    h.sync()  # the synth (the handle's stream) has read d_bits before torch may reuse its memory
     del d_bits
     # ---- outputs ----
     pl = torch.empty((C, B), dtype=torch.float32, device=dev)

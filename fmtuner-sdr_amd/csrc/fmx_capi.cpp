@@ -36,12 +36,12 @@ namespace fmx {
 // Every step's schedules reach the GPU in ONE copy per set: slot b (step k
 // mod FMX_NBUF) is [group map (C ints) | counts (cap ints) | schedules (G x
 // stride)] in one device allocation, staged from a pinned host image of the
-// same layout.  process_block uploads the NEXT step's schedules one step
-// early, on the PLL stream (sB) while the front end runs, assuming the same
-// n and no reset in between (`spec`); a step that breaks the assumption rolls
-// the speculation back and uploads on sA as before.  On sA the uploads sat
-// between consecutive front-end kernels: 6 copies, ~0.1 ms per step
-// (rocprofv3 --memory-copy-trace).
+// same layout, copied by a small kernel on the stream of the set's only
+// reader, right before it (the RDS set on sA before the front end, the
+// audio set on sD before k_audio): stream order alone covers the slot, so
+// no event joins the streams for it.  (Round 2 uploaded the next step's
+// schedules one step early on sB: the front end then waited, through the
+// upload's event, for the previous step's k_pll -- 35-50 us per step.)
 #define FMX_HSLOTS 8 // pinned schedule images per timing set
 struct TimingSet {
   float del = 1.0f;
@@ -64,13 +64,7 @@ struct TimingSet {
   FmxSched *d_sched[FMX_NBUF] = {};
   int *d_count[FMX_NBUF] = {};
   int *d_group[FMX_NBUF] = {};
-  hipEvent_t ev_up[FMX_NBUF] = {}; // after the last copy into d_slot[b]
-  bool ev_up_set[FMX_NBUF] = {};
-  // speculation: state before the speculative advance, its n and slot
-  bool spec = false;
-  int spec_n = 0, spec_slot = -1;
-  std::vector<ResampTiming> spec_groups;
-  std::vector<int> spec_map;
+  hipStream_t up_stream = nullptr; // stream of the last copy into the slots (the set's reader)
 };
 
 struct Handle {
@@ -86,18 +80,8 @@ struct Handle {
   // audio of step k overlaps the PLL of step k+1 (raw L/R double-buffered).
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
-  hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr;
+  hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr, evTmpU = nullptr;
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
-  int serial_prio = 1; // k_pll / k_rds waves at raised issue priority (s_setprio 2)
-  bool lr_rows = false; // raw L/R in rows instead of octet tiles (FMX_LR_ROWS=1)
-  int fe_prio = 0;       // k_fe8 issue priority (FMX_FE_PRIO=0..3)
-  bool diag_rds_dump = false; // FMX_DIAG_RDS_DUMP=1: RDS-rate samples over the caller's MPX rows
-  // FMX_DIAG_HOST=1: host time per process_block part (printed at destroy)
-  bool diag_host = false;
-  double hd_sync = 0, hd_sync_max = 0, hd_sim = 0, hd_total = 0, hd_total_max = 0;
-  double hd_seg[10] = {}, hd_seg_max[10] = {};
-  std::chrono::steady_clock::time_point hd_last;
-  long hd_calls = 0;
   uint64_t step = 0;
   int st_idx = 0;
   FmxDesign *hdes = nullptr;
@@ -118,7 +102,7 @@ struct Handle {
   float *sig_smooth = nullptr;
   unsigned long long *sig_sums[FMX_NBUF] = {}; // [C][6] byte sums of step k (front end -> k_audio)
   bool sig_dirty = true;
-  unsigned long long *dbg = nullptr;  // frontend stage clocks when FMX_STAMPS=1
+  unsigned long long *dbg = nullptr;  // stage clocks (FMX_DIAG builds with STAMPS=1 kernels only)
   float2_t *iq_hist = nullptr;
   float *st_hist = nullptr, *lr_hist = nullptr, *af_win = nullptr, *af_iir = nullptr;
   float *mono_win = nullptr, *mono_iir = nullptr, *rds_hist = nullptr, *ring = nullptr;
@@ -137,9 +121,11 @@ struct Handle {
   TimingSet t_af, t_mono, t_rds;
   // kernel timing
   bool timing = false;
-  // diagnostic (FMX_DIAG_SKIP=rds,pll,audio): kernels left out of
-  // process_block to measure what the others cost together -- outputs invalid
+#if FMX_DIAG
+  // diagnostics build only (make variant V=diag KDEFS=-DFMX_DIAG=1): kernels
+  // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
   bool skip_rds = false, skip_pll = false, skip_audio = false;
+#endif
   struct Pending {
     int k;
     hipEvent_t a, b;
@@ -167,15 +153,10 @@ template <typename T> static int dalloc(Handle *h, T **p, size_t count) {
 }
 
 // Events that only order work on this device (stream joins, kernel timing)
-// skip the system-scope fence at record time (hipEventDisableSystemFence);
-// FMX_EVENT_SYSFENCE=1 keeps HIP's default, for A/B runs.
+// skip the system-scope fence at record time (hipEventDisableSystemFence).
 static unsigned ev_flags(bool timing) {
-  static const bool sysfence = [] {
-    const char *e = std::getenv("FMX_EVENT_SYSFENCE");
-    return e && e[0] == '1';
-  }();
   return (timing ? 0u : static_cast<unsigned>(hipEventDisableTiming)) |
-         (sysfence ? 0u : static_cast<unsigned>(hipEventDisableSystemFence));
+         static_cast<unsigned>(hipEventDisableSystemFence);
 }
 
 static hipEvent_t ev_get(Handle *h) {
@@ -274,7 +255,6 @@ static int tset_alloc_slots(Handle *h, TimingSet &t) {
     t.d_group[b] = reinterpret_cast<int *>(t.d_slot[b]);
     t.d_count[b] = t.d_group[b] + h->C;
     t.d_sched[b] = reinterpret_cast<FmxSched *>(t.d_slot[b] + off);
-    if (!t.ev_up[b]) HIP_TRY(hipEventCreateWithFlags(&t.ev_up[b], ev_flags(false)));
   }
   for (int i = 0; i < FMX_HSLOTS; ++i) {
     HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.h_slot[i]), t.slot_bytes, hipHostMallocMapped));
@@ -297,14 +277,6 @@ static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.cap_groups = 4;
   return tset_alloc_slots(h, t);
 }
-// undo a speculative advance (a reset, a stage call or another n follows)
-static void tset_unspec(TimingSet &t) {
-  if (!t.spec) return;
-  t.groups = t.spec_groups;
-  t.chan_group = t.spec_map;
-  t.spec = false;
-}
-
 // channel c's resampler was reset (liquid resamp_reset): move it to a group
 // in the post-reset state, creating the group if needed; drop empty groups.
 static void tset_reset_channel(TimingSet &t, int c) {
@@ -360,18 +332,15 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
     HIP_TRY(hipDeviceSynchronize());
     tset_free_slots(h, t);
     t.cap_groups = G * 2;
-    for (int b = 0; b < FMX_NBUF; ++b) t.ev_up_set[b] = false;
     for (int i = 0; i < FMX_HSLOTS; ++i) t.ev_h_set[i] = false;
     int rc;
     if ((rc = tset_alloc_slots(h, t)) != FMX_OK) return rc;
   }
   // the previous copy out of this pinned image must have run
-  const auto ts0 = std::chrono::steady_clock::now();
   const int hb = t.hnext;
   t.hnext = (hb + 1) % FMX_HSLOTS;
   t.hcur = hb;
   if (t.ev_h_set[hb]) HIP_TRY(hipEventSynchronize(t.ev_h[hb]));
-  const auto ts1 = std::chrono::steady_clock::now();
   FmxSched *hs = tset_hsched(h, t, hb);
   int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
   int mx = 0;
@@ -386,12 +355,6 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
   }
   std::memcpy(t.h_slot[hb], t.chan_group.data(), sizeof(int) * h->C);
   t.G = G;
-  if (h->diag_host) {
-    const double w = std::chrono::duration<double, std::milli>(ts1 - ts0).count();
-    h->hd_sync += w;
-    h->hd_sync_max = std::max(h->hd_sync_max, w);
-    h->hd_sim += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts1).count();
-  }
   if (max_count) *max_count = mx;
   return FMX_OK;
 }
@@ -399,48 +362,24 @@ static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
   // a copy kernel reading the mapped pinned image, not hipMemcpyAsync: the
   // runtime's small host-to-device copy blocked the host until the stream
-  // reached it (0.65 ms per step, up to 9 ms; FMX_DIAG_HOST part 4)
+  // reached it (round 2: 0.65 ms per step, up to 9 ms)
+  if (t.up_stream && t.up_stream != s) { // the slot's last reader ran on another stream (stage calls vs process_block)
+    HIP_TRY(hipEventRecord(h->evTmpU, t.up_stream));
+    HIP_TRY(hipStreamWaitEvent(s, h->evTmpU, 0));
+  }
   if (launch_copy16(t.h_dev[t.hcur], t.d_slot[buf], (bytes + 15) / 16, s) != FMX_OK) return FMX_E_HIP;
-  HIP_TRY(hipEventRecord(t.ev_up[buf], s));
-  t.ev_up_set[buf] = true;
   HIP_TRY(hipEventRecord(t.ev_h[t.hcur], s));
   t.ev_h_set[t.hcur] = true;
+  t.up_stream = s;
   return FMX_OK;
 }
-// Simulate n inputs and upload the schedules into slot `buf` on sA.
-static int tset_advance(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
-  tset_unspec(t);
+// Simulate n inputs and upload the schedules into slot `buf` on stream s,
+// the stream of the set's reader.
+static int tset_advance(Handle *h, TimingSet &t, int n, int buf, hipStream_t s, int *max_count) {
   int rc;
   if ((rc = tset_simulate(h, t, n, buf, max_count)) != FMX_OK) return rc;
-  // an earlier copy into this slot may still be queued on another stream
-  if (t.ev_up_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, t.ev_up[buf], 0));
-  if ((rc = tset_upload(h, t, buf, h->sA)) != FMX_OK) return rc;
-  t.cur = buf;
-  return FMX_OK;
-}
-// process_block: the schedules of this step were uploaded one step early
-// into `buf` (same n, nothing reset since) -- use them
-static bool tset_take_spec(TimingSet &t, int n, int buf) {
-  if (!t.spec || t.spec_n != n || t.spec_slot != buf) return false;
-  t.spec = false;
-  t.cur = buf;
-  return true;
-}
-// process_block: simulate the next step (n inputs again) from the state this
-// step leaves and upload it into `buf` on stream s
-static int tset_speculate(Handle *h, TimingSet &t, int n, int buf, hipStream_t s) {
-  t.spec_groups = t.groups;
-  t.spec_map = t.chan_group;
-  int rc;
-  if ((rc = tset_simulate(h, t, n, buf, nullptr)) != FMX_OK) {
-    t.spec = true;
-    tset_unspec(t);
-    return rc;
-  }
   if ((rc = tset_upload(h, t, buf, s)) != FMX_OK) return rc;
-  t.spec = true;
-  t.spec_n = n;
-  t.spec_slot = buf;
+  t.cur = buf;
   return FMX_OK;
 }
 
@@ -585,8 +524,6 @@ static void destroy(Handle *h) {
   for (auto e : h->pool) hipEventDestroy(e);
   for (TimingSet *t : {&h->t_af, &h->t_mono, &h->t_rds}) {
     tset_free_slots(h, *t);
-    for (hipEvent_t e : t->ev_up)
-      if (e) hipEventDestroy(e);
     for (hipEvent_t e : t->ev_h)
       if (e) hipEventDestroy(e);
   }
@@ -597,6 +534,7 @@ static void destroy(Handle *h) {
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
   if (h->evTmpD) hipEventDestroy(h->evTmpD);
+  if (h->evTmpU) hipEventDestroy(h->evTmpU);
   if (h->sD && h->sD != h->sA) hipStreamDestroy(h->sD);
   if (h->sC && h->sC != h->sA) hipStreamDestroy(h->sC);
   if (h->sB && h->sB != h->sA) hipStreamDestroy(h->sB);
@@ -640,56 +578,26 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     return FMX_E_INVALID;
   }
   HIP_TRY(hipStreamCreateWithFlags(&h->sA, hipStreamNonBlocking));
+  // The product library reads no environment: its outputs and its schedule
+  // depend only on the configuration and the calls.  A diagnostics build
+  // (FMX_DIAG=1, never the shipped libfmx.so) adds FMX_SERIAL=1 (every kernel
+  // on one stream: isolated per-kernel times) and FMX_DIAG_SKIP.
+  bool serial = false;
+#if FMX_DIAG
   if (const char *e = std::getenv("FMX_DIAG_SKIP")) {
     const std::string v(e);
     h->skip_rds = v.find("rds") != std::string::npos;
     h->skip_pll = v.find("pll") != std::string::npos;
     h->skip_audio = v.find("audio") != std::string::npos;
   }
-  // k_pll / k_rds waves run at raised issue priority beside the front end's
-  // (measured 1.39 -> 1.375 ms/step); FMX_SERIAL_PRIO=0 turns it off
-  h->serial_prio = 1;
-  // FMX_LR_ROWS=1: raw L/R in [C][block] rows instead of octet tiles (A/B runs)
-  if (const char *e = std::getenv("FMX_LR_ROWS"); e && e[0] == '1') h->lr_rows = true;
-  if (const char *e = std::getenv("FMX_FE_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->fe_prio = e[0] - '0';
-  if (const char *e = std::getenv("FMX_DIAG_RDS_DUMP"); e && e[0] == '1') h->diag_rds_dump = true;
-  if (const char *e = std::getenv("FMX_DIAG_HOST"); e && e[0] == '1') h->diag_host = true;
-  if (const char *e = std::getenv("FMX_SERIAL_PRIO"); e && e[0] >= '0' && e[0] <= '3') h->serial_prio = e[0] - '0';
-  if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') {
-    h->sB = h->sC = h->sD = h->sA; // diagnostic: one stream, kernels timed in isolation
+  if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') serial = true;
+#endif
+  if (serial) {
+    h->sB = h->sC = h->sD = h->sA;
   } else {
-    const char *cu = std::getenv("FMX_CU_SERIAL");
-    if (cu && cu[0]) {
-      // Experiment: pin the serial kernels (sB k_pll, sC k_rds) to every s-th
-      // CU ("s": both on CUs i % s == 0; "s,d": k_pll on i % s == 0, k_rds on
-      // i % s == s/2) and the data-parallel ones (sA, sD) to the rest
-      // (FMX_CU_PAR_ALL=1: everywhere).
-      const int s = std::max(2, std::atoi(cu));
-      const bool disjoint = std::strchr(cu, ',') != nullptr;
-      const bool par_all = std::getenv("FMX_CU_PAR_ALL") && std::getenv("FMX_CU_PAR_ALL")[0] == '1';
-      hipDeviceProp_t prop;
-      HIP_TRY(hipGetDeviceProperties(&prop, h->device));
-      const int ncu = prop.multiProcessorCount;
-      const int words = (ncu + 31) / 32;
-      std::vector<uint32_t> mb(words, 0), mc(words, 0), ma(words, 0);
-      for (int i = 0; i < ncu; ++i) {
-        const bool b = i % s == 0, c = disjoint ? i % s == s / 2 : b;
-        if (b) mb[i / 32] |= 1u << (i % 32);
-        if (c) mc[i / 32] |= 1u << (i % 32);
-        if (par_all || !(b || c)) ma[i / 32] |= 1u << (i % 32);
-      }
-      hipStream_t a2 = nullptr;
-      HIP_TRY(hipExtStreamCreateWithCUMask(&a2, words, ma.data()));
-      HIP_TRY(hipStreamDestroy(h->sA));
-      h->sA = a2;
-      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sB, words, mb.data()));
-      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sC, words, mc.data()));
-      HIP_TRY(hipExtStreamCreateWithCUMask(&h->sD, words, ma.data()));
-    } else {
-      HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
-      HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
-      HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
-    }
+    HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(false)));
@@ -700,6 +608,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, ev_flags(false)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, ev_flags(false)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpD, ev_flags(false)));
+  HIP_TRY(hipEventCreateWithFlags(&h->evTmpU, ev_flags(false)));
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
@@ -728,10 +637,12 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->fd_prev, C * 2)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->clip, C)) != FMX_OK) return rc;
   if ((rc = dalloc(h, &h->dsig, C * 4)) != FMX_OK) return rc;
+#if FMX_DIAG
   if (const char *e = std::getenv("FMX_STAMPS"); e && e[0] == '1') {
     if ((rc = dalloc(h, &h->dbg, 32)) != FMX_OK) return rc; // [0,8) frontend, [8,16) k_rds, [16,26) k_pll
     HIP_TRY(hipMemset(h->dbg, 0, 32 * sizeof(unsigned long long)));
   }
+#endif
   if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
   for (int b = 0; b < FMX_NBUF; ++b)
     if ((rc = dalloc(h, &h->sig_sums[b], C * 6)) != FMX_OK) return rc;
@@ -812,7 +723,6 @@ static FeArgs fe_args(Handle *h, int n, int mode, int buf) {
   a.rds_sched_n = h->t_rds.d_count[h->t_rds.cur];
   a.rds_group = h->t_rds.d_group[h->t_rds.cur];
   a.rds_sched_stride = h->t_rds.stride;
-  a.prio = h->fe_prio;
   return a;
 }
 
@@ -849,7 +759,7 @@ static void audio_signal_level(Handle *h, AudioArgs &a, const fmx_block_out *o, 
 }
 
 // raw L/R (k_pll -> k_audio) in octet tiles when the block is whole 4-sample tiles
-static int lr_tiled(const Handle *h) { return (h->cfg.block % 4 == 0 && !h->lr_rows) ? 1 : 0; }
+static int lr_tiled(const Handle *h) { return (h->cfg.block % 4 == 0) ? 1 : 0; }
 
 static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
   PllArgs a{};
@@ -868,7 +778,7 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
-  a.prio = h->serial_prio;
+  a.prio = 1; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
   return a;
 }
 
@@ -883,7 +793,7 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
-  a.prio = h->serial_prio;
+  a.prio = 1; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
   return a;
 }
 
@@ -901,16 +811,25 @@ static void step_done(Handle *h, bool stereo_hist_written) {
   h->step++;
 }
 
-// FMX_DIAG_HOST: host time of process_block's parts (0 prepare, 1 waits +
-// schedules, 2 front end, 3 RDS, 4 speculative uploads, 5 PLL, 6 audio)
-#define HD_MARK(i)                                                                               \
-  if (h->diag_host) {                                                                            \
-    const auto t_ = std::chrono::steady_clock::now();                                            \
-    const double w_ = std::chrono::duration<double, std::milli>(t_ - h->hd_last).count();        \
-    h->hd_seg[i] += w_;                                                                          \
-    h->hd_seg_max[i] = std::max(h->hd_seg_max[i], w_);                                           \
-    h->hd_last = t_;                                                                             \
-  }
+#if FMX_DIAG
+#define FMX_SKIP(k) (h->skip_##k)
+#else
+#define FMX_SKIP(k) false
+#endif
+
+// One reference block for every channel (main.cpp:1239-1308), on four
+// streams: sA front end, sC RDS, sB stereo PLL, sD audio.  Per step k (slot
+// buf = k mod FMX_NBUF of the intermediates):
+//   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evA(k)
+//   sC: [wait evA(k)] k_rds -> evC(k)
+//   sB: [wait evA(k)] k_pll -> evB(k)
+//   sD: [wait evB(k), evC(k)] [audio schedule copy] k_audio -> evD(k)
+// evD(k) therefore marks every reader of slot buf done (k_audio waits for
+// k_rds as well as k_pll), so the front end of step k+3 -- the next writer of
+// the slot, and through evA of the raw L/R slot k_pll writes -- needs ONE
+// cross-stream wait.  The resampler schedules go on the stream of their only
+// reader, right before it.  Front end k+1 runs while k_pll / k_rds / k_audio
+// of step k (and k-1) still run.
 static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *o) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
@@ -920,33 +839,17 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   if (n == 0) return FMX_OK;
   if ((rc = prepare(h)) != FMX_OK) return rc;
-  if (h->diag_host) h->hd_last = std::chrono::steady_clock::now();
   if (h->timing) harvest_timing(h);
-  HD_MARK(0);
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
   const int buf = static_cast<int>(h->step % FMX_NBUF);
-  // buffers `buf` (step k mod FMX_NBUF) were last read by step k-FMX_NBUF on
-  // sB / sC, and by its audio on sD in mono mode.  In stereo mode the audio of step k-2 only
-  // reads raw L/R, but waiting for it anyway throttles the frontend: measured,
-  // letting the frontends run ahead starves the PLL / audio chain (2.25 vs
-  // 1.61 ms per step, tools/gpu_timeline.sh)
-  if (h->evB_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[buf], 0));
-  if (h->evC_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[buf], 0));
-  if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
-  if (o->d_mpx) { // a caller-owned MPX buffer is read by step k-1's stereo/RDS/audio kernels
-    if (h->evB_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evB[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
-    if (h->evC_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evC[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
-    if (h->evD_set[(buf + FMX_NBUF - 1) % FMX_NBUF]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[(buf + FMX_NBUF - 1) % FMX_NBUF], 0));
-  }
-  // resampler schedules of this step: uploaded one step early (below), or now on sA
-  TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
-  const bool hit_rds = rds && tset_take_spec(h->t_rds, n, buf);
-  const bool hit_af = tset_take_spec(*tau, n, buf);
-  if (rds && !hit_rds && (rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
-  if (!hit_af && (rc = tset_advance(h, *tau, n, buf, nullptr)) != FMX_OK) return rc;
-  if (hit_rds) HIP_TRY(hipStreamWaitEvent(h->sA, h->t_rds.ev_up[buf], 0)); // the front end reads it
-  HD_MARK(1);
+  const int prev = (buf + FMX_NBUF - 1) % FMX_NBUF;
+  // slot buf was last read by step k-FMX_NBUF; a caller-owned MPX buffer by
+  // step k-1's readers
+  if (o->d_mpx && h->evD_set[prev]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[prev], 0));
+  else if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
+  // RDS resampler schedule of this step (read by the front end only)
+  if (rds && (rc = tset_advance(h, h->t_rds, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
   // ---- front end (sA) ----
@@ -974,15 +877,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
     dec_advance(h, n);
   }
-  if (h->diag_rds_dump && o->d_mpx && rds) {
-    // diagnostic (FMX_DIAG_RDS_DUMP=1): the step's 171 kHz RDS-rate samples over the caller's MPX rows
-    const size_t w = static_cast<size_t>(std::min(h->rds_stride, o->mpx_stride)) * sizeof(float);
-    HIP_TRY(hipMemcpy2DAsync(o->d_mpx, sizeof(float) * static_cast<size_t>(o->mpx_stride), h->rds_in[buf],
-                             sizeof(float) * static_cast<size_t>(h->rds_stride), w, static_cast<size_t>(h->C),
-                             hipMemcpyDeviceToDevice, h->sA));
-  }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
-  HD_MARK(2);
   // ---- RDS (sC) ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   if (rds) {
@@ -991,7 +886,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
     KTimer t(h, FMX_K_RDS, h->sC);
-    if (!h->skip_rds && (rc = launch_rds(a, h->sC)) != FMX_OK) {
+    if (!FMX_SKIP(rds) && (rc = launch_rds(a, h->sC)) != FMX_OK) {
       h->err = "rds launch failed";
       return rc;
     }
@@ -999,30 +894,16 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
   }
   HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
-  HD_MARK(3);
   h->evC_set[buf] = true;
-  // ---- next step's schedules, one step early, on sB ahead of this step's
-  // PLL (off the front end's stream).  Slot nb was last read by step
-  // k+1-FMX_NBUF's front end (sB's previous PLL waited for a later one) and
-  // audio (sD).
-  {
-    const int nb = (buf + 1) % FMX_NBUF;
-    if (h->evD_set[nb]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[nb], 0));
-    if (rds && (rc = tset_speculate(h, h->t_rds, n, nb, h->sB)) != FMX_OK) return rc;
-    if ((rc = tset_speculate(h, *tau, n, nb, h->sB)) != FMX_OK) return rc;
-  HD_MARK(4);
-  }
-  // ---- stereo PLL (sB), audio (sD) ----
+  // ---- stereo PLL (sB) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
   if (stereo) {
-    // raw L/R `buf` were last read by step k-FMX_NBUF's audio
-    if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sB, h->evD[buf], 0));
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;
     a.pilot_tenths_out = o->d_pilot_tenths;
     a.indicator_out = o->d_stereo_indicator;
     KTimer t(h, FMX_K_STEREO, h->sB);
-    if (!h->skip_pll && (rc = launch_pll(a, h->sB)) != FMX_OK) {
+    if (!FMX_SKIP(pll) && (rc = launch_pll(a, h->sB)) != FMX_OK) {
       h->err = "pll launch failed";
       return rc;
     }
@@ -1032,51 +913,42 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     if (o->d_stereo_indicator) HIP_TRY(hipMemsetAsync(o->d_stereo_indicator, 0, sizeof(int) * h->C, h->sB));
   }
   HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
-  HD_MARK(5);
   h->evB_set[buf] = true;
-  HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0)); // after the PLL (stereo) / the frontend (mono)
-  if (stereo) {
-    AudioArgs a = audio_args(h, n, 0, &h->t_af);
-    a.in_l = h->lraw[buf];
-    a.in_r = h->rraw[buf];
-    a.in_stride = h->cfg.block;
-    a.in_tiled = lr_tiled(h);
-    a.out_l = o->d_pcm_l;
-    a.out_r = o->d_pcm_r;
-    a.out_stride = o->pcm_stride;
-    a.out_count = o->d_pcm_count;
-    a.cap = h->cfg.block;
-    a.clamp = 1;
-    a.mute = h->mute;
-    a.mute_fade = h->cfg.out_rate / 200;
-    audio_signal_level(h, a, o, buf, n);
-    KTimer t(h, FMX_K_AUDIO, h->sD);
-    if (!h->skip_audio && (rc = launch_audio(a, h->sD)) != FMX_OK) {
-      h->err = "audio launch failed";
-      return rc;
+  // ---- audio (sD): after the PLL (stereo) / the front end (mono), and
+  // after k_rds, so that evD closes the step ----
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evC[buf], 0));
+  TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
+  if ((rc = tset_advance(h, *tau, n, buf, h->sD, nullptr)) != FMX_OK) return rc;
+  {
+    AudioArgs a = audio_args(h, n, stereo ? 0 : 3, tau);
+    if (stereo) {
+      a.in_l = h->lraw[buf];
+      a.in_r = h->rraw[buf];
+      a.in_stride = h->cfg.block;
+      a.in_tiled = lr_tiled(h);
+      a.cap = h->cfg.block;
+    } else {
+      a.in_l = mpx;
+      a.in_r = nullptr;
+      a.in_stride = mpx_stride;
+      a.cap = 1 << 30;
     }
-  } else {
-    AudioArgs a = audio_args(h, n, 3, &h->t_mono);
-    a.in_l = mpx;
-    a.in_r = nullptr;
-    a.in_stride = mpx_stride;
     a.out_l = o->d_pcm_l;
     a.out_r = o->d_pcm_r;
     a.out_stride = o->pcm_stride;
     a.out_count = o->d_pcm_count;
-    a.cap = 1 << 30;
     a.clamp = 1;
     a.mute = h->mute;
     a.mute_fade = h->cfg.out_rate / 200;
     audio_signal_level(h, a, o, buf, n);
     KTimer t(h, FMX_K_AUDIO, h->sD);
-    if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
+    if (!FMX_SKIP(audio) && (rc = launch_audio(a, h->sD)) != FMX_OK) {
       h->err = "audio launch failed";
       return rc;
     }
   }
   HIP_TRY(hipEventRecord(h->evD[buf], h->sD));
-  HD_MARK(6);
   h->evD_set[buf] = true;
   h->block_index++;
   step_done(h, stereo);
@@ -1088,7 +960,6 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
 static int stage_begin(Handle *h, int n) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
-  for (TimingSet *t : {&h->t_af, &h->t_mono, &h->t_rds}) tset_unspec(*t);
   if ((rc = prepare(h)) != FMX_OK) return rc;
   return join_into_A(h);
 }
@@ -1126,13 +997,6 @@ int fmx_create(const fmx_config *cfg, int n_channels, int device, void **handle)
 }
 
 int fmx_destroy(void *handle) {
-  if (Handle *h = H(handle); h && h->diag_host && h->hd_calls)
-    std::fprintf(stderr, "fmx host: %ld process_block calls, mean %.3f ms (max %.3f); schedule-slot waits %.3f ms/call "
-                 "(max %.3f), simulation %.3f ms/call\n", h->hd_calls, h->hd_total / h->hd_calls, h->hd_total_max,
-                 h->hd_sync / h->hd_calls, h->hd_sync_max, h->hd_sim / h->hd_calls);
-  if (Handle *h = H(handle); h && h->diag_host && h->hd_calls)
-    for (int i = 0; i < 7; ++i)
-      std::fprintf(stderr, "fmx host part %d: mean %.3f ms max %.3f\n", i, h->hd_seg[i] / h->hd_calls, h->hd_seg_max[i]);
   destroy(H(handle));
   return FMX_OK;
 }
@@ -1157,9 +1021,6 @@ static int reset_channels(Handle *h, int channel, int extra) {
     return FMX_E_INVALID;
   }
   const int c0 = (channel < 0) ? 0 : channel, c1 = (channel < 0) ? h->C : channel + 1;
-  tset_unspec(h->t_af);
-  tset_unspec(h->t_mono);
-  tset_unspec(h->t_rds);
   for (int c = c0; c < c1; ++c) {
     int m = RS_DECIM | RS_DEMOD | RS_STEREO | RS_AF | RS_RDS | extra;
     if (h->agc_ready[static_cast<size_t>(c)]) m |= RS_AGC;
@@ -1266,14 +1127,7 @@ int fmx_set_signal_params(void *handle, int channel, int applied_gain_db, double
 int fmx_process_block(void *handle, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *out) {
   Handle *h = H(handle);
   if (!h) return FMX_E_INVALID;
-  if (!h->diag_host) return process_block(h, d_iq, iq_stride, n, out);
-  const auto t0 = std::chrono::steady_clock::now();
-  const int rc = process_block(h, d_iq, iq_stride, n, out);
-  const double w = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  h->hd_total += w;
-  h->hd_total_max = std::max(h->hd_total_max, w);
-  h->hd_calls++;
-  return rc;
+  return process_block(h, d_iq, iq_stride, n, out);
 }
 
 int fmx_decimate(void *handle, const uint8_t *d_iq, size_t iq_stride, int n_out, float *d_out, int out_stride) {
@@ -1340,7 +1194,7 @@ static int demod_common(Handle *h, int mode, const void *d_in, size_t in_stride,
     if ((rc = launch_frontend_m(a, 1, 1, h->sA)) != FMX_OK) return rc;
   }
   if (d_mono) {
-    if ((rc = tset_advance(h, h->t_mono, n, buf, nullptr)) != FMX_OK) return rc;
+    if ((rc = tset_advance(h, h->t_mono, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
     AudioArgs a = audio_args(h, n, 2, &h->t_mono);
     a.in_l = mpx;
     a.in_stride = ms;
@@ -1382,7 +1236,7 @@ int fmx_downsample(void *handle, const float *d_mpx, int mpx_stride, int n, floa
   if ((rc = stage_begin(h, n)) != FMX_OK) return rc;
   if (n == 0) return FMX_OK;
   const int buf = static_cast<int>(h->step % FMX_NBUF);
-  if ((rc = tset_advance(h, h->t_mono, n, buf, nullptr)) != FMX_OK) return rc;
+  if ((rc = tset_advance(h, h->t_mono, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
   AudioArgs a = audio_args(h, n, 2, &h->t_mono);
   a.in_l = d_mpx;
   a.in_stride = mpx_stride;
@@ -1455,7 +1309,7 @@ int fmx_afpost(void *handle, const float *d_left, const float *d_right, int in_s
   std::vector<int> saved_map = h->t_af.chan_group;
   int mx = 0;
   const int buf = static_cast<int>(h->step % FMX_NBUF);
-  if ((rc = tset_advance(h, h->t_af, n, buf, &mx)) != FMX_OK) return rc;
+  if ((rc = tset_advance(h, h->t_af, n, buf, h->sA, &mx)) != FMX_OK) return rc;
   if (mx > cap) {
     h->t_af.groups = saved;
     h->t_af.chan_group = saved_map;
@@ -1490,7 +1344,7 @@ int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_gro
     return FMX_OK;
   }
   const int buf = static_cast<int>(h->step % FMX_NBUF);
-  if ((rc = tset_advance(h, h->t_rds, n, buf, nullptr)) != FMX_OK) return rc;
+  if ((rc = tset_advance(h, h->t_rds, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
   {
     FeArgs a = fe_args(h, n, FE_IN_MPX, buf);
     a.in_f = d_mpx;

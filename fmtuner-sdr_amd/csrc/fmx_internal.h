@@ -57,10 +57,9 @@ struct FeArgs {
   int *rds_count;    // [C]
   float *clip_out;   // [C]
   unsigned long long *sig_sums; // [C][6] RF-level byte sums (u8 inputs; k_audio evaluates them), may be null
-  unsigned long long *dbg;    // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
+  unsigned long long *dbg;    // [8] stage clocks (diagnostics build, FMX_STAMPS), may be null
   // stages
   int do_demod;      // run DC + IQ FIR + AGC + discriminator
-  int prio;          // k_fe8 waves' issue priority (s_setprio 0..3; FMX_FE_PRIO, A/B runs)
   // state
   uint8_t *dec_hist;
   int *dec_valid;

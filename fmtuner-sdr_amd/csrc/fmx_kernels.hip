@@ -37,9 +37,6 @@
 // reference's separate multiply and add (its dotprod order, rounded twice).
 // The RDS path is held to bit-exact groups, not to bit-exact floats (its
 // mix-down sine is already the hardware one).
-#ifndef FMX_RDS_FMA
-#define FMX_RDS_FMA 1
-#endif
 
 namespace fmx {
 
@@ -982,100 +979,64 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 }
 
 /* ================================================================== */
-/* k_pll: StereoDecoder per-sample recurrences, one lane per channel   */
+/* k_pll: StereoDecoder per-sample recurrences                         */
 /* ================================================================== */
-__device__ __forceinline__ float blend_target(float ratio, float coh, float errHz, int mode, bool fmono,
-                                              bool fstereo, bool detected, float gate) {
-  if (fmono) return 0.0f;
-  if (fstereo) return 1.0f;
-  // divisions by constants as d_div_const: bit-identical to x / c for every
-  // float 0 < |x| <= 2^60 or x = +0 for these divisors (all 2^32 words
-  // checked on the host; -0 comes out +0, which the clamps, fminf and the
-  // "0 + shaped" below absorb); these numerators are 0 or >= 1e-9 in size
-  constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cP = 320.0f - 180.0f; // > the fmaxf floors
-  const float ratioQ = d_clamp(d_div_const(ratio - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
-  const float cohQ = d_clamp(d_div_const(coh - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
-  const float pllQ = d_clamp(d_div_const(320.0f - errHz, cP, 1.0f / cP), 0.0f, 1.0f);
-  const float quality = fminf(ratioQ, fminf(cohQ, pllQ));
-  float shaped = quality * quality;
-  if (mode == 0) shaped = sqrtf(fmaxf(0.0f, quality));
-  else if (mode == 2) shaped = quality * quality * quality;
-  if (ratio < (0.022f * gate) || coh < (0.11f * gate) || errHz > (320.0f * 1.10f)) return 0.0f;
-  if (detected) return d_clamp(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
-  return 0.0f;
-}
-
-/* k_pll is an eight-wave software pipeline over tiles of PLL_T samples for
- * PLL_CH channels (lane = channel in the serial waves):
+/* k_pll is a seven-wave software pipeline over tiles of PLL_T samples for
+ * PLL_CH channels.  Serial waves hold one channel per lane; the P waves
+ * hold one item (row, t) of a tile per lane (rows 16 p .. 16 p + 15, t =
+ * lane % 4) and run two stages per iteration:
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
- *                 pll_step, step, sin(phase) straight from the phase word
- *                 (pll_sin_word); it hands the words on     stereo_decoder.cpp:251-256
- *   W4            (lane = (channel, t)) the reference's float phase of each
- *                 word with its sine and cosine (fmx_sincos_q) for the
- *                 outputs; shares W0's SIMD                 :251-253
- *   W2a..W2d      (lane = (channel, t)) everything parallel in time: the
- *                 blend target (sqrt, divisions) and the L-R matrix   :120-166,268-284
- *   W1 (serial)   what consumes the PLL without feeding it back: pilot/MPX
- *                 envelopes, pilot I/Q integrators (cos(phase)), PLL
- *                 frequency, cos(2 phase)                    stereo_decoder.cpp:246-250,257-266,275-279
- *   W3 (serial)   the blend recursion, the outputs, and the loads of later
- *                 input tiles                               :286-288
- * At iteration k, W0 runs tile k, W4 the phases of tile k-1, W1 tile k-2,
- * W2 tile k-3, W3 tile k-4; LDS slots rotate.  Apart from
- * the chain's sine (below) every value is computed with the reference's
- * arithmetic in the reference's order; only WHERE it runs moved. */
+ *                 pll_step, step; it hands the NCO words on       stereo_decoder.cpp:178-186
+ *   P phase       tile k-1: v_sin / v_cos of each word, the float phase of
+ *                 the word (the reference's phase()), the previous
+ *                 sample's values by DPP within the item quad (t = 0: the
+ *                 quad's t = 3 of the previous iteration); the pilot I/Q
+ *                 integrator inputs (pilot * vco) * kI, the PLL frequency
+ *                 (unwrap, clamp) and cos(2 phase)                  :176-199,219-221
+ *   W1 (serial)   the four linear recurrences (pilot / MPX envelopes, the
+ *                 pilot I/Q integrators) and |I, Q|^2; loads the MPX and
+ *                 delay-line tiles                                  :172-177,196-200
+ *   P target      tile k-3: blend target and the L/R matrix terms :120-166,201-225
+ *   W3 (serial)   the blend recursion, the outputs, and the loads of the
+ *                 pilot tiles (register-staged two iterations ahead) :227-234
+ * At iteration k: W0 tile k, P phase k-1, W1 k-2, P target k-3, W3 k-4.
+ * Waves w and w + 4 share a SIMD (tools/ubench/hwid.hip): SIMD 0 W0 + P2,
+ * SIMD 1 W1 + W3, SIMD 2 P0 + P3, SIMD 3 P1.  Every value except the
+ * chain's sine / NCO constrain and the outputs' sines (below) is computed
+ * with the reference's arithmetic in the reference's order; only WHERE it
+ * runs moved.
+ *
+ * Round 3 (from eight waves): the chain's NCO constrain is
+ * fract(err * beta/2pi) * 2^32 in f32 and its sine v_sin_f32 of the word in
+ * turns (tools/ubench/chainlat.hip: 147 -> 72 ticks per sample); the
+ * outputs' sine / cosine are v_sin / v_cos of the word (the reference takes
+ * cos / sin of the word's float phase: |difference| <= 5e-7); the
+ * per-sample frequency, cos(2 phase) and I/Q products moved off the serial
+ * W1, the old W4 (phases) and W2 (targets) became the four P waves. */
 #define PLL_CH 64
-#define PLL_TS PLL_T                       // 32-B rows (16-B aligned float4s; 2-way conflicts on row reads, 64 KB of LDS)
-#define PLL_WAVES 8
-// Waves w and w + 4 of a workgroup share a SIMD (measured,
-// tools/ubench/hwid.hip), and a SIMD retires about one wave64 VALU
-// instruction per 4 cycles whichever wave issues it.  Wave numbers:
-// 0 = W0, 1 = W1, 2/3/6/7 = W2a/W2b/W2c/W2d, 4 = W4, 5 = W3, so
-// SIMD 0: W0 (chain) + W4 (output phases); SIMD 1: W1 + W3;
-// SIMD 2: W2a + W2c; SIMD 3: W2b + W2d.  The blend-target items (the
-// longest per-tile work once stereo is detected) are spread over four
-// waves on two SIMDs, one item per lane per W2 wave.
+#define PLL_TS PLL_T
+#define PLL_WAVES 7
 #define PLL_W1 1
-#define PLL_IDLE 4
 #define PLL_W3 5
-#define PLL_NW2 4                          // W2 waves: 2, 3, 6, 7
 #define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
 #define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
+static_assert(PLL_T == 4, "the P waves' items are quads (DPP quad_perm)");
 
-// The chain's sine: pll_sin_word (fmx_math.h) straight from the phase word
-// (11 VALU), or with FMX_PLL_SIN_WORD=0 the reference's float phase and
-// fmx_sincos_q (the outputs' arithmetic) for A/B parity runs.
-#ifndef FMX_PLL_FAST_DIV
-#define FMX_PLL_FAST_DIV 1 // k_pll W2: blend-target sqrt / divisions on v_sqrt / v_rcp (~1 ulp); 0: IEEE (A/B)
-#endif
-#ifndef FMX_PLL_SIN_WORD
-#define FMX_PLL_SIN_WORD 1
-#endif
-__device__ __forceinline__ float pll_chain_sin(uint32_t theta, uint32_t *sg) {
-#if FMX_PLL_SIN_WORD
-  return pll_sin_word(theta, sg);
-#else
-  const float ph = d_nco_phase(theta);
-  const int qn = fmx_nco_quadrant(theta);
-  float s0, c0;
-  fmx_sincos_q_abs(ph, (float)qn, qn, &s0, &c0);
-  *sg = (qn & 2) ? 0x80000000u : 0u;
-  return s0;
-#endif
-}
 struct PllShared {
-  float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-2 in W1
+  float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-1 (P), k-2 (W1)
   float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k-1 loading, k-2 in W1)
-  uint32_t s0t[2][PLL_CH][PLL_TS];         // W0 -> W4: NCO phase words after each step
-  float s0[2][3][PLL_CH][PLL_TS];          // W4 -> W1: phase after the step, its sine and cosine
-  float s1[2][5][PLL_CH][PLL_TS];          // W1 -> W2: PBM, MM, MAG2, FREQ, COS2
-  float s2[2][4][PLL_CH][PLL_TS];          // W2 -> W3: TGT, MONO, DL, DR
-  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles for W2
+  uint32_t s0t[2][PLL_CH][PLL_TS];         // W0 -> P: NCO words after each step
+  float su[2][2][PLL_CH][PLL_TS];          // P -> W1: (pilot * vcoI) * kI, (pilot * vcoQ) * kI
+  float sf[3][2][PLL_CH][PLL_TS];          // P phase (k-1) -> P target (k-3): FREQ, COS2
+  float sr[2][3][PLL_CH][PLL_TS];          // W1 -> P target: PBM, MM, MAG2
+  float s2[2][4][PLL_CH][PLL_TS];          // P target -> W3: TGT, MONO, DL, DR
+  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles
   int s2_flags[PLL_CH];                    // bit0 fmono, bit1 fstereo, bit2 detected, bits 8.. blend mode
   float s2_gate[PLL_CH];
 };
-enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2, F_FREQ = 3, F_COS2 = 4 };  // W1 output
-enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };                 // W2 output
+enum { F_FREQ = 0, F_COS2 = 1 };                      // sf
+enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2 };             // sr
+enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };  // s2
 
 // One row-tile (PLL_CH rows x PLL_T samples from t0) of a [rows][stride]
 // array, staged through registers: issue() starts 16-B buffer loads (one
@@ -1159,7 +1120,24 @@ struct PllDlyStage {
   }
 };
 
-__global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
+// the value of the previous sample of this lane's item quad: lane t of a
+// quad reads lane t - 1; t = 0 reads the quad's t = 3 of the PREVIOUS
+// iteration (lanes with t = 3 offer `prev`, the others `cur`)
+__device__ __forceinline__ float quad_prev(float cur, float prev, bool t3) {
+  const float x = t3 ? prev : cur;
+  // quad_perm [3, 0, 1, 2]: lane 0 <- 3, lane 1 <- 0, lane 2 <- 1, lane 3 <- 2
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x93, 0xF, 0xF, false));
+}
+// sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
+// which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
+__device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) {
+  const float r = (float)(int32_t)theta * 2.3283064365386963e-10f;
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
+
+// <= 88 VGPRs: two k_pll waves (P0 + P3 on SIMD 2) beside two k_fe8 waves (168 each) in 512
+__global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))) void k_pll(PllArgs a) {
   if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
   else if (a.prio) __builtin_amdgcn_s_setprio(2);
   __shared__ PllShared shm;
@@ -1180,7 +1158,7 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     pw_wait += pw_last - t_;                                         \
   }
 #define PLL_STAMP_OUT()                                              \
-  if (a.dbg && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 6) { \
+  if (a.dbg && (threadIdx.x & 63) == 0) {                            \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6), pw_work);              \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6) + 1, pw_wait);          \
   }
@@ -1230,63 +1208,52 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
 
   const int c = c0 + lane;
   const bool act = c < a.C;
-  const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
   // block-end values gathered for W0, after the loop (aliases the pilot tiles)
   float(*fin)[PLL_CH] = reinterpret_cast<float(*)[PLL_CH]>(&sh->inp[0][0][0]);
   if (wave == 0) {
     // ---------------- W0: the PLL feedback chain ----------------
-    uint32_t theta = s0.theta, dtheta = s0.dtheta;
-    const float alpha = D->pll_alpha, beta = D->pll_beta;
-    uint32_t vsg; // sign bit of sin(phase) not yet applied to vcoQ
-    float vcoQ = pll_chain_sin(theta, &vsg);
+    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
+    uint32_t theta = s0.theta, dtheta = s0.dtheta, tprev = s0.theta;
+    // liquid pll_step: dtheta += constrain(e alpha), theta += constrain(e
+    // beta) (then step: theta += dtheta), constrain(x) = frac(x / 2 pi) 2^32
+    const float ka = D->pll_alpha * 0.159154943091895f, kb = D->pll_beta * 0.159154943091895f;
+    float vcoQ;
+    {
+      float cq;
+      word_sincos(theta, &vcoQ, &cq);
+    }
     // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
     // iteration k), so its LDS latency overlaps the chain of the current tile
-    float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
-#pragma unroll
-    for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = *reinterpret_cast<const float4 *>(&sh->inp[0][lane][4 * q]);
+    float4 pcur = *reinterpret_cast<const float4 *>(&sh->inp[0][lane][0]), pnxt = pcur;
     for (int k = 0; k < PLL_NIT(NT); ++k) {
-      if (k + 1 < NT) {
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q)
-          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lane][4 * q]);
-      }
-      // full tiles run without per-sample guards: the guards would sink the
-      // tile's LDS read into every sample (an LDS round trip on the chain)
+      if (k + 1 < NT) pnxt = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lane][0]);
+      // full tiles run without per-sample guards (a compile-time case)
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int ob = k & 1;
-        float pv[PLL_T];
+        const float pv[4] = {pcur.x, pcur.y, pcur.z, pcur.w};
+        uint32_t tw[4];
 #pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 x = pcur[q];
-          pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
-        }
-        uint32_t tw[PLL_T];
-#pragma unroll
-        for (int t = 0; t < PLL_T; ++t) {
+        for (int t = 0; t < 4; ++t) {
           if (FULL || t < cnt) {
-            // the sine's sign goes onto the pilot sample (off the chain)
-            const float err = __uint_as_float(__float_as_uint(pv[t]) ^ vsg) * vcoQ; // pv * sin(phase)
-            dtheta += d_nco_constrain(err * alpha);
-            theta += d_nco_constrain(err * beta);
-            theta += dtheta;
-            vcoQ = pll_chain_sin(theta, &vsg);
-            tw[t] = theta;
-          } else {
-            tw[t] = 0u;
+            const float err = pv[t] * vcoQ; // pilot * sin(phase)
+            const uint32_t ca = (uint32_t)(__builtin_amdgcn_fractf(err * ka) * 4294967296.0f);
+            const uint32_t cb = (uint32_t)(__builtin_amdgcn_fractf(err * kb) * 4294967296.0f);
+            const uint32_t T = theta + dtheta; // off the chain
+            tprev = theta;
+            dtheta += ca;
+            theta = T + (ca + cb);
+            vcoQ = __builtin_amdgcn_sinf((float)(int32_t)theta * 2.3283064365386963e-10f);
           }
+          tw[t] = theta;
         }
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q)
-          *reinterpret_cast<uint4 *>(&sh->s0t[ob][lane][4 * q]) = make_uint4(tw[4 * q], tw[4 * q + 1], tw[4 * q + 2], tw[4 * q + 3]);
+        *reinterpret_cast<uint4 *>(&sh->s0t[k & 1][lane][0]) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
       };
       if (k < NT) {
         const int cnt = min(PLL_T, n - k * PLL_T);
         if (cnt == PLL_T) tile(std::true_type{}, cnt);
         else tile(std::false_type{}, cnt);
       }
-#pragma unroll
-      for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = pnxt[q];
+      pcur = pnxt;
       PLL_SYNC()
     }
     PLL_SYNC() // W1 / W3 block-end values in sh->fin
@@ -1303,11 +1270,12 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     s.theta = theta;
     s.dtheta = dtheta;
     s.pll_phase = d_nco_phase(theta);
+    // m_pllFreq of the last sample: clamp(unwrap(phaseNext - phaseNow))
+    s.pll_freq = d_clamp(d_unwrap(s.pll_phase - d_nco_phase(tprev)), D->pll_min, D->pll_max);
     s.pilot_band_mag = fin[0][lane];
     s.mpx_mag = fin[1][lane];
     s.pilot_i = fin[2][lane];
     s.pilot_q = fin[3][lane];
-    s.pll_freq = fin[4][lane];
     s.blend = fin[5][lane];
     const float nominal = D->nominal;
     const FmxChanParam par = a.par[c];
@@ -1352,65 +1320,62 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // (main.cpp:1298-1300; k_pll runs only with processing.stereo)
     if (a.indicator_out) a.indicator_out[c] = (s.detected || (par.force_mono && s.level >= 20)) ? 1 : 0;
   } else if (wave == PLL_W1) {
-    // ---------------- W1: envelopes, pilot I/Q, frequency, cos 2phi ----------------
-    float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q, freq = s0.pll_freq;
-    const float pmin = D->pll_min, pmax = D->pll_max;
-    float phaseNow = d_nco_phase(s0.theta);
-    float vcoQ, vcoI;
-    fmx_sincos(phaseNow, &vcoQ, &vcoI);
-    for (int k = 0; k < PLL_NIT(NT); ++k) {
+    // ---------------- W1: envelopes and pilot I/Q integrators; MPX / delay loader ----------------
+    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
+    float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q;
+    // loads staged in registers across the barriers (as W3's pilot tiles):
+    // iteration k stores mpx tile k-1 (read here at k+1) and delay tile k-2
+    // (the P targets at k+1), then issues mpx k+1 and delay k
+    PllStage stm0, stm1;
+    PllDlyStage sd0, sd1;
+    auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
+    auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
+    const int rows_valid = min(PLL_CH, a.C - c0);
+    const __amdgpu_buffer_rsrc_t rm4 =
+        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, vec ? (uint32_t)((size_t)rows_valid * a.mpx_stride * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t rm =
+        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, (uint32_t)((size_t)rows_valid * a.mpx_stride * 4));
+    const __amdgpu_buffer_rsrc_t rh =
+        make_rsrc(a.st_hist_rd + (size_t)c0 * FMX_HIST, (uint32_t)((size_t)rows_valid * FMX_HIST * 4));
+    __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0): the state loads retired before the staged loads
+    stm0.issue(rm4, a.mpx_stride, 0, lane);
+    auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
+      constexpr int P = decltype(par_c)::value; // k & 1
+      PllStage &stm = P ? stm0 : stm1;          // mpx tile k-1, then k+1
+      PllDlyStage &std_ = P ? sd1 : sd0;        // delay tile k-2, then k
+      if (k - 1 >= 0 && k - 1 < NT) {
+        if (full(k - 1)) stm.store(sh->inm[(k - 1) & 1], lane);
+        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[(k - 1) & 1], c0, (k - 1) * PLL_T, tcnt(k - 1), lane);
+      }
+      if (k - 2 >= 0 && k - 2 < NT) std_.store(sh->dly[(k - 2) & 1], lane);
+      stm.issue(rm4, a.mpx_stride, (k + 1) * PLL_T, lane);
+      std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
       const int kt = k - 2;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int ib = kt % PLL_NINP, sb = kt & 1;
-        float pv[PLL_T], mv[PLL_T], ph[PLL_T], sq[PLL_T], cq[PLL_T];
+        const int sb = kt & 1;
+        const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[kt % PLL_NINP][lane][0]);
+        const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[sb][lane][0]);
+        const float4 ui = *reinterpret_cast<const float4 *>(&sh->su[sb][0][lane][0]);
+        const float4 uq = *reinterpret_cast<const float4 *>(&sh->su[sb][1][lane][0]);
+        const float pv[4] = {x.x, x.y, x.z, x.w}, mv[4] = {y.x, y.y, y.z, y.w};
+        const float uiv[4] = {ui.x, ui.y, ui.z, ui.w}, uqv[4] = {uq.x, uq.y, uq.z, uq.w};
+        float o_pbm[4], o_mm[4], o_mag2[4];
 #pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[ib][lane][4 * q]);
-          const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[kt & 1][lane][4 * q]);
-          const float4 z = *reinterpret_cast<const float4 *>(&sh->s0[sb][0][lane][4 * q]);
-          const float4 w = *reinterpret_cast<const float4 *>(&sh->s0[sb][1][lane][4 * q]);
-          const float4 u = *reinterpret_cast<const float4 *>(&sh->s0[sb][2][lane][4 * q]);
-          pv[4 * q] = x.x; pv[4 * q + 1] = x.y; pv[4 * q + 2] = x.z; pv[4 * q + 3] = x.w;
-          mv[4 * q] = y.x; mv[4 * q + 1] = y.y; mv[4 * q + 2] = y.z; mv[4 * q + 3] = y.w;
-          ph[4 * q] = z.x; ph[4 * q + 1] = z.y; ph[4 * q + 2] = z.z; ph[4 * q + 3] = z.w;
-          sq[4 * q] = w.x; sq[4 * q + 1] = w.y; sq[4 * q + 2] = w.z; sq[4 * q + 3] = w.w;
-          cq[4 * q] = u.x; cq[4 * q + 1] = u.y; cq[4 * q + 2] = u.z; cq[4 * q + 3] = u.w;
-        }
-        float o_pbm[PLL_T], o_mm[PLL_T], o_mag2[PLL_T], o_fr[PLL_T], o_c2[PLL_T];
-#pragma unroll
-        for (int t = 0; t < PLL_T; ++t) {
+        for (int t = 0; t < 4; ++t) {
           if (FULL || t < cnt) {
-            const float pilot = pv[t];
-            pbm = (pbm * kS) + (fabsf(pilot) * kI);
+            pbm = (pbm * kS) + (fabsf(pv[t]) * kI);
             mm = (mm * kS) + (fabsf(mv[t]) * kI);
-            const float phaseNext = ph[t];
-            const float dphi = d_unwrap(phaseNext - phaseNow);
-            freq = d_clamp(dphi, pmin, pmax);
-            pi_ = (pi_ * kS) + ((pilot * vcoI) * kI);
-            pq = (pq * kS) + ((pilot * vcoQ) * kI);
-            const float sN = sq[t], cN = cq[t]; // W4's sine / cosine of phaseNext
-            o_pbm[t] = pbm;
-            o_mm[t] = mm;
-            o_mag2[t] = (pi_ * pi_) + (pq * pq);
-            o_fr[t] = freq;
-            o_c2[t] = (cN * cN) - (sN * sN);
-            phaseNow = phaseNext;
-            vcoI = cN;
-            vcoQ = sN;
-          } else {
-            o_pbm[t] = o_mm[t] = o_mag2[t] = o_fr[t] = o_c2[t] = 0.0f;
+            pi_ = (pi_ * kS) + uiv[t];
+            pq = (pq * kS) + uqv[t];
           }
+          o_pbm[t] = pbm;
+          o_mm[t] = mm;
+          o_mag2[t] = (pi_ * pi_) + (pq * pq);
         }
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const int t = 4 * q;
-          *reinterpret_cast<float4 *>(&sh->s1[sb][F_PBM][lane][t]) = make_float4(o_pbm[t], o_pbm[t + 1], o_pbm[t + 2], o_pbm[t + 3]);
-          *reinterpret_cast<float4 *>(&sh->s1[sb][F_MM][lane][t]) = make_float4(o_mm[t], o_mm[t + 1], o_mm[t + 2], o_mm[t + 3]);
-          *reinterpret_cast<float4 *>(&sh->s1[sb][F_MAG2][lane][t]) = make_float4(o_mag2[t], o_mag2[t + 1], o_mag2[t + 2], o_mag2[t + 3]);
-          *reinterpret_cast<float4 *>(&sh->s1[sb][F_FREQ][lane][t]) = make_float4(o_fr[t], o_fr[t + 1], o_fr[t + 2], o_fr[t + 3]);
-          *reinterpret_cast<float4 *>(&sh->s1[sb][F_COS2][lane][t]) = make_float4(o_c2[t], o_c2[t + 1], o_c2[t + 2], o_c2[t + 3]);
-        }
+        *reinterpret_cast<float4 *>(&sh->sr[sb][F_PBM][lane][0]) = make_float4(o_pbm[0], o_pbm[1], o_pbm[2], o_pbm[3]);
+        *reinterpret_cast<float4 *>(&sh->sr[sb][F_MM][lane][0]) = make_float4(o_mm[0], o_mm[1], o_mm[2], o_mm[3]);
+        *reinterpret_cast<float4 *>(&sh->sr[sb][F_MAG2][lane][0]) = make_float4(o_mag2[0], o_mag2[1], o_mag2[2], o_mag2[3]);
       };
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
@@ -1418,39 +1383,28 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
         else tile(std::false_type{}, cnt);
       }
       PLL_SYNC()
+    };
+    for (int k = 0; k < PLL_NIT(NT); k += 2) {
+      iter(k, std::integral_constant<int, 0>{});
+      if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
     }
     fin[0][lane] = pbm;
     fin[1][lane] = mm;
     fin[2][lane] = pi_;
     fin[3][lane] = pq;
-    fin[4][lane] = freq;
     PLL_SYNC()
     PLL_STAMP_OUT()
   } else if (wave == PLL_W3) {
     // ---------------- W3: blend recursion + outputs; loader ----------------
+    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
     float blend = s0.blend;
     const int mode = sh->s2_flags[lane] >> 8;
     const float attack = D->blend_attack[mode], release = D->blend_release[mode];
-    // loads staged in registers TWO iterations ahead, across the barriers
-    // (one iteration, ~0.8 us, left W3 waiting on HBM latency at the
-    // stores): iteration k stores pilot tile k+2 (W0 reads it ahead at k+1),
-    // mpx tile k-1 and delay tile k-2 (W1 and W2 at iteration k+1), then
-    // issues pilot k+4, mpx k+1, delay k into the registers just stored.
-    // Two register sets by tile parity; the loop is unrolled by two so every
-    // set is static.
-    PllStage stp0, stp1, stm0, stm1;
-    PllDlyStage sd0, sd1;
-#ifdef FMX_STAMPS
-    unsigned long long w3acc[2] = {0, 0}, w3last = 0;
-#define W3_STAMP(i)                                              \
-  {                                                              \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
-    if (i == 0) { w3last = t_; w3acc[1] += t_ - pw_last; }       \
-    else w3acc[0] += t_ - w3last;                                \
-  }
-#else
-#define W3_STAMP(i)
-#endif
+    // pilot tiles staged in registers TWO iterations ahead, across the
+    // barriers: iteration k stores tile k+2 (W0 reads it ahead at k+1), then
+    // issues tile k+4 into the registers just stored.  Two register sets by
+    // tile parity; the loop is unrolled by two so every set is static.
+    PllStage stp0, stp1;
     auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
     auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
     const int rows_valid = min(PLL_CH, a.C - c0);
@@ -1460,64 +1414,44 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     // and are replaced by pll_load_sync at the store
     const __amdgpu_buffer_rsrc_t rp =
         make_rsrc(a.pilot + (size_t)c0 * a.pilot_stride, vec ? (uint32_t)((size_t)rows_valid * a.pilot_stride * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t rm4 =
-        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, vec ? (uint32_t)((size_t)rows_valid * a.mpx_stride * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t rm =
-        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, (uint32_t)((size_t)rows_valid * a.mpx_stride * 4));
-    const __amdgpu_buffer_rsrc_t rh =
-        make_rsrc(a.st_hist_rd + (size_t)c0 * FMX_HIST, (uint32_t)((size_t)rows_valid * FMX_HIST * 4));
     // retire every load made so far (blend, attack, release): otherwise the
     // waitcnt pass, merging states at the loop header, drains the staged
     // tile loads (vmcnt(0)) at their first use inside the loop
     __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
     stp0.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
     stp1.issue(rp, a.pilot_stride, 3 * PLL_T, lane);
-    stm0.issue(rm4, a.mpx_stride, 0, lane);
     auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
       constexpr int P = decltype(par_c)::value; // k & 1
       PllStage &stp = P ? stp1 : stp0;          // pilot tile k+2, then k+4
-      PllStage &stm = P ? stm0 : stm1;          // mpx tile k-1, then k+1
-      PllDlyStage &std_ = P ? sd1 : sd0;        // delay tile k-2, then k
       if (k + 2 < NT) {
         const int sl = (k + 2) % PLL_NINP;
         if (full(k + 2)) stp.store(sh->inp[sl], lane);
         else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[sl], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
       }
-      if (k - 1 >= 0 && k - 1 < NT) {
-        if (full(k - 1)) stm.store(sh->inm[(k - 1) & 1], lane);
-        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[(k - 1) & 1], c0, (k - 1) * PLL_T, tcnt(k - 1), lane);
-      }
-      if (k - 2 >= 0 && k - 2 < NT) std_.store(sh->dly[(k - 2) & 1], lane);
-      W3_STAMP(0)
       stp.issue(rp, a.pilot_stride, (k + 4) * PLL_T, lane);
-      stm.issue(rm4, a.mpx_stride, (k + 1) * PLL_T, lane);
-      std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
-      W3_STAMP(1)
       const int kt = k - 4;
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
         const int sb = kt & 1;
-        float ov[2][PLL_T];
+        const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lane][0]);
+        const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lane][0]);
+        const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lane][0]);
+        const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lane][0]);
+        const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
+        const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
+        float ov[2][4];
 #pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lane][4 * q]);
-          const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lane][4 * q]);
-          const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lane][4 * q]);
-          const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lane][4 * q]);
-          const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
-          const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int t = 4 * q + u;
-            if (FULL || t < cnt) {
-              const float tgt = tga[u];
-              const float ba = (tgt > blend) ? attack : release;
-              blend += (tgt - blend) * ba;
-              ov[0][t] = moa[u] + (dla[u] * blend);
-              ov[1][t] = moa[u] + (dra[u] * blend);
-            } else {
-              ov[0][t] = ov[1][t] = 0.0f;
-            }
+        for (int t = 0; t < 4; ++t) {
+          if (FULL || t < cnt) {
+            // blend += (tgt - blend) * (tgt > blend ? attack : release),
+            // select-free: exactly one of the two products is nonzero and
+            // adding the other (+0 / -0) leaves the sum unchanged
+            const float d = tga[t] - blend;
+            blend = (blend + fmaxf(d, 0.0f) * attack) + fminf(d, 0.0f) * release;
+            ov[0][t] = moa[t] + (dla[t] * blend);
+            ov[1][t] = moa[t] + (dra[t] * blend);
+          } else {
+            ov[0][t] = ov[1][t] = 0.0f;
           }
         }
         if (act) {
@@ -1527,12 +1461,9 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
                                        : (size_t)c * a.lr_stride + kt * PLL_T;
           float *ol = a.lraw + ob;
           float *orr = a.rraw + ob;
-          if (cnt == PLL_T && ((((uintptr_t)ol) | ((uintptr_t)orr)) & 15) == 0) {
-#pragma unroll
-            for (int q = 0; q < PLL_T / 4; ++q) {
-              reinterpret_cast<float4 *>(ol)[q] = make_float4(ov[0][4 * q], ov[0][4 * q + 1], ov[0][4 * q + 2], ov[0][4 * q + 3]);
-              reinterpret_cast<float4 *>(orr)[q] = make_float4(ov[1][4 * q], ov[1][4 * q + 1], ov[1][4 * q + 2], ov[1][4 * q + 3]);
-            }
+          if (FULL && ((((uintptr_t)ol) | ((uintptr_t)orr)) & 15) == 0) {
+            *reinterpret_cast<float4 *>(ol) = make_float4(ov[0][0], ov[0][1], ov[0][2], ov[0][3]);
+            *reinterpret_cast<float4 *>(orr) = make_float4(ov[1][0], ov[1][1], ov[1][2], ov[1][3]);
           } else {
 #pragma unroll
             for (int t = 0; t < PLL_T; ++t) {
@@ -1558,112 +1489,89 @@ __global__ __launch_bounds__(64 * PLL_WAVES) void k_pll(PllArgs a) {
     fin[5][lane] = blend;
     PLL_SYNC()
     PLL_STAMP_OUT()
-#ifdef FMX_STAMPS
-    if (a.dbg && lane == 0) {
-      atomicAdd(a.dbg + 12, w3acc[0]);
-      atomicAdd(a.dbg + 13, w3acc[1]);
-    }
-#endif
-#undef W3_STAMP
-  } else if (wave == PLL_IDLE) {
-    // ---------------- W4: phases for the outputs (shares W0's SIMD) ----------------
-    for (int k = 0; k < PLL_NIT(NT); ++k) {
-      // tile k-1 for W1 (iteration k+1): the reference's float phase of each
-      // word W0 produced and its sine / cosine (stereo_decoder.cpp:251-253)
-      const int kp = k - 1;
-      if (kp >= 0 && kp < NT) {
-        const int pb = kp & 1;
-#pragma unroll
-        for (int j = 0; j < PLL_CH * PLL_T / 64; ++j) {
-          const int idx = lane + 64 * j;
-          const int row = idx / PLL_T, t = idx % PLL_T;
-          const uint32_t th = sh->s0t[pb][row][t];
-          const float ph = d_nco_phase(th);
-          const int qn = fmx_nco_quadrant(th);
-          float sN, cN;
-          fmx_sincos_q(ph, (float)qn, qn, &sN, &cN);
-          sh->s0[pb][0][row][t] = ph;
-          sh->s0[pb][1][row][t] = sN;
-          sh->s0[pb][2][row][t] = cN;
-        }
-      }
-      PLL_SYNC()
-    }
-    PLL_SYNC()
-    PLL_STAMP_OUT()
   } else {
-    // ---------------- W2a..W2d: time-parallel work ----------------
-    const int g2 = (wave == 2) ? 0 : (wave == 3) ? 1 : (wave == 6) ? 2 : 3; // W2a, W2b, W2c, W2d
-    const float nominal = D->nominal;
-    const float fsf = (float)D->fs;
+    // ---------------- P0..P3: the time-parallel stages ----------------
+    const int pw = (wave == 2) ? 0 : (wave == 3) ? 1 : (wave == 4) ? 2 : 3;
+    const int row = (lane >> 2) + 16 * pw, tt = lane & 3;
+    const bool t3 = tt == 3;
+    const int ch = c0 + row;
+    const float nominal = D->nominal, fsf = (float)D->fs;
+    const float pmin = D->pll_min, pmax = D->pll_max;
+    const int fl0 = sh->s2_flags[row];
+    const float gate = sh->s2_gate[row];
+    const int mode = fl0 >> 8;
+    // previous-iteration values of this lane's item (t = 3 offers them to
+    // the quad's t = 0): the state's phase word before the first tile
+    float prev_s, prev_c, prev_ph;
+    {
+      const uint32_t th0 = (ch < a.C) ? a.st[ch].theta : 0u;
+      word_sincos(th0, &prev_s, &prev_c);
+      prev_ph = d_nco_phase(th0);
+    }
     for (int k = 0; k < PLL_NIT(NT); ++k) {
-      const int kt = k - 3;
-      if (kt >= 0 && kt < NT) {
-        const int cnt = min(PLL_T, n - kt * PLL_T);
-        const int sb = kt & 1;
-        // both items of a lane side by side and branch-free (the flag cases
-        // as selects), so their long dependent chains (IEEE sqrt, two IEEE
-        // divisions) interleave; blend_target's arithmetic is unchanged
-        constexpr int NJ = PLL_CH * PLL_T / (64 * PLL_NW2);
-        float tg[NJ], q[NJ];
-        int fl[NJ], row[NJ], tt[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int idx = lane + 64 * (g2 + PLL_NW2 * j);
-          row[j] = idx / PLL_T;
-          tt[j] = idx % PLL_T;
-          fl[j] = sh->s2_flags[row[j]];
-          const float pbm = sh->s1[sb][F_PBM][row[j]][tt[j]];
-          const float mm = sh->s1[sb][F_MM][row[j]][tt[j]];
-          const float mag2 = sh->s1[sb][F_MAG2][row[j]][tt[j]];
-          const float pf = sh->s1[sb][F_FREQ][row[j]][tt[j]];
-          const float gate = sh->s2_gate[row[j]];
-#if FMX_PLL_FAST_DIV
-          // hardware sqrt / reciprocal (~1 ulp) instead of the IEEE sequences
-          const float magNow = __builtin_amdgcn_sqrtf(mag2);
-          const float ratioNow = pbm * __builtin_amdgcn_rcpf(fmaxf(mm, 1e-3f));
-          const float cohNow = magNow * __builtin_amdgcn_rcpf(fmaxf(pbm, 1e-4f));
-#else
-          const float magNow = sqrtf(mag2);
-          const float ratioNow = pbm / fmaxf(mm, 1e-3f);
-          const float cohNow = magNow / fmaxf(pbm, 1e-4f);
-#endif
-          const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
-          // blend_target(ratioNow, cohNow, errHzNow, mode, false, false, true, gate)
-          constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cP = 320.0f - 180.0f;
-          const float ratioQ = d_clamp(d_div_const(ratioNow - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
-          const float cohQ = d_clamp(d_div_const(cohNow - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
-          const float pllQ = d_clamp(d_div_const(320.0f - errHzNow, cP, 1.0f / cP), 0.0f, 1.0f);
-          q[j] = fminf(ratioQ, fminf(cohQ, pllQ));
-          const bool gated = ratioNow < (0.022f * gate) || cohNow < (0.11f * gate) || errHzNow > (320.0f * 1.10f);
-          const int mode = fl[j] >> 8;
-          const float sq2 = q[j] * q[j];
-          const float shaped = (mode == 2) ? sq2 * q[j] : sq2; // mode 0 below
-          tg[j] = gated ? 0.0f : d_clamp(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
-          fl[j] |= gated ? 16 : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) { // mode 0 (soft): sqrt shaping, lanes of soft-blend channels only
-          if ((fl[j] >> 8) == 0 && !(fl[j] & 16)) tg[j] = d_clamp(0.0f + ((1.0f - 0.0f) * sqrtf(fmaxf(0.0f, q[j]))), 0.0f, 1.0f);
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int f = fl[j];
-          // force mono -> 0, force stereo -> 1, not detected -> 0 (blend_target's paths)
-          const float tgt = (f & 1) ? 0.0f : ((f & 2) ? 1.0f : ((f & 4) ? tg[j] : 0.0f));
-          const float delayed = sh->dly[sb][row[j]][tt[j]];
-          const float cos2 = sh->s1[sb][F_COS2][row[j]][tt[j]];
-          const float monoNorm = delayed * 0.5f;
-          const float lr = 2.0f * delayed * cos2;
-          const float sl = (delayed + lr) * 0.5f;
-          const float sr = (delayed - lr) * 0.5f;
-          if (tt[j] < cnt) {
-            sh->s2[sb][F_TGT][row[j]][tt[j]] = tgt;
-            sh->s2[sb][F_MONO][row[j]][tt[j]] = monoNorm;
-            sh->s2[sb][F_DL][row[j]][tt[j]] = sl - monoNorm;
-            sh->s2[sb][F_DR][row[j]][tt[j]] = sr - monoNorm;
-          }
-        }
+      // both stages every iteration in one basic block (their LDS reads and
+      // dependent chains overlap); tiles outside the block compute on stale
+      // rows and store nothing
+      const int kp = k - 1, kt = k - 3; // phase stage tile, target stage tile
+      const bool dop = kp >= 0 && kp < NT;
+      const bool dot = kt >= 0 && kt < NT && tt < min(PLL_T, n - kt * PLL_T);
+      const int kpc = max(kp, 0), ktc = max(kt, 0);
+      const int sb = ktc & 1, sf3 = ktc % 3;
+      const uint32_t th = sh->s0t[kpc & 1][row][tt];
+      const float pilot = sh->inp[kpc % PLL_NINP][row][tt];
+      const float pbm = sh->sr[sb][F_PBM][row][tt];
+      const float mm = sh->sr[sb][F_MM][row][tt];
+      const float mag2 = sh->sr[sb][F_MAG2][row][tt];
+      const float pf = sh->sf[sf3][F_FREQ][row][tt];
+      const float cos2 = sh->sf[sf3][F_COS2][row][tt];
+      const float delayed = sh->dly[sb][row][tt];
+      // ---- phase stage (tile k-1) ----
+      float sN, cN;
+      word_sincos(th, &sN, &cN);
+      const float ph = d_nco_phase(th);
+      // vco of this sample = sin / cos of the previous sample's phase
+      const float sP = quad_prev(sN, prev_s, t3), cP = quad_prev(cN, prev_c, t3), phP = quad_prev(ph, prev_ph, t3);
+      const float uI = (pilot * cP) * kI, uQ = (pilot * sP) * kI;
+      const float fr = __builtin_amdgcn_fmed3f(d_unwrap(ph - phP), pmin, pmax); // clamp(dphi, min, max)
+      const float c2 = (cN * cN) - (sN * sN);
+      // ---- target stage (tile k-3): blend target (stereo_decoder.cpp:120-166)
+      // with hardware sqrt / reciprocal (~1 ulp) for the three quality ratios;
+      // divisions by constants as d_div_const (bit-identical to x / c for these
+      // divisors, all 2^32 words checked on the host); clamps as v_med3
+      const float magNow = __builtin_amdgcn_sqrtf(mag2);
+      const float ratioNow = pbm * __builtin_amdgcn_rcpf(fmaxf(mm, 1e-3f));
+      const float cohNow = magNow * __builtin_amdgcn_rcpf(fmaxf(pbm, 1e-4f));
+      const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
+      constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cPl = 320.0f - 180.0f;
+      const float ratioQ = __builtin_amdgcn_fmed3f(d_div_const(ratioNow - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
+      const float cohQ = __builtin_amdgcn_fmed3f(d_div_const(cohNow - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
+      const float pllQ = __builtin_amdgcn_fmed3f(d_div_const(320.0f - errHzNow, cPl, 1.0f / cPl), 0.0f, 1.0f);
+      const float q = fminf(ratioQ, fminf(cohQ, pllQ));
+      const bool gated = ratioNow < (0.022f * gate) || cohNow < (0.11f * gate) || errHzNow > (320.0f * 1.10f);
+      float shaped = q * q;
+      if (mode == 0) shaped = sqrtf(fmaxf(0.0f, q));
+      else if (mode == 2) shaped = shaped * q;
+      const float tg = gated ? 0.0f : __builtin_amdgcn_fmed3f(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
+      // force mono -> 0, force stereo -> 1, not detected -> 0 (computeBlendTarget's paths)
+      const float tgt = (fl0 & 1) ? 0.0f : ((fl0 & 2) ? 1.0f : ((fl0 & 4) ? tg : 0.0f));
+      const float monoNorm = delayed * 0.5f;
+      const float lr = 2.0f * delayed * cos2;
+      const float sl = (delayed + lr) * 0.5f;
+      const float sr = (delayed - lr) * 0.5f;
+      if (dop) {
+        prev_s = sN;
+        prev_c = cN;
+        prev_ph = ph;
+        sh->su[kp & 1][0][row][tt] = uI;
+        sh->su[kp & 1][1][row][tt] = uQ;
+        sh->sf[kp % 3][F_FREQ][row][tt] = fr;
+        sh->sf[kp % 3][F_COS2][row][tt] = c2;
+      }
+      if (dot) {
+        sh->s2[sb][F_TGT][row][tt] = tgt;
+        sh->s2[sb][F_MONO][row][tt] = monoNorm;
+        sh->s2[sb][F_DL][row][tt] = sl - monoNorm;
+        sh->s2[sb][F_DR][row][tt] = sr - monoNorm;
       }
       PLL_SYNC()
     }
@@ -2098,37 +2006,30 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
          ((uint32_t)bs_block_number(ooff) + d / 26) % 4 == (uint32_t)bs_block_number(off);
 }
 
-// k_rds input: a ring of RDS_RING samples x 64 channels in LDS, sample-major
-// (tin[s][lane]), filled by LDS-DMA one dword per lane per instruction: lane
-// l's buffer load from its own channel row lands at LDS dword l of the
-// instruction's row, so a tile of RDS_TILE samples is RDS_TILE instructions
-// and every read of one sample by the wave is 64 consecutive dwords
-// (conflict-free ds_read_b32).
-#ifndef FMX_HWSIN_RDS
-#define FMX_HWSIN_RDS 1
-#endif
-// FMX_RDS_DIRECT_PHASE (default 1): the mix-down phase of sample k is the
-// NCO word's own phase, v_sin / v_cos of theta / 2^32 turns.  The reference
-// mixes with the quad-phase wrapper's accumulator phases_[0] (liquid_wrappers
-// .cpp:121-139), which sums unwrap(phase_now - prev) * 57000 / 57000 over the
-// NCO's steps (PLL jumps included): it is the NCO phase mod 2 pi up to float
-// rounding (a random walk of ~1e-7 rad per step, also through resets, which
-// keep phases_ and prev).  Dropping that sum removes ~15 dependent VALU per
-// sample from the issue-bound k_rds wave; RDS groups stay bit-exact against
-// the oracle (which keeps the reference's sum).  0: the reference's sum.
-#ifndef FMX_RDS_DIRECT_PHASE
-#define FMX_RDS_DIRECT_PHASE 1
-#endif
-#define RDS_TILE 8  // samples per LDS-DMA tile
-#define RDS_RING 32 // ring of 4 tiles: up to 3 in flight ahead of the one being read
-#ifndef RDS_U
-#define RDS_U 8 // samples per chunk (divides 24)
-#endif
-#define RDS_SYMQ 12 // symbols queued per lane before the bit decoders run (~40 per 4096-sample block)
-// Per-lane state lives in LDS (odd dword stride: conflict-free across lanes);
-// only the per-sample quantities (NCO, FIR partial sums, AGC, symsync
-// scalars) are held in registers.  Block sync / biphase state is touched once
-// per symbol.
+// k_rds (round 3): RDS_LPC lanes per channel, RDS_CPW channels per
+// workgroup (one wave).  The 255-tap low-pass runs as streaming partial sums
+// (acc[i]: the i-th next decimation instant) kept PER LANE: the lanes of a
+// channel take the samples of a decimation period in turn (period position
+// j = lane + 8 q, q = 0..2), each with its own three tap columns, so the
+// mix-down and the FIR products of a period run in parallel; the channel's
+// output is the sum of its lanes' acc[0] (three DPP butterfly adds, bit-
+// identical in every lane).  The NCO word of every sample is exact uint32
+// arithmetic (theta_period_start + j * dtheta): between decimation instants
+// the reference's NCO only steps (stepPLL runs at symbol instants,
+// subcarrier.cpp:195-216).  AGC, symsync and the PSK2 PLL (the serial part,
+// once per 24 samples) run redundantly in the channel's lanes; the bit
+// decoders (biphase, delta, block sync) in its first lane.
+// The mix-down phase of sample k is the NCO word's own phase, v_sin / v_cos
+// of theta / 2^32 turns.  The reference mixes with the quad-phase wrapper's
+// accumulator phases_[0] (liquid_wrappers.cpp:121-139), which sums
+// unwrap(phase_now - prev) * 57000 / 57000 over the NCO's steps (PLL jumps
+// included): it is the NCO phase mod 2 pi up to float rounding (a random walk
+// of ~1e-7 rad per step); RDS groups stay bit-exact against the oracle
+// (which keeps the reference's sum).
+#define RDS_LPC 8                  // lanes per channel
+#define RDS_CPW (64 / RDS_LPC)     // channels per wave / workgroup
+#define RDS_SYMQ 12                // symbols queued per channel before the bit decoders run
+static_assert(FMX_RDS_DECIM == 3 * RDS_LPC, "three samples per lane and decimation period");
 // The bit-decoder state of FmxRdsState (biphase, delta, block sync) -- the
 // only state k_rds keeps in LDS; the per-sample state lives in registers.
 struct RdsBits {
@@ -2199,36 +2100,17 @@ __device__ __forceinline__ void rds_bits_store(FmxRdsState &g, const RdsBits &b)
   }
   g.bs_bits_since_lost = b.bs_bits_since_lost;
 }
-// The 8 chunk taps of one accumulator (two 16-B broadcast LDS reads).  The
-// __restrict__ parameter gives the inlined loads alias-scope metadata, which
-// lets the wait-count pass see they cannot alias the input ring's LDS-DMA
-// writes in flight (without it every chunk waited vmcnt(0) for them).
-__device__ __forceinline__ void rds_taps8(const float *__restrict__ p, float (&t)[8]) {
-  const float4 a = *reinterpret_cast<const float4 *>(p);
-  const float4 b = *reinterpret_cast<const float4 *>(p + 4);
-  t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w;
-  t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
-}
-// One FIR product into a partial sum: FMX_RDS_FMA (fmx_kernels.hip top).
-__device__ __forceinline__ f32x2 rds_mac(float h, f32x2 m, f32x2 acc) {
-#if FMX_RDS_FMA
-  return __builtin_elementwise_fma(f32x2{h, h}, m, acc);
-#else
-  const f32x2 p = f32x2{h, h} * m;
-  return acc + p;
-#endif
-}
 struct RdsLds {
-  // chunk taps by accumulator: tT[p][i][u] = h[J - u + 24 i] for the chunk
-  // starting at period phase j0 = 1 + 8p (J = 24 - j0), zero past tap 254
-  float tT[3][FMX_RDS_NACC][8] __attribute__((aligned(16)));
+  // tap columns: hq[j0][i][q] = h[23 - (j0 + 8 q) + 24 i] (zeros past tap 254),
+  // q padded to 4 (one 16-B read per accumulator)
+  float hq[RDS_LPC][FMX_RDS_NACC][4] __attribute__((aligned(16)));
   float mf[FMX_NPFB * FMX_SS_SUB];
   float dmf[FMX_NPFB * FMX_SS_SUB];
   uint32_t esyn[5][52];
   uint32_t eerr[5][52];
-  f32x2 win[FMX_SS_SUB][64];     // symsync window ring per lane, newest at wp
-  float symq[RDS_SYMQ][64];      // symbols (real part) awaiting biphase / block sync
-  RdsCold cold[64];
+  f32x2 win[FMX_SS_SUB][RDS_CPW];  // symsync window ring per channel, newest at wp
+  float symq[RDS_SYMQ][RDS_CPW];   // symbols (real part) awaiting biphase / block sync
+  RdsCold cold[RDS_CPW];
 };
 
 __device__ __forceinline__ void rds_emit_group(RdsBits &s, const RdsArgs &a, int c, int &ng) {
@@ -2342,69 +2224,58 @@ __device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &
   s.bs_until_next = s.bs_in_sync ? 26u : 1u;
 }
 
-/* k_rds: one lane per channel, 64 channels per workgroup (one wave).  The
- * per-sample chain of SubcarrierSet::processSample (subcarrier.cpp:153-235,
- * liquid_wrappers.cpp:125-139,271-353) in the reference's order:
- *   mix x * polar(1, -phase0)            (fmx_sincos)
- *   255-tap FIR push: 11 streaming partial sums acc[i] (the i-th next
- *   decimation instant), accumulated oldest -> newest exactly as the
- *   window dot product, with packed (re, im) multiplies and adds
- *   every 24th sample: FIR output -> AGC -> symsync (MF / dMF in an LDS ring)
- *   -> PSK2 phase error -> NCO PLL -> biphase -> delta -> block sync
- *   NCO step + quad-phase wrapper.
- * When every lane of the wave shares the decimation phase (all channels in
- * step, the normal case) the samples run in chunks of 8 (three per FIR
- * period): the 7 NCO phases with no PLL update in between are evaluated
- * independently, only their wrapped sum is serial, then 8 sincos and the
- * partial sums with wave-uniform (LDS broadcast) tap rows. */
-// s_waitcnt as a builtin plus a compiler-only memory barrier: no inline asm
-// in k_rds, so the backend can prove it uses no AGPRs and does not reserve
-// the whole register file for them (inline asm there made every k_rds wave
-// allocate 257 registers, leaving no room for two k_fe8 waves on its SIMD)
-#define rds_wait(imm)                    \
-  do {                                    \
-    __atomic_signal_fence(__ATOMIC_SEQ_CST); \
-    __builtin_amdgcn_s_waitcnt(imm);      \
-    __atomic_signal_fence(__ATOMIC_SEQ_CST); \
-  } while (0)
+
+// the sum of a value over the 8 lanes of a channel group (DPP butterfly:
+// quad_perm xor 1, xor 2, then row_half_mirror): every lane of the group
+// gets the same bits (each step adds two identical pairs in swapped order)
+__device__ __forceinline__ float rds_sum8(float x) {
+  auto dpp = [](float v, auto ctrl_c) __attribute__((always_inline)) {
+    constexpr int ctrl = decltype(ctrl_c)::value;
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false));
+  };
+  x = x + dpp(x, std::integral_constant<int, 0xB1>{});  // quad_perm [1, 0, 3, 2]
+  x = x + dpp(x, std::integral_constant<int, 0x4E>{});  // quad_perm [2, 3, 0, 1]
+  x = x + dpp(x, std::integral_constant<int, 0x141>{}); // row_half_mirror
+  return x;
+}
+
 __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
   else if (a.prio) __builtin_amdgcn_s_setprio(2);
   // dynamic LDS (sizeof(RdsLds) at launch): with a static size the backend
   // sees an LDS-limited occupancy and pads every wave's register allocation
-  // up to it (257 VGPRs), which keeps k_rds off SIMDs running k_fe8
+  // up to it
   extern __shared__ __align__(16) unsigned char rds_smem[];
   RdsLds &L = *reinterpret_cast<RdsLds *>(rds_smem);
-  // the LDS-DMA input ring (sample t of lane l at tin[t % RDS_RING][l]) is a
-  // separate (static, 8 KB) object: reads of the tables in L then provably
-  // do not alias the DMA writes in flight and need no vmcnt wait
-  __shared__ __align__(16) float tin[RDS_RING][64];
 #ifdef FMX_STAMPS
+  // stage clocks (diagnostics build): 0 setup, 1 mix + FIR products, 2 FIR
+  // output -> AGC -> symsync -> PLL, 3 bit decoders, 4 state store
   unsigned long long rs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long rs_last = __builtin_amdgcn_s_memtime();
-#define RDS_STAMP(k)                                      \
-  if (a.dbg) {                                            \
+#define RDS_STAMP(k)                                            \
+  if (a.dbg) {                                                  \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    rs_acc[k] += t_ - rs_last;                            \
-    rs_last = t_;                                         \
+    rs_acc[k] += t_ - rs_last;                                  \
+    rs_last = t_;                                               \
   }
 #else
 #define RDS_STAMP(k)
 #endif
   const int lane = threadIdx.x;
-  const int c0 = blockIdx.x * 64;
-  const int c = c0 + lane;
+  const int g = lane / RDS_LPC, j0 = lane % RDS_LPC; // channel slot, first period position
+  const int c0 = blockIdx.x * RDS_CPW;
+  const int c = c0 + g;
   const bool act = c < a.C;
+  const bool lead = j0 == 0;
   const FmxDesign *__restrict__ D = a.des;
   // ---- LDS tables ----
-  for (int idx = lane; idx < 3 * FMX_RDS_NACC * 8; idx += 64) {
-    const int p = idx / (FMX_RDS_NACC * 8), i = (idx / 8) % FMX_RDS_NACC, u = idx % 8;
-    const int k = (FMX_RDS_DECIM - 1 - 8 * p) - u + FMX_RDS_DECIM * i;
-    L.tT[p][i][u] = (k < FMX_RDS_FIR) ? D->rds_fir[k] : 0.0f;
-  }
   for (int idx = lane; idx < FMX_NPFB * FMX_SS_SUB; idx += 64) {
     L.mf[idx] = D->ss_mf[idx];
     L.dmf[idx] = D->ss_dmf[idx];
+  }
+  for (int idx = lane; idx < RDS_LPC * FMX_RDS_NACC * 4; idx += 64) {
+    const int jj = idx / (FMX_RDS_NACC * 4), i = (idx / 4) % FMX_RDS_NACC, q = idx % 4;
+    L.hq[jj][i][q] = (q < 3) ? D->rds_fir[FMX_RDS_DECIM - 1 - (jj + 8 * q) + FMX_RDS_DECIM * i] : 0.0f;
   }
   if (lane < 5) {
     const uint32_t words[5] = {0x0FC, 0x198, 0x168, 0x350, 0x1B4};
@@ -2417,25 +2288,19 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
         idx++;
       }
   }
-  RdsBits &S = L.cold[lane].s;
+  RdsBits &S = L.cold[g].s;
   const FmxRdsState G = act ? a.st[c] : FmxRdsState{}; // the compiler loads only the fields used
   const int count = act ? a.in_count[c] : 0;
-  rds_bits_load(S, G);
+  if (lead) rds_bits_load(S, G);
   float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
   // ---- hot state -> registers ----
-  uint32_t theta = G.theta, dtheta = G.dtheta, ssr = G.sample_since_reset;
-  float prev_f0 = G.prev_f0, phase0 = G.phase0;
+  uint32_t theta = G.theta, dtheta = G.dtheta;
+  const uint32_t ssr0 = G.sample_since_reset;
+  // this lane's share of the streaming partial sums (the channel's sums in
+  // its first lane at entry)
   f32x2 acc[FMX_RDS_NACC];
-  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{G.acc_re[i], G.acc_im[i]};
-  float agc_g = G.agc_g, agc_y2p = G.agc_y2p;
-  float ss_rate = G.ss_rate, ss_del = G.ss_del, ss_tau = G.ss_tau, ss_q_hat = G.ss_q_hat, ss_v1 = G.ss_v1;
-  int ss_b = G.ss_b, ss_decim = G.ss_decim, ss_valid = G.ss_mf_valid;
-  for (int m = 0; m < FMX_SS_SUB; ++m) {
-    const f32x2 w = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
-    L.win[m][lane] = w;
-  }
-  int wp = FMX_SS_SUB - 1; // newest window sample at wp (and wp + 18)
-  if (act && G.rebuild) {
+  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = lead ? f32x2{G.acc_re[i], G.acc_im[i]} : f32x2{0.0f, 0.0f};
+  if (act && lead && G.rebuild) {
     // decimation phase changed by a reset: rebuild the partial sums from the
     // last mixed samples (the reference's FIR window survives the reset)
     for (int i = 0; i < FMX_RDS_NACC; ++i) {
@@ -2451,6 +2316,12 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       acc[i] = f32x2{ar, ai};
     }
   }
+  float agc_g = G.agc_g, agc_y2p = G.agc_y2p;
+  float ss_rate = G.ss_rate, ss_del = G.ss_del, ss_tau = G.ss_tau, ss_q_hat = G.ss_q_hat, ss_v1 = G.ss_v1;
+  int ss_b = G.ss_b, ss_decim = G.ss_decim, ss_valid = G.ss_mf_valid;
+  if (lead)
+    for (int m = 0; m < FMX_SS_SUB; ++m) L.win[m][g] = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
+  int wp = FMX_SS_SUB - 1; // newest window sample at wp
   int ng = 0;
   const f32x2 fscale2 = f32x2{D->rds_fir_scale, D->rds_fir_scale};
   const float agc_bw = D->agc_bw;
@@ -2459,361 +2330,219 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   const float alpha = D->rds_alpha, beta = D->rds_beta;
   const float dphi_psk = (float)(3.14159265358979323846 * (1.0 - 1.0 / 2));
   const uint32_t ring0 = G.ring_pos;
-  int nmax = count, cmin = act ? count : 0x7fffffff;
-  for (int d = 32; d >= 1; d >>= 1) {
-    nmax = max(nmax, __shfl_xor(nmax, d));
-    cmin = min(cmin, __shfl_xor(cmin, d));
-  }
-  const int ring_from = cmin - FMX_RDS_RING;
+  // Rounds: round r of a channel ends on its r-th decimation instant of the
+  // call (sample o0 + 24 r, sample_since_reset % 24 == 0 there,
+  // subcarrier.cpp:186); round 0 holds samples 0..o0, the last round may end
+  // before its instant (the tail, carried in acc).  Sample t of round r sits
+  // at period position j = t - base_r.
+  const int o0 = (int)((FMX_RDS_DECIM - ssr0 % FMX_RDS_DECIM) % FMX_RDS_DECIM);
+  const int R = (count <= 0) ? 0 : (o0 >= count ? 1 : 1 + (count - o0 - 1 + FMX_RDS_DECIM - 1) / FMX_RDS_DECIM);
+  int rmax = R;
+  for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, __shfl_xor(rmax, d));
+  // the NCO word at period position 0 of round 0 (virtual for o0 < 23)
+  uint32_t thp = theta - (uint32_t)(FMX_RDS_DECIM - 1 - o0) * dtheta;
   int nq = 0;
   float last_symi = 0.0f;
-
-  // one mixed sample into the 11 streaming partial sums (reference order)
-  // the last FMX_RDS_RING mixed samples of the call are kept (decimation-
-  // phase rebuild after a reset)
-  auto ring_store = [&](f32x2 m, int t) __attribute__((always_inline)) {
-    if (t >= ring_from) { // wave-uniform test first
-      if (t >= count - FMX_RDS_RING) {
-        const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
-        *reinterpret_cast<f32x2 *>(ring + 2 * idx) = m;
-      }
-    }
+  // input: the channel rows of this workgroup, sample t of lane's channel at
+  // ((g * stride) + t) * 4; samples outside [0, count) read 0 (out of range)
+  const int rows_valid = min(RDS_CPW, a.C - c0);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + (size_t)c0 * a.in_stride,
+                                               (uint32_t)((size_t)max(rows_valid, 0) * a.in_stride * sizeof(float)));
+  auto in_off = [&](int r, int q) __attribute__((always_inline)) {
+    const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
+    const int t = base + j0 + 8 * q;
+    return (act && r < R && t >= 0 && t < count) ? (uint32_t)((g * a.in_stride + t) * 4) : 0x80000000u;
   };
-  // tp: the sample's tap row (D->rds_rows[jp]); through the constant address
-  // space (SGPR operands) when jp is wave-uniform, a per-lane global row otherwise
-  auto acc_add = [&](f32x2 m, int t, auto tp) __attribute__((always_inline)) {
-    float h[FMX_RDS_NACC];
+  // the round's three input samples, loaded RDS_PF rounds ahead (a round
+  // is ~0.3 us; the input comes from the Infinity Cache or HBM)
+  constexpr int RDS_PF = 4;
+  float xr[RDS_PF + 1][3];
 #pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC; ++i) h[i] = tp[i];
+  for (int p = 0; p < RDS_PF; ++p)
 #pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = rds_mac(h[i], m, acc[i]);
-    ring_store(m, t);
-  };
-#if !FMX_RDS_DIRECT_PHASE
-  auto mix = [&](float x, float ph) __attribute__((always_inline)) {
-    float sn, cs;
-#if FMX_HWSIN_RDS
-    // polar(1, -ph) from v_sin_f32 / v_cos_f32 on ph / 2pi (|err| <= 4e-7):
-    // 3 VALU (two quarter-rate) instead of fmx_sincos's ~28 on this
-    // issue-bound wave; the mix-down feeds only the 2.4 kHz symbol path
-    const float r = ph * 0.15915494309189535f;
-    sn = -__builtin_amdgcn_sinf(r);
-    cs = __builtin_amdgcn_cosf(r);
-#else
-    fmx_sincos(-ph, &sn, &cs);
-#endif
-    return f32x2{x, x} * f32x2{cs, sn};
-  };
-#endif
-  // x * polar(1, -phase(w)) from the NCO word: v_sin / v_cos take turns
-  auto mix_word = [&](float x, uint32_t w) __attribute__((always_inline)) {
-    const float r = (float)(int32_t)w * 2.3283064365386963e-10f; // w / 2^32 turns, in [-0.5, 0.5)
-    const float sn = -__builtin_amdgcn_sinf(r);
-    const float cs = __builtin_amdgcn_cosf(r);
-    return f32x2{x, x} * f32x2{cs, sn};
-  };
-  // NCO step + quad-phase wrapper (liquid_wrappers.cpp:271-312)
-  auto nco_step = [&]() __attribute__((always_inline)) {
-    theta += dtheta;
-#if FMX_RDS_DIRECT_PHASE
-    ssr++;
-    return;
-#endif
-    const float now = d_nco_phase(theta);
-    float delta = now - prev_f0;
-    delta = d_unwrap(delta);
-    prev_f0 = now;
-    const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
-    float ph = phase0 + scaled;
-    ph = d_unwrap(ph);
-    phase0 = ph;
-    ssr++;
-  };
-  // FIR output (every 24th sample) -> AGC -> symsync -> PSK2 PLL -> bits
-  auto fir_output = [&]() __attribute__((always_inline)) {
-    const f32x2 f = acc[0] * fscale2;
-#pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC - 1; ++i) acc[i] = acc[i + 1];
-    acc[FMX_RDS_NACC - 1] = f32x2{0.0f, 0.0f};
-    const float yr = f.x * agc_g, yi = f.y * agc_g;
-    const float y2 = yr * yr + yi * yi;
-    agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
-    if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
-    if (agc_g > 1e6f) agc_g = 1e6f;
-    // ---- symsync: push into both MF banks' window ----
-    wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
-    L.win[wp][lane] = f32x2{yr, yi};
-    if (ss_valid < FMX_SS_SUB) ss_valid++;
-    const int w0 = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1; // oldest
-    // window entry m (oldest first) of the ring
-    auto wat = [&](int m) __attribute__((always_inline)) {
-      const int i = w0 + m;
-      return L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][lane];
-    };
-    int ns = 0;
-    f32x2 sym = f32x2{0.0f, 0.0f};
-    while (ss_b < FMX_NPFB && ns < 16) {
-      const float *hm = L.mf + ss_b * FMX_SS_SUB;
-      f32x2 acm = f32x2{0.0f, 0.0f};
-      // entries not pushed since the reset are the zeros k_reset wrote
-#pragma unroll
-      for (int m = 0; m < FMX_SS_SUB; ++m) {
-        const float h = hm[FMX_SS_SUB - 1 - m];
-        const f32x2 w = wat(m);
-        const f32x2 p = f32x2{h, h} * w;
-        acm = acm + p;
-      }
-      if (ns == 0) sym = f32x2{acm.x / 3.0f, acm.y / 3.0f};
-      if (ss_decim == 1) {
-        ss_decim = 0;
-        const float *hd = L.dmf + ss_b * FMX_SS_SUB;
-        f32x2 acd = f32x2{0.0f, 0.0f};
-#pragma unroll
-        for (int m = 0; m < FMX_SS_SUB; ++m) {
-          const float h = hd[FMX_SS_SUB - 1 - m];
-          const f32x2 p = f32x2{h, h} * wat(m);
-          acd = acd + p;
-        }
-        float q = acm.x * acd.x + acm.y * acd.y;
-        if (q > 1.0f) q = 1.0f;
-        else if (q < -1.0f) q = -1.0f;
-        const float t1 = ss_a1 * ss_v1;
-        const float v0 = q - t1;
-        ss_q_hat = ss_b0 * v0;
-        ss_v1 = v0;
-        ss_rate += ss_adj * ss_q_hat;
-        ss_del = ss_rate + ss_q_hat;
-      }
-      ss_decim++;
-      ss_tau += ss_del;
-      ss_b = (int)roundf(ss_tau * (float)FMX_NPFB);
-      ns++;
-    }
-    ss_tau -= 1.0f;
-    ss_b -= FMX_NPFB;
-    if (ns == 1) {
-      // ---- PSK2 modem phase error -> NCO PLL ----
-      const float symr = sym.x, symi = sym.y;
-      float th = atan2f(symi, symr) - dphi_psk;
-      if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
-      const bool s1 = th > 0.0f;
-      const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
-      float pe = symi * xr - symr * xi;
-      pe = d_clamp(pe, -kPiF, kPiF);
-      const float dphi = pe * 12.0f;
-      dtheta += d_nco_constrain(dphi * alpha);
-      theta += d_nco_constrain(dphi * beta);
-      // biphase / delta / block sync only consume symbols: queue them and
-      // run those decoders outside the sample loop (flush_symbols)
-      L.symq[nq][lane] = symr;
-      last_symi = symi;
-      nq++;
-    }
-  };
-  // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued symbols
+    for (int q = 0; q < 3; ++q) xr[p][q] = bload1(rin, in_off(p, q), 0);
+  // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued
+  // symbols, in the channel's first lane
   auto flush_symbols = [&]() __attribute__((always_inline)) {
-    const int nrun = act ? nq : 0; // lanes past C run the DSP in lockstep but decode nothing
-    for (int k = 0; k < nrun; ++k) {
-      const float symr = L.symq[k][lane];
-      const float bir = (symr - S.bi_prev_re) * 0.5f;
-      const int val = bir >= 0.0f;
-      const bool has = (S.bi_clock % 2u) == S.bi_polarity;
-      S.bi_prev_re = symr;
-      if ((S.bi_clock & 1u) == 0) S.bi_even += fabsf(bir);
-      else S.bi_odd += fabsf(bir);
-      S.bi_clock++;
-      if (S.bi_clock == 128u) {
-        if (S.bi_even > S.bi_odd) S.bi_polarity = 0;
-        else if (S.bi_odd > S.bi_even) S.bi_polarity = 1;
-        S.bi_even = 0.0f;
-        S.bi_odd = 0.0f;
-        S.bi_clock = 0;
+    if (lead && act) {
+      for (int k = 0; k < nq; ++k) {
+        const float symr = L.symq[k][g];
+        const float bir = (symr - S.bi_prev_re) * 0.5f;
+        const int val = bir >= 0.0f;
+        const bool has = (S.bi_clock % 2u) == S.bi_polarity;
+        S.bi_prev_re = symr;
+        if ((S.bi_clock & 1u) == 0) S.bi_even += fabsf(bir);
+        else S.bi_odd += fabsf(bir);
+        S.bi_clock++;
+        if (S.bi_clock == 128u) {
+          if (S.bi_even > S.bi_odd) S.bi_polarity = 0;
+          else if (S.bi_odd > S.bi_even) S.bi_polarity = 1;
+          S.bi_even = 0.0f;
+          S.bi_odd = 0.0f;
+          S.bi_clock = 0;
+        }
+        if (has) {
+          const int bit = (val != S.delta_prev) ? 1 : 0;
+          S.delta_prev = val;
+          rds_push_bit(S, bit, L, a, c, ng);
+        }
       }
-      if (has) {
-        const int bit = (val != S.delta_prev) ? 1 : 0;
-        S.delta_prev = val;
-        rds_push_bit(S, bit, L, a, c, ng);
-      }
+      if (nq > 0) S.bi_prev_im = last_symi;
     }
-    if (nq > 0) S.bi_prev_im = last_symi;
     nq = 0;
   };
-  __syncthreads(); // LDS tables and per-lane state written
-  // ---- input ring (see RdsLds::tin): tiles k = samples [8k, 8k + 8), tile
-  // k in ring rows (8k) % RDS_RING.  Tiles up to `ti` - 1 are issued; a tile
-  // is read once two later tiles were issued after it (vmcnt(2 x 8) then
-  // guarantees it landed, whatever stores sit between).  Rows past C read 0.
-  const int rows_valid = min(64, a.C - c0);
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + (size_t)c0 * a.in_stride,
-                                               (uint32_t)((size_t)rows_valid * a.in_stride * sizeof(float)));
-  const uint32_t row_off = (uint32_t)(lane * a.in_stride * 4);
-  int ti = 0;     // next tile to issue
-  int landed = -1; // tiles <= landed are in LDS
-  auto dma_tile = [&](int k) __attribute__((always_inline)) {
-    k = __builtin_amdgcn_readfirstlane(k); // wave-uniform: M0 without a waterfall loop
-    float *dst = &tin[(RDS_TILE * k) & (RDS_RING - 1)][0];
-    // the instruction's immediate offset would move the LDS address too: the
-    // sample offset goes into soffset
-    const int so = RDS_TILE * 4 * k;
-#define RDS_DMA1(i)                                                                                           \
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void *)(dst + 64 * (i)), 4, \
-                                           row_off, so + 4 * (i), 0, 0)
-    static_assert(RDS_TILE == 8, "dma_tile issues 8 samples");
-    RDS_DMA1(0); RDS_DMA1(1); RDS_DMA1(2); RDS_DMA1(3); RDS_DMA1(4); RDS_DMA1(5); RDS_DMA1(6); RDS_DMA1(7);
-#undef RDS_DMA1
-  };
+  __syncthreads(); // LDS tables and per-channel state written
   RDS_STAMP(0)
-  // make samples [t, t + len) readable (t moves forward, len <= RDS_TILE)
-  auto need = [&](int t, int len) __attribute__((always_inline)) {
-    t = __builtin_amdgcn_readfirstlane(t); // the sample loop's t is wave-uniform
-    const int k0 = t / RDS_TILE;
-    if (ti <= k0 + 3) {
-      // the ring slots being refilled were read by earlier chunks only
-      rds_wait(0xC07F); // lgkmcnt(0)
-      while (ti <= k0 + 3) dma_tile(ti++);
-      ti = __builtin_amdgcn_readfirstlane(ti);
-    }
-    if ((t + len - 1) / RDS_TILE > landed) {
-      RDS_STAMP(2)
-      rds_wait(0x4F70); // vmcnt(16)
-      landed = __builtin_amdgcn_readfirstlane(ti - 3);
-      RDS_STAMP(1)
-    }
-  };
-  auto read1 = [&](int t) __attribute__((always_inline)) { return tin[t & (RDS_RING - 1)][lane]; };
-  // one sample for every lane that still has input: its own tap row
-  auto step_one = [&](int t) __attribute__((always_inline)) {
-    need(t, 1);
-    if (act && t < count) {
-      const int j = (int)(ssr % FMX_RDS_DECIM);
-      const int jp = (j == 0) ? 0 : FMX_RDS_DECIM - j;
-#if FMX_RDS_DIRECT_PHASE
-      acc_add(mix_word(read1(t), theta), t, &D->rds_rows[jp][0]);
-#else
-      acc_add(mix(read1(t), phase0), t, &D->rds_rows[jp][0]);
-#endif
-      if (j == 0) fir_output();
-      nco_step();
-    }
-  };
-  const uint32_t j_mine = act ? (ssr % FMX_RDS_DECIM) : 0xFFFFFFFFu;
-  uint32_t j_first = j_mine;
-  for (int d = 32; d >= 1; d >>= 1) j_first = min(j_first, (uint32_t)__shfl_xor((int)j_first, d));
-  j_first = (uint32_t)__builtin_amdgcn_readfirstlane((int)j_first); // same in every lane: an SGPR
-  const bool uniform_j = __ballot(act && j_mine != j_first) == 0;
-  constexpr int U = RDS_U;
-  static_assert(U == 8, "the chunk tap table tT holds 8 samples");
-  // one chunk of U samples starting at a period phase of 1, 9 or 17
-  // RING: the chunk may hold some of the last FMX_RDS_RING samples (a
-  // separate instantiation: a store there makes the register allocator's
-  // reuse of its address VGPRs cost a vmcnt(0) wait in every chunk)
-  auto chunk = [&](int t, auto ring_c) __attribute__((always_inline)) {
-    constexpr bool RING = decltype(ring_c)::value;
-    t = __builtin_amdgcn_readfirstlane(t); // wave-uniform
-    need(t, U);
-    const uint32_t j0 = (j_first + (uint32_t)t) % FMX_RDS_DECIM;
-#if FMX_RDS_DIRECT_PHASE
-    float xs[U];
+  for (int r = 0; r < rmax; ++r) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) xs[u] = read1(t + u);
-    f32x2 mx[U];
+    for (int q = 0; q < 3; ++q) xr[RDS_PF][q] = bload1(rin, in_off(r + RDS_PF, q), 0);
+    const bool live = r < R;
+    const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
+    // ---- mix-down and FIR products of this lane's samples (oldest first) ----
+    f32x2 mq[3];
+    bool vq[3];
 #pragma unroll
-    for (int u = 0; u < U; ++u) mx[u] = mix_word(xs[u], theta + (uint32_t)u * dtheta);
-    theta += (uint32_t)(U - 1) * dtheta;
-    ssr += U - 1;
-#else
-    float ph[U];
-    ph[0] = phase0;
-    {
-      float nw[U - 1];
-#pragma unroll
-      for (int v = 0; v < U - 1; ++v) nw[v] = d_nco_phase(theta + (uint32_t)(v + 1) * dtheta);
-#pragma unroll
-      for (int v = 0; v < U - 1; ++v) {
-        float delta = nw[v] - (v == 0 ? prev_f0 : nw[v - 1]);
-        delta = d_unwrap(delta);
-        const float scaled = d_div_const(delta * 57000.f, 57000.f, 1.0f / 57000.f);
-        float p2 = ph[v] + scaled;
-        p2 = d_unwrap(p2);
-        ph[v + 1] = p2;
+    for (int q = 0; q < 3; ++q) {
+      const int j = j0 + 8 * q;
+      const int t = base + j;
+      vq[q] = live && t >= 0 && t < count;
+      const uint32_t w = thp + (uint32_t)j * dtheta;
+      const float rr = (float)(int32_t)w * 2.3283064365386963e-10f; // w / 2^32 turns
+      const float sn = -__builtin_amdgcn_sinf(rr);
+      const float cs = __builtin_amdgcn_cosf(rr);
+      // samples outside the call contribute nothing (their input reads 0)
+      mq[q] = vq[q] ? f32x2{xr[0][q], xr[0][q]} * f32x2{cs, sn} : f32x2{0.0f, 0.0f};
+      if (vq[q] && t >= count - FMX_RDS_RING) {
+        const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
+        *reinterpret_cast<f32x2 *>(ring + 2 * idx) = mq[q];
       }
-      theta += (uint32_t)(U - 1) * dtheta;
-      prev_f0 = nw[U - 2];
-      phase0 = ph[U - 1];
-      ssr += U - 1;
     }
-    float xs[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) xs[u] = read1(t + u);
-    f32x2 mx[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) mx[u] = mix(xs[u], ph[u]);
-#endif
-    // accumulator by accumulator, the chunk's samples oldest first: every
-    // partial sum sees the same products in the same order as the
-    // per-sample push (h[jp + 24 i] * mix, jp = 24 - j); the 8 taps of one
-    // accumulator are two broadcast 16-B LDS reads
-    if (RING) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) ring_store(mx[u], t + u);
-    }
-    {
-      const int p = (int)(j0 >> 3); // j0 = 1, 9, 17
+    if (live) {
 #pragma unroll
       for (int i = 0; i < FMX_RDS_NACC; ++i) {
-        float tu[8];
-        rds_taps8(&L.tT[p][i][0], tu);
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[i] = rds_mac(tu[u], mx[u], acc[i]);
+        const float4 h = *reinterpret_cast<const float4 *>(&L.hq[j0][i][0]);
+        // the lane's samples oldest first, as the window dot product (a
+        // sample outside the call is 0 and adds +0)
+        acc[i] = __builtin_elementwise_fma(f32x2{h.x, h.x}, mq[0], acc[i]);
+        acc[i] = __builtin_elementwise_fma(f32x2{h.y, h.y}, mq[1], acc[i]);
+        acc[i] = __builtin_elementwise_fma(f32x2{h.z, h.z}, mq[2], acc[i]);
       }
+    }
+    RDS_STAMP(1)
+    const bool has_out = live && base + FMX_RDS_DECIM - 1 < count;
+    if (has_out) {
+      // ---- FIR output (every 24th sample) -> AGC -> symsync -> PSK2 PLL ----
+      const f32x2 f = f32x2{rds_sum8(acc[0].x), rds_sum8(acc[0].y)} * fscale2;
+#pragma unroll
+      for (int i = 0; i < FMX_RDS_NACC - 1; ++i) acc[i] = acc[i + 1];
+      acc[FMX_RDS_NACC - 1] = f32x2{0.0f, 0.0f};
+      const float yr = f.x * agc_g, yi = f.y * agc_g;
+      const float y2 = yr * yr + yi * yi;
+      agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
+      if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
+      if (agc_g > 1e6f) agc_g = 1e6f;
+      // ---- symsync: push into both MF banks' window ----
+      wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
+      if (lead) L.win[wp][g] = f32x2{yr, yi};
+      if (ss_valid < FMX_SS_SUB) ss_valid++;
+      const int w0 = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1; // oldest
+      auto wat = [&](int m) __attribute__((always_inline)) {
+        const int i = w0 + m;
+        return L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][g];
+      };
+      int ns = 0;
+      f32x2 sym = f32x2{0.0f, 0.0f};
+      while (ss_b < FMX_NPFB && ns < 16) {
+        const float *hm = L.mf + ss_b * FMX_SS_SUB;
+        f32x2 acm = f32x2{0.0f, 0.0f};
+        // entries not pushed since the reset are the zeros k_reset wrote
+#pragma unroll 6
+        for (int m = 0; m < FMX_SS_SUB; ++m) {
+          const float h = hm[FMX_SS_SUB - 1 - m];
+          const f32x2 w = wat(m);
+          const f32x2 p = f32x2{h, h} * w;
+          acm = acm + p;
+        }
+        if (ns == 0) sym = f32x2{acm.x / 3.0f, acm.y / 3.0f};
+        if (ss_decim == 1) {
+          ss_decim = 0;
+          const float *hd = L.dmf + ss_b * FMX_SS_SUB;
+          f32x2 acd = f32x2{0.0f, 0.0f};
+#pragma unroll 6
+          for (int m = 0; m < FMX_SS_SUB; ++m) {
+            const float h = hd[FMX_SS_SUB - 1 - m];
+            const f32x2 p = f32x2{h, h} * wat(m);
+            acd = acd + p;
+          }
+          float qe = acm.x * acd.x + acm.y * acd.y;
+          if (qe > 1.0f) qe = 1.0f;
+          else if (qe < -1.0f) qe = -1.0f;
+          const float t1 = ss_a1 * ss_v1;
+          const float v0 = qe - t1;
+          ss_q_hat = ss_b0 * v0;
+          ss_v1 = v0;
+          ss_rate += ss_adj * ss_q_hat;
+          ss_del = ss_rate + ss_q_hat;
+        }
+        ss_decim++;
+        ss_tau += ss_del;
+        ss_b = (int)roundf(ss_tau * (float)FMX_NPFB);
+        ns++;
+      }
+      ss_tau -= 1.0f;
+      ss_b -= FMX_NPFB;
+      // the NCO word of the instant's sample; step() follows the PLL update
+      uint32_t tho = thp + (uint32_t)(FMX_RDS_DECIM - 1) * dtheta;
+      if (ns == 1) {
+        // ---- PSK2 modem phase error -> NCO PLL ----
+        const float symr = sym.x, symi = sym.y;
+        float th = atan2f(symi, symr) - dphi_psk;
+        if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
+        const bool s1 = th > 0.0f;
+        const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
+        float pe = symi * xr - symr * xi;
+        pe = d_clamp(pe, -kPiF, kPiF);
+        const float dphi = pe * 12.0f;
+        dtheta += d_nco_constrain(dphi * alpha);
+        tho += d_nco_constrain(dphi * beta);
+        // biphase / delta / block sync only consume symbols: queue them and
+        // run those decoders outside the sample loop (flush_symbols)
+        if (lead) L.symq[nq][g] = symr;
+        last_symi = symi;
+        nq++;
+      }
+      thp = tho + dtheta; // period position 0 of the next round
+    } else if (live) {
+      // tail: samples base .. count-1 stepped, no decimation instant
+      thp = thp + (uint32_t)(count - base) * dtheta;
     }
     RDS_STAMP(2)
-    if (j0 == (uint32_t)(FMX_RDS_DECIM + 1 - U)) { // the chunk ends on the FIR output
-      fir_output();
+#pragma unroll
+    for (int p = 0; p < RDS_PF; ++p)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xr[p][q] = xr[p + 1][q];
+    // decoders every RDS_SYMQ - 2 rounds (at most one symbol per round)
+    if (r % (RDS_SYMQ - 2) == RDS_SYMQ - 3) {
+      flush_symbols();
       RDS_STAMP(3)
     }
-    nco_step(); // the chunk's last sample, after a PLL update if any
-  };
-  // Segments of <= RDS_SEG samples (<= RDS_SYMQ - 2 symbols), the queued
-  // symbols decoded at each segment end.  One call site each for the chunk,
-  // the generic sample step and the decoders keeps the code (and the exec-mask
-  // nesting) small.
-  constexpr int RDS_SEG = FMX_RDS_DECIM * (RDS_SYMQ - 4);
-  int t = 0;
-  while (t < nmax) {
-    int tend = t + RDS_SEG;
-    if (uniform_j) tend -= (int)(((j_first + (uint32_t)tend) % FMX_RDS_DECIM + FMX_RDS_DECIM - 1) % FMX_RDS_DECIM);
-    tend = min(tend, nmax);
-    const int cend = min(tend, cmin);
-    while (t < tend) {
-      if (uniform_j && t + U <= cend && ((j_first + (uint32_t)t) % FMX_RDS_DECIM) % (uint32_t)U == 1u) {
-        if (t + U > ring_from) chunk(t, std::true_type{});
-        else chunk(t, std::false_type{});
-        t += U;
-      } else {
-        step_one(t++);
-        RDS_STAMP(4)
-      }
-    }
-    flush_symbols();
-    RDS_STAMP(5)
   }
-  // no LDS-DMA may still be in flight when the workgroup's LDS is released
-  rds_wait(0x0F70); // vmcnt(0)
-  if (!act) return;
+  flush_symbols();
+  RDS_STAMP(3)
+  // the channel's partial sums: the lanes' shares added (every lane gets them)
+#pragma unroll
+  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{rds_sum8(acc[i].x), rds_sum8(acc[i].y)};
+  if (!act || !lead) return;
   // ---- registers -> state ----
   FmxRdsState *out = a.st + c;
-  out->theta = theta;
+  // the NCO word of the next sample: after a decimation instant thp is the
+  // next period's position 0, after a tail (period start + tail length)
+  out->theta = (R > 0) ? thp : theta;
   out->dtheta = dtheta;
-#if FMX_RDS_DIRECT_PHASE
   // the wrapper's phases as the reference would hold them (= the NCO phase)
   out->prev_f0 = d_nco_phase(theta);
   out->phase0 = d_unwrap(d_nco_phase(theta));
-#else
-  out->prev_f0 = prev_f0;
-  out->phase0 = phase0;
-#endif
-  out->sample_since_reset = ssr;
+  out->sample_since_reset = ssr0 + (uint32_t)count;
   out->ring_pos = ring0 + (uint32_t)count;
   out->rebuild = 0;
   for (int i = 0; i < FMX_RDS_NACC; ++i) {
@@ -2824,7 +2553,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   out->agc_y2p = agc_y2p;
   for (int m = 0; m < FMX_SS_SUB; ++m) {
     const int i = wp + 1 + m;
-    const f32x2 w = L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][lane];
+    const f32x2 w = L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][g];
     out->ss_win_re[m] = w.x;
     out->ss_win_im[m] = w.y;
   }
@@ -2839,7 +2568,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   out->ss_decim = ss_decim;
   rds_bits_store(*out, S);
   if (a.group_count) a.group_count[c] = ng;
-  RDS_STAMP(6)
+  RDS_STAMP(4)
 #ifdef FMX_STAMPS
   if (a.dbg && lane == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, rs_acc[k]);
@@ -3026,21 +2755,6 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
 __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
-#ifndef FMX_DEC_MFMA
-#define FMX_DEC_MFMA 1 // k_fe8 decimator on v_mfma_f32_16x16x32_f16 (0: packed-FMA VALU decimator, A/B runs)
-#endif
-#ifndef FMX_IQ_MFMA
-#define FMX_IQ_MFMA 1 // k_fe8 IQ FIR on v_mfma_f32_16x16x32_f16 (0: packed-FMA fir8_c, A/B runs)
-#endif
-#ifndef FMX_DEC_FRAG
-#define FMX_DEC_FRAG 1 // MFMA decimator A fragments from FmxDesign::dec_frag (0: per-chunk LDS tap table)
-#endif
-#ifndef FMX_RS_FMA
-#define FMX_RS_FMA 0 // 1: k_fe8's RDS resampler terms as scalar FMAs (k_fe8 isolated -1.7 %, step unchanged)
-#endif
-#ifndef FMX_RS_PACKED
-#define FMX_RS_PACKED 0 // 1: k_fe8's RDS resampler on packed FP32 (v_pk_mul / v_pk_add), see the resampler
-#endif
 #ifndef FMX_DEC_KS_UNROLL
 #define FMX_DEC_KS_UNROLL 7
 #endif
@@ -3085,11 +2799,6 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
-  // MFMA decimator tap table (copy 0 of FmxDesign::dec_q16: hi, lo), per
-  // chunk in the hi image's chunk part (dead until the discriminator)
-  static constexpr int TQ = MX + 2 * FMX_HIST;
-  static constexpr int TQ_WORDS = FMX_DQ_N; // [hi, lo][FMX_DQ_N] f16
-  static_assert(TQ_WORDS * 4 <= 2 * FE8_T, "tap table inside the hi image's chunk part");
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
   // (16-B aligned, above the complex image, inside the dead raw region)
   static constexpr int STG = (YB + 15) & ~15;
@@ -3098,53 +2807,17 @@ template <int M, int TPP> struct Fe8Layout {
                 "IQ images below yb, 16-B aligned rows");
 };
 
-// 8 outputs j0..j0+7 (j0 % 8 == 0) of a real-tap FIR of runtime length P on
-// a padded LDS image x (input i at x[fe8_i(i)]); hz = taps with 16 zeros on
-// each side (hz[16 + k] = h[k]).  Per output the FMA chain runs oldest input
-// first.  The filter is run as length P8 = P rounded up to 8k + 1 (up to 7
-// zero taps at the oldest end: the chain starts with +0 products, same sums),
-// so every group of 8 inputs is one 9-element row of the image: one address
-// per group, the 8 reads by immediate offsets.
+// The MFMA FIRs (IQ FIR, pilot BPF) run a P-tap filter as length P8 = P
+// rounded up to 8k + 1 (up to 7 zero taps at the oldest end, same sums), so
+// every K step starts on an 8-sample boundary.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
-// Complex input (float2 image), real taps: 8 outputs as packed (re, im).
-__device__ __forceinline__ void fir8_c(const float2 *x, int j0, const float *__restrict__ hz, int P, f32x2 (&acc)[8]) {
-#pragma unroll
-  for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
-  const int P8 = fir8_len(P);
-  const float2 *xg = x + 9 * ((j0 - (P8 - 1)) >> 3);
-#pragma unroll 2
-  for (int m0 = 0; m0 < P8 + 7; m0 += 8) {
-    const FMX_CONST float *tw = cptr(hz) + 16 + (P8 - 1) - m0 - 7;
-    float t[16];
-#pragma unroll
-    for (int k = 0; k < 15; ++k) t[k] = tw[k];
-    t[15] = 0.0f;
-    const float2 *xr = xg + 9 * (m0 >> 3);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float2 v = xr[u];
-      const f32x2 vv = {v.x, v.y};
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float h = t[7 + r - u];
-        acc[r] = __builtin_elementwise_fma(f32x2{h, h}, vv, acc[r]);
-      }
-    }
-  }
-}
-
 template <int M, int TPP>
 __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP>;
-  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
-  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
-  else if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
-  float2 *xin = reinterpret_cast<float2 *>(smem + LY::XIN);
-  (void)xin;
   float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
   _Float16 *xh = reinterpret_cast<_Float16 *>(smem + LY::MX);  // MPX hi, index FMX_HIST + j
   _Float16 *xl = reinterpret_cast<_Float16 *>(smem + LY::XLO); // MPX lo
@@ -3158,7 +2831,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
   typedef float f32x4_t __attribute__((ext_vector_type(4)));
   const bool want_sig = a.sig_sums != nullptr;
-#if FMX_IQ_MFMA
   // IQ FIR input images (alias xin): I hi, I lo, Q hi, Q lo of the DC blockers'
   // outputs x 2^10, sample i at [i] (i < FE_HALO_IQ: the carried history)
   _Float16 *xih = reinterpret_cast<_Float16 *>(smem + LY::XIN);
@@ -3166,7 +2838,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   _Float16 *xqh = xih + 2 * LY::IQW;
   _Float16 *xql = xih + 3 * LY::IQW;
   constexpr float kIqIn = 1024.0f;
-#endif
 #ifdef FMX_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
@@ -3189,8 +2860,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   const int n = a.n;
   const FmxChanParam par = a.par[c];
   const int iqL = D->iq_len[par.iqsel];
-  const float *__restrict__ iqz = D->iq_z16[par.iqsel];
-  (void)iqz;
   const float iqscale = D->iq_scale[par.iqsel];
   const bool pilot = a.pilot_out != nullptr;
   const bool rds = a.rds_out != nullptr;
@@ -3285,19 +2954,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
     // ================= decimator =================
-#if FMX_DEC_MFMA && !FMX_DEC_FRAG
-    // the MFMA tap tables into the MPX image's chunk part (dead until the
-    // discriminator below writes it)
-    {
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(&D->dec_q16[0][0][0]);
-      uint32_t *dst = reinterpret_cast<uint32_t *>(smem + LY::TQ);
-#pragma unroll
-      for (int k = 0; k < (LY::TQ_WORDS + 255) / 256; ++k) {
-        const int i = tid + 256 * k;
-        if (i < LY::TQ_WORDS) dst[i] = src[i];
-      }
-    }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
     FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
@@ -3321,7 +2977,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
     }
     float2 xv[8]; // decimator outputs of this thread
-#if FMX_DEC_MFMA
     {
       // Decimator as v_mfma_f32_16x16x32_f16 tiles.  Output o = 16 B + r of
       // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
@@ -3340,15 +2995,11 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN && KS <= FMX_DEC_KS_MAX, "tap table range");
       const int col = lane & 15, g = lane >> 4;
       const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0 (even)
-#if FMX_DEC_FRAG
       // A fragments from the design (FmxDesign::dec_frag, 16-B per lane, one
       // K step ahead) instead of 8 dword LDS reads per K step
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag[0][0][0][0]) + lane;
       u32x4 fh = fa[0], fl = fa[64];
       (void)d00;
-#else
-      const uint32_t *ta = reinterpret_cast<const uint32_t *>(smem + LY::TQ) + ((d00 - FMX_DQ_MIN) >> 1);
-#endif
       const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 16 * g;
       f32x4_t acc[2][2];
 #pragma unroll
@@ -3359,26 +3010,13 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         return __builtin_bit_cast(f16x2_t, __builtin_amdgcn_perm(0x64646464u, w, sel)) -
                f16x2_t{(_Float16)1152.0f, (_Float16)1152.0f};
       };
-#ifdef FMX_DIAG_DEC_KS
-      // diagnostic builds only: the MFMA loop cut to FMX_DIAG_DEC_KS steps (outputs invalid)
-#pragma unroll FMX_DEC_KS_UNROLL
-      for (int ks = 0; ks < FMX_DIAG_DEC_KS; ++ks) {
-#else
 #pragma unroll FMX_DEC_KS_UNROLL
       for (int ks = 0; ks < KS; ++ks) {
-#endif
-#if FMX_DEC_FRAG
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, fh), alo = __builtin_bit_cast(f16x8_t, fl);
         if (ks + 1 < KS) {
           fh = fa[128 * (ks + 1)];
           fl = fa[128 * (ks + 1) + 64];
         }
-#else
-        // 4-B aligned fragments (d00 is even): dword reads
-        const uint32_t *th = ta + 16 * ks, *tlo = ta + FMX_DQ_N / 2 + 16 * ks;
-        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, u32x4{th[0], th[1], th[2], th[3]});
-        const f16x8_t alo = __builtin_bit_cast(f16x8_t, u32x4{tlo[0], tlo[1], tlo[2], tlo[3]});
-#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const u32x4 w = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * ks);
@@ -3423,75 +3061,9 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         if (fabsf(xv[r].x) >= 0.995f || fabsf(xv[r].y) >= 0.995f) myclip++;
       if (myclip) atomicAdd(&sh->clip, myclip);
     }
-#else
-    {
-      // thread window: samples s = 0 .. 8G-1 from raw sample 8*M*tid; output
-      // r uses s in [r*M + 1, r*M + L] with tap L + r*M - s
-      f32x2 acc[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.0f, 0.0f};
-      const u32x4 *rw = reinterpret_cast<const u32x4 *>(raw) + M * tid;
-      const FMX_CONST float *hd = cptr(D->dec_taps);
-      // one group of 8 samples: live (s, r) pairs known at compile time
-      // (head / tail of the window), or all live (middle, runtime loop with
-      // the tap base in SGPRs)
-      auto group = [&](int g, auto live_known) __attribute__((always_inline)) {
-        const u32x4 w = rw[g];
-        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-        // tap of (u, r) = hb[r*M - u]; the opaque zero keeps the compiler from
-        // hoisting every group's tap loads into SGPRs at once (spills)
-        int z;
-        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-        const FMX_CONST float *hb = hd + (L - 8 * g + z);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          constexpr bool known = decltype(live_known)::value;
-          if (known) {
-            bool live = false;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) live = live || (8 * g + u >= r * M + 1 && 8 * g + u <= r * M + L);
-            if (!live) continue;
-          }
-          const uint32_t wd = ww[u >> 1];
-          const int sh0 = (u & 1) ? 16 : 0;
-          f32x2 x;
-          // raw byte values: 127.5 * sum(h) comes off once per output below
-          x.x = (float)((wd >> sh0) & 255u);
-          x.y = (float)((wd >> (sh0 + 8)) & 255u);
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            if (known) {
-              const int k = L + r * M - (8 * g + u);
-              if (k < 0 || k >= L) continue;
-            }
-            const float h = hb[r * M - u];
-            acc[r] = __builtin_elementwise_fma(f32x2{h, h}, x, acc[r]);
-          }
-        }
-      };
-      constexpr int GH = (7 * M + 1 + 7) / 8;  // first group where every output is live
-      constexpr int GT = (L - 7) / 8;          // last such group
-#pragma unroll
-      for (int g = 0; g < GH; ++g) group(g, std::true_type{});
-#pragma unroll 2
-      for (int g = GH; g <= GT; ++g) group(g, std::false_type{});
-#pragma unroll
-      for (int g = GT + 1; g < LY::G; ++g) group(g, std::true_type{});
-      int myclip = 0;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float yr = (acc[r].x - D->dec_dc) * D->dec_scale;
-        const float yi = (acc[r].y - D->dec_dc) * D->dec_scale;
-        if (fabsf(yr) >= 0.995f || fabsf(yi) >= 0.995f) myclip++;
-        xv[r] = make_float2(yr, yi);
-      }
-      if (myclip) atomicAdd(&sh->clip, myclip);
-    }
-#endif
     __syncthreads(); // raw is dead: xin / yb alias it from here on
     FE_STAMP(0)
     // IQ FIR history and the zero slack past the chunk (read with zero taps)
-#if FMX_IQ_MFMA
     if (tid < FE_HALO_IQ) {
       const float2 v = hx[tid];
       const float sI = v.x * kIqIn, sQ = v.y * kIqIn;
@@ -3505,10 +3077,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       const int i = FE_HALO_IQ + FE8_T + tid;
       xih[i] = xil[i] = xqh[i] = xql[i] = (_Float16)0.0f;
     }
-#else
-    if (tid < FE_HALO_IQ) xin[fe8_i(tid)] = hx[tid];
-    if (tid < 16) xin[fe8_i(FE_HALO_IQ + FE8_T + tid)] = make_float2(0.0f, 0.0f);
-#endif
     // ================= DC blockers: affine scan, 8 per thread =================
     {
       float A = 1.0f, BI = 0.0f, BQ = 0.0f;
@@ -3547,14 +3115,11 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       vI = eA * vI + eI;
       vQ = eA * vQ + eQ;
       // the state before this thread's first element, then the reference's op order
-#if FMX_IQ_MFMA
       f16x8_t ih, il, qh, ql;
-#endif
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const float tI = dc_a1 * vI, tQ = dc_a1 * vQ;
         const float nI = xv[r].x - tI, nQ = xv[r].y - tQ;
-#if FMX_IQ_MFMA
         const float oI = nI - vI, oQ = nQ - vQ;
         const float sI = oI * kIqIn, sQ = oQ * kIqIn;
         ih[r] = (_Float16)sI;
@@ -3563,18 +3128,13 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         ql[r] = (_Float16)(sQ - (float)qh[r]);
         // the next chunk's IQ FIR history (f32; read above before the scan's barrier)
         if (j0 + r >= FE8_T - FE_HALO_IQ) hx[j0 + r - (FE8_T - FE_HALO_IQ)] = make_float2(oI, oQ);
-#else
-        xin[fe8_i(FE_HALO_IQ + j0 + r)] = make_float2(nI - vI, nQ - vQ);
-#endif
         vI = nI;
         vQ = nQ;
       }
-#if FMX_IQ_MFMA
       *reinterpret_cast<f16x8_t *>(xih + FE_HALO_IQ + j0) = ih;
       *reinterpret_cast<f16x8_t *>(xil + FE_HALO_IQ + j0) = il;
       *reinterpret_cast<f16x8_t *>(xqh + FE_HALO_IQ + j0) = qh;
       *reinterpret_cast<f16x8_t *>(xql + FE_HALO_IQ + j0) = ql;
-#endif
       __syncthreads();
       if (tid == 255) {
         sh->carry_i = vI;
@@ -3584,7 +3144,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     __syncthreads();
     FE_STAMP(1)
     // ================= IQ FIR =================
-#if FMX_IQ_MFMA
     {
       // v_mfma_f32_16x16x32_f16 tiles as the pilot BPF's: 16 outputs (rows,
       // A = taps, FmxDesign::iq_frag) of 16 blocks of 16 outputs (columns, B
@@ -3632,15 +3191,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
       if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
     }
-#else
-    {
-      f32x2 z[8];
-      fir8_c(xin, FE_HALO_IQ + j0, iqz, iqL, z);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) yb[1 + j0 + r] = make_float2(z[r].x * iqscale, z[r].y * iqscale);
-      if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
-    }
-#endif
     __syncthreads();
     // ================= AGC (serial, only when enabled) =================
     if (par.agc != 0) {
@@ -3668,11 +3218,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         const float2 p = yb[j], r = yb[1 + j];
         const float re = p.x * r.x + p.y * r.y;
         const float im = p.x * r.y - p.y * r.x;
-#if defined(FMX_DIAG_DISC) && FMX_DIAG_DISC == 1
-        const float m = atan2f(im, re) * ref; // diagnostic builds only: the libm atan2f (not deterministic here)
-#else
         const float m = fmx_atan2f(im, re) * ref; // select-free (fmx_math.h)
-#endif
         mv[k] = m;
         // f16 hi / lo split for the MFMA pilot BPF (m = hi + lo to 22 bits)
         const _Float16 hv = (_Float16)m;
@@ -3685,9 +3231,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         sh->fd_re = yb[FE8_T].x;
         sh->fd_im = yb[FE8_T].y;
       }
-#if !FMX_IQ_MFMA
-      if (tid < FE_HALO_IQ) hx[tid] = xin[fe8_i(tid + FE8_T)]; // IQ FIR history for the next chunk
-#endif
     }
     __syncthreads(); // xin / yb are dead: the next chunk may land in raw (below uc)
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
@@ -3772,16 +3315,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           asm volatile("" : "+v"(xa), "+v"(ha));
           const lds_f32 *xu = (const lds_f32 *)(uintptr_t)xa;
           const lds_f32x2 *hk = (const lds_f32x2 *)(uintptr_t)ha;
-#if FMX_RS_PACKED
-          f32x2 y = {0.0f, 0.0f};
-#pragma unroll
-          for (int m = 0; m < LY::RS_M; ++m) {
-            const float v = xu[m];
-            // separate multiply and add (an FMA here measured no faster)
-            const f32x2 p = hk[m] * f32x2{v, v};
-            y = y + p;
-          }
-#else
           // scalar multiplies and adds (same rounding): the packed-FP32 form
           // (v_pk_mul / v_pk_add) returned wrong upper-32-lane results,
           // nondeterministically, with two k_fe8 workgroups per CU issuing
@@ -3792,21 +3325,13 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
             const float v = xu[m];
             const f32x2 hm = hk[m];
             // as asm so that the vectorizer cannot pair them into v_pk_* again
-#if FMX_RS_FMA
-            // one FMA per term (one rounding instead of two; RDS groups stay
-            // bit-exact against the oracle, as k_rds's FMA partial sums)
-            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(y0) : "v"(hm.x), "v"(v), "v"(y0));
-            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(y1) : "v"(hm.y), "v"(v), "v"(y1));
-#else
             float p0, p1;
             asm("v_mul_f32 %0, %1, %2" : "=v"(p0) : "v"(hm.x), "v"(v));
             asm("v_mul_f32 %0, %1, %2" : "=v"(p1) : "v"(hm.y), "v"(v));
             asm("v_add_f32 %0, %1, %2" : "=v"(y0) : "v"(y0), "v"(p0));
             asm("v_add_f32 %0, %1, %2" : "=v"(y1) : "v"(y1), "v"(p1));
-#endif
           }
           const f32x2 y = {y0, y1};
-#endif
           const float w0f = (1.0f - en[k].mu) * y.x;
           const float w1f = en[k].mu * y.y;
           a.rds_out[(size_t)c * a.rds_stride + e] = w0f + w1f;
@@ -3888,13 +3413,7 @@ template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st)
   // k_pll or k_rds workgroup (36 KB each, 36 864 B allocated)
   static_assert(Fe8Layout<M, TPP>::BYTES <= (160 * 1024 - 36864) / 2, "k_fe8: two workgroups per CU plus a k_pll / k_rds workgroup");
   static_assert(Fe8Layout<M, TPP>::UOFF >= Fe8Layout<M, TPP>::YB, "RDS copy above the IQ image");
-  size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
-  // diagnostic: FMX_DIAG_FE8_LDS=<bytes> launches with more LDS (fewer workgroups per CU)
-  static const size_t diag_lds = [] {
-    const char *e = std::getenv("FMX_DIAG_FE8_LDS");
-    return e ? (size_t)std::atol(e) : (size_t)0;
-  }();
-  if (diag_lds > smem) smem = diag_lds;
+  const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
   static bool configured = false;
   if (!configured) {
     if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fe8<M, TPP>),
@@ -3937,11 +3456,7 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   const bool fe8 = vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
                    (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
                    a.des_fs >= 190000;
-  static const bool no_fe8 = [] { // diagnostic: FMX_DIAG_NO_FE8=1 runs k_frontend for every call
-    const char *e = std::getenv("FMX_DIAG_NO_FE8");
-    return e && e[0] == '1';
-  }();
-  if (fe8 && !no_fe8) {
+  if (fe8) {
     if (M == 10 && tpp == 28) return fe8_launch<10, 28>(a, st);
     if (M == 8 && tpp == 28) return fe8_launch<8, 28>(a, st);
     if (M == 4 && tpp == 20) return fe8_launch<4, 20>(a, st);
@@ -3959,22 +3474,14 @@ int launch_pll(const PllArgs &a, void *stream) {
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {
-  // diagnostic: FMX_DIAG_AU_LDS=<bytes> launches with more LDS (fewer workgroups per CU)
-  static const size_t au_lds = [] {
-    const char *e = std::getenv("FMX_DIAG_AU_LDS");
-    const size_t v = e ? (size_t)std::atol(e) : (size_t)0;
-    if (v > sizeof(AuShared))
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_audio), hipFuncAttributeMaxDynamicSharedMemorySize, (int)v);
-    return v > sizeof(AuShared) ? v : sizeof(AuShared);
-  }();
-  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), au_lds, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_rds(const RdsArgs &a, void *stream) {
-  // two k_fe8 workgroups (2 x 60.5 KB) leave 39 KB of a CU's 160 KB: k_rds
-  // fits beside them (as k_pll's 35.5 KB does)
-  static_assert(sizeof(RdsLds) + RDS_RING * 64 * 4 <= 38 * 1024, "k_rds LDS must fit beside two k_fe8 workgroups");
-  hipLaunchKernelGGL(k_rds, dim3((a.C + 63) / 64), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
+  // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
+  // k_rds workgroups fit beside them
+  static_assert(sizeof(RdsLds) <= 12 * 1024, "k_rds LDS");
+  hipLaunchKernelGGL(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 // 16-B words src -> dst (the schedule upload from mapped pinned memory)

@@ -1,6 +1,6 @@
 """Diagnostic: per-stage clocks of k_frontend and k_rds on the bench workload.
-Needs libfmx.so built with `make -C fmtuner-sdr_amd STAMPS=1 -B`; runs with
-FMX_STAMPS=1 (set here).  Prints
+Needs the diagnostics library (make -C fmtuner-sdr_amd diag; FMX_LIB=...
+libfmx_diag.so); runs with FMX_STAMPS=1 (set here).  Prints
 the share of each stage in thread 0's timeline."""
 import ctypes as C
 import os
@@ -37,17 +37,15 @@ tot = sum(v[:8])
 print("k_frontend (thread 0 of each workgroup)")
 for k in range(8):
     print(f"  {NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
-RN = ["setup", "tile-wait", "chunk", "fir_out", "step_one", "decode", "store", "-"]
-tot = sum(v[8:]) or 1
-nwg = (Cn + 63) // 64
-print("k_rds (lane 0 of each workgroup)")
+RN = ["setup", "mix+fir", "out+agc+ss+pll", "decode", "store", "-", "-", "-"]
+tot = sum(v[8:16]) or 1
+nwg = (Cn + 7) // 8
+print("k_rds (lane 0 of each workgroup of 8 channels)")
 for k in range(8):
     print(f"  {RN[k]:10s} {v[8 + k] / tot * 100:6.1f} %  {v[8 + k] / (nwg * nblk):10.0f} ticks/launch-WG")
 nwg = (Cn + 63) // 64
 print("k_pll per wave (lane 0): work / barrier-wait ticks per launch-WG")
-for w, nm in enumerate(["W0 chain", "W1 env", "W2a", "W2b", "(idle)", "W3 blend+load"]):
+for w, nm in enumerate(["W0 chain", "W1 recurrences", "P0", "P1", "P2", "W3 blend+load", "P3"]):
     wk, wt = v[16 + 2 * w], v[17 + 2 * w]
     print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}")
-print(f"  W3 issue part {v[28] / (nwg * nblk):10.0f}")
-print(f"  W3 store part {v[29] / (nwg * nblk):10.0f}")
 print(f"  W0 realtime per WG (100 MHz ticks): mean {v[30] / (nwg * nblk):10.0f}  max over WGs and launches {v[31]:10.0f}")
