@@ -639,8 +639,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->dsig, C * 4)) != FMX_OK) return rc;
 #if FMX_DIAG
   if (const char *e = std::getenv("FMX_STAMPS"); e && e[0] == '1') {
-    if ((rc = dalloc(h, &h->dbg, 32)) != FMX_OK) return rc; // [0,8) frontend, [8,16) k_rds, [16,26) k_pll
-    HIP_TRY(hipMemset(h->dbg, 0, 32 * sizeof(unsigned long long)));
+    if ((rc = dalloc(h, &h->dbg, 48)) != FMX_OK) return rc; // [0,8) frontend, [8,16) k_rds, [16,32) k_pll, [32,48) sub-stage clocks
+    HIP_TRY(hipMemset(h->dbg, 0, 48 * sizeof(unsigned long long)));
   }
 #endif
   if ((rc = dalloc(h, &h->sig_smooth, C * 2)) != FMX_OK) return rc;
@@ -1100,7 +1100,7 @@ int fmx_debug_stamps(void *handle, unsigned long long *out, int n) {
   Handle *h = H(handle);
   if (!h || !h->dbg || n < 8) return FMX_E_INVALID;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->dbg, (n >= 32 ? 32 : n >= 16 ? 16 : 8) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, h->dbg, (n >= 48 ? 48 : n >= 32 ? 32 : n >= 16 ? 16 : 8) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return FMX_OK;
 }
 
@@ -1586,22 +1586,25 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
-    case 13: // k_fe8 MFMA decimator taps back from the A fragments (row 0 lanes), as dec_taps_raw
+    case 13: // k_fe8 i8 MFMA decimator taps back from the int8 digit fragments (row 0 lanes), as dec_taps_raw
       for (int k = 0; k < d->dec_len; ++k) {
         const int dd = d->dec_len - k;
-        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
-        const double q = f16_value(d->dec_frag[ks][0][l][j]) + f16_value(d->dec_frag[ks][1][l][j]);
-        v.push_back(static_cast<float>(q / 65536.0 * 127.5));
+        const int ks = dd / 64, gg = (dd % 64) / 16, j = dd % 16, l = 16 * gg;
+        const long q = 65536L * d->dec_frag8[ks][0][l][j] + 256L * d->dec_frag8[ks][1][l][j] + d->dec_frag8[ks][2][l][j];
+        v.push_back(static_cast<float>(std::ldexp(static_cast<double>(q), -d->dec_s8) * 127.5));
       }
       break;
-    case 9: // k_fe8 MFMA decimator taps back from the f16 hi/lo tables (copy 0 and copy 1), as dec_taps_raw
-      for (int cp = 0; cp < 2; ++cp)
+    case 9: { // the i8 decimator's rows 1..15 (lane l = row r): every row holds the same taps shifted by M r
+      const int M = d->M;
+      for (int r = 0; r < 16; ++r)
         for (int k = 0; k < d->dec_len; ++k) {
-          const int x = (d->dec_len - k) - FMX_DQ_MIN + 2 * cp;
-          const double q = f16_value(d->dec_q16[cp][0][x]) + f16_value(d->dec_q16[cp][1][x]);
-          v.push_back(static_cast<float>(q / 65536.0 * 127.5));
+          const int dd = d->dec_len - k + M * r;
+          const int ks = dd / 64, gg = (dd % 64) / 16, j = dd % 16, l = 16 * gg + r;
+          const long q = 65536L * d->dec_frag8[ks][0][l][j] + 256L * d->dec_frag8[ks][1][l][j] + d->dec_frag8[ks][2][l][j];
+          v.push_back(static_cast<float>(std::ldexp(static_cast<double>(q), -d->dec_s8) * 127.5));
         }
       break;
+    }
     default: delete d; return FMX_E_INVALID;
   }
   delete d;

@@ -46,7 +46,6 @@ namespace fmx {
 #define AU_HALO 120
 #define AU_RHALO 32
 #define AU_MAXOUT 256
-#define PLL_T 4
 
 static constexpr float kPiF = 3.14159265358979323846f;
 
@@ -982,15 +981,16 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 /* k_pll: StereoDecoder per-sample recurrences                         */
 /* ================================================================== */
 /* k_pll is a seven-wave software pipeline over tiles of PLL_T samples for
- * PLL_CH channels.  Serial waves hold one channel per lane; the P waves
- * hold one item (row, t) of a tile per lane (rows 16 p .. 16 p + 15, t =
- * lane % 4) and run two stages per iteration:
+ * PLL_CH channels (PLL_CH x PLL_T = 256 items per tile).  Serial waves hold
+ * one channel per lane (lanes >= PLL_CH idle); the P waves hold one item
+ * (row, t) of a tile per lane (items 64 p .. 64 p + 63, row = item / PLL_T,
+ * t = item % PLL_T) and run two stages per iteration:
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
  *                 pll_step, step; it hands the NCO words on       stereo_decoder.cpp:178-186
  *   P phase       tile k-1: v_sin / v_cos of each word, the float phase of
  *                 the word (the reference's phase()), the previous
- *                 sample's values by DPP within the item quad (t = 0: the
- *                 quad's t = 3 of the previous iteration); the pilot I/Q
+ *                 sample's values from the lane before (t = 0: the row's
+ *                 t = PLL_T - 1 of the previous iteration); the pilot I/Q
  *                 integrator inputs (pilot * vco) * kI, the PLL frequency
  *                 (unwrap, clamp) and cos(2 phase)                  :176-199,219-221
  *   W1 (serial)   the four linear recurrences (pilot / MPX envelopes, the
@@ -1006,23 +1006,31 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
  * with the reference's arithmetic in the reference's order; only WHERE it
  * runs moved.
  *
- * Round 3 (from eight waves): the chain's NCO constrain is
- * fract(err * beta/2pi) * 2^32 in f32 and its sine v_sin_f32 of the word in
- * turns (tools/ubench/chainlat.hip: 147 -> 72 ticks per sample); the
- * outputs' sine / cosine are v_sin / v_cos of the word (the reference takes
- * cos / sin of the word's float phase: |difference| <= 5e-7); the
- * per-sample frequency, cos(2 phase) and I/Q products moved off the serial
- * W1, the old W4 (phases) and W2 (targets) became the four P waves. */
+ * Round 3: the chain's NCO constrain is fract(err * beta/2pi) * 2^32 in f32
+ * and its sine v_sin_f32 of the word in turns (tools/ubench/chainlat.hip:
+ * 147 -> 72 ticks per sample); the outputs' sine / cosine are v_sin /
+ * v_cos of the word (the reference takes cos / sin of the word's float
+ * phase: |difference| <= 5e-7); the per-sample frequency, cos(2 phase) and
+ * I/Q products moved off the serial W1.  The tile shape is a build switch
+ * (PLL_CH channels x PLL_T samples, 256 items): 32 x 8 halves the pipeline
+ * iterations (each costs a barrier and an LDS round trip) and runs 0.45 ms
+ * alone against 0.60 for 64 x 4, but occupies twice the CUs beside k_fe8,
+ * which the pipelined step pays for. */
+#ifndef PLL_CH
 #define PLL_CH 64
+#endif
+#ifndef PLL_T
+#define PLL_T 4
+#endif
 #define PLL_TS PLL_T
 #define PLL_WAVES 7
 #define PLL_W1 1
 #define PLL_W3 5
 #define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
 #define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
-static_assert(PLL_T == 4, "the P waves' items are quads (DPP quad_perm)");
+static_assert(PLL_CH * PLL_T == 256 && PLL_T % 4 == 0 && 64 % PLL_T == 0 && PLL_CH <= 64, "k_pll tile shape");
 
-struct PllShared {
+struct alignas(16) PllShared {
   float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-1 (P), k-2 (W1)
   float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k-1 loading, k-2 in W1)
   uint32_t s0t[2][PLL_CH][PLL_TS];         // W0 -> P: NCO words after each step
@@ -1120,13 +1128,18 @@ struct PllDlyStage {
   }
 };
 
-// the value of the previous sample of this lane's item quad: lane t of a
-// quad reads lane t - 1; t = 0 reads the quad's t = 3 of the PREVIOUS
-// iteration (lanes with t = 3 offer `prev`, the others `cur`)
-__device__ __forceinline__ float quad_prev(float cur, float prev, bool t3) {
-  const float x = t3 ? prev : cur;
-  // quad_perm [3, 0, 1, 2]: lane 0 <- 3, lane 1 <- 0, lane 2 <- 1, lane 3 <- 2
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x93, 0xF, 0xF, false));
+// the value of the previous sample of this lane's item: lane t of a row
+// reads lane t - 1; t = 0 reads the row's t = PLL_T - 1 of the PREVIOUS
+// iteration (lanes with t = PLL_T - 1 offer `prev`, the others `cur`)
+__device__ __forceinline__ float item_prev(float cur, float prev, bool tlast, int src_addr) {
+  const float x = tlast ? prev : cur;
+  if constexpr (PLL_T == 4) {
+    // quad_perm [3, 0, 1, 2]: lane 0 <- 3, lane 1 <- 0, lane 2 <- 1, lane 3 <- 2
+    (void)src_addr;
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x93, 0xF, 0xF, false));
+  } else {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_addr, __builtin_bit_cast(int, x)));
+  }
 }
 // sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
 // which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
@@ -1157,12 +1170,25 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
     pw_last = __builtin_amdgcn_s_memtime();                          \
     pw_wait += pw_last - t_;                                         \
   }
+  // sub-stage clocks of a wave's work (W1: loads | tile), a.dbg[16 + 4 w + i]
+  unsigned long long pw_sub[2] = {0, 0}, pw_s0 = pw_last;
+#define PLL_SUB(i)                                                   \
+  {                                                                  \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
+    pw_sub[i] += t_ - ((i) == 0 ? pw_last : pw_s0);                  \
+    pw_s0 = t_;                                                      \
+  }
 #define PLL_STAMP_OUT()                                              \
   if (a.dbg && (threadIdx.x & 63) == 0) {                            \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6), pw_work);              \
     atomicAdd(a.dbg + 2 * (threadIdx.x >> 6) + 1, pw_wait);          \
+    if ((threadIdx.x >> 6) < 4) {                                    \
+      atomicAdd(a.dbg + 16 + 4 * (threadIdx.x >> 6), pw_sub[0]);     \
+      atomicAdd(a.dbg + 17 + 4 * (threadIdx.x >> 6), pw_sub[1]);     \
+    }                                                                \
   }
 #else
+#define PLL_SUB(i)
 #define PLL_SYNC() PLL_BARRIER();
 #define PLL_STAMP_OUT()
 #endif
@@ -1206,10 +1232,15 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
   }
   __syncthreads();
 
+  // serial waves: lane = row (channel c0 + lane); lanes >= PLL_CH idle (they
+  // read row lrow and store nothing)
+  const int lrow = lane < PLL_CH ? lane : PLL_CH - 1;
   const int c = c0 + lane;
-  const bool act = c < a.C;
+  const bool act = lane < PLL_CH && c < a.C;
+  const bool own = lane < PLL_CH;
   // block-end values gathered for W0, after the loop (aliases the pilot tiles)
   float(*fin)[PLL_CH] = reinterpret_cast<float(*)[PLL_CH]>(&sh->inp[0][0][0]);
+  static_assert(6 * PLL_CH <= PLL_NINP * PLL_CH * PLL_TS, "fin inside the pilot tiles");
   if (wave == 0) {
     // ---------------- W0: the PLL feedback chain ----------------
     const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
@@ -1224,16 +1255,26 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
     }
     // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
     // iteration k), so its LDS latency overlaps the chain of the current tile
-    float4 pcur = *reinterpret_cast<const float4 *>(&sh->inp[0][lane][0]), pnxt = pcur;
+    float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
+#pragma unroll
+    for (int q = 0; q < PLL_T / 4; ++q) pnxt[q] = pcur[q] = *reinterpret_cast<const float4 *>(&sh->inp[0][lrow][4 * q]);
     for (int k = 0; k < PLL_NIT(NT); ++k) {
-      if (k + 1 < NT) pnxt = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lane][0]);
+      if (k + 1 < NT) {
+#pragma unroll
+        for (int q = 0; q < PLL_T / 4; ++q)
+          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lrow][4 * q]);
+      }
       // full tiles run without per-sample guards (a compile-time case)
       auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value;
-        const float pv[4] = {pcur.x, pcur.y, pcur.z, pcur.w};
-        uint32_t tw[4];
+        float pv[PLL_T];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          pv[4 * q] = pcur[q].x; pv[4 * q + 1] = pcur[q].y; pv[4 * q + 2] = pcur[q].z; pv[4 * q + 3] = pcur[q].w;
+        }
+        uint32_t tw[PLL_T];
+#pragma unroll
+        for (int t = 0; t < PLL_T; ++t) {
           if (FULL || t < cnt) {
             const float err = pv[t] * vcoQ; // pilot * sin(phase)
             const uint32_t ca = (uint32_t)(__builtin_amdgcn_fractf(err * ka) * 4294967296.0f);
@@ -1246,14 +1287,20 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
           }
           tw[t] = theta;
         }
-        *reinterpret_cast<uint4 *>(&sh->s0t[k & 1][lane][0]) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+        if (own) {
+#pragma unroll
+          for (int q = 0; q < PLL_T / 4; ++q)
+            *reinterpret_cast<uint4 *>(&sh->s0t[k & 1][lane][4 * q]) =
+                make_uint4(tw[4 * q], tw[4 * q + 1], tw[4 * q + 2], tw[4 * q + 3]);
+        }
       };
       if (k < NT) {
         const int cnt = min(PLL_T, n - k * PLL_T);
         if (cnt == PLL_T) tile(std::true_type{}, cnt);
         else tile(std::false_type{}, cnt);
       }
-      pcur = pnxt;
+#pragma unroll
+      for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = pnxt[q];
       PLL_SYNC()
     }
     PLL_SYNC() // W1 / W3 block-end values in sh->fin
@@ -1350,55 +1397,82 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
       if (k - 2 >= 0 && k - 2 < NT) std_.store(sh->dly[(k - 2) & 1], lane);
       stm.issue(rm4, a.mpx_stride, (k + 1) * PLL_T, lane);
       std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
+      PLL_SUB(0)
       const int kt = k - 2;
-      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
-        constexpr bool FULL = decltype(full_c)::value;
+      // full tiles: straight-line code, 16-B LDS reads and writes, four
+      // samples at a time (short live ranges); a ragged last tile (n not a
+      // multiple of PLL_T) takes the rolled per-sample loop below, kept
+      // structurally apart so that the compiler does not merge the two into
+      // one per-sample-branching body
+      auto tile_full = [&]() __attribute__((always_inline)) {
         const int sb = kt & 1;
-        const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[kt % PLL_NINP][lane][0]);
-        const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[sb][lane][0]);
-        const float4 ui = *reinterpret_cast<const float4 *>(&sh->su[sb][0][lane][0]);
-        const float4 uq = *reinterpret_cast<const float4 *>(&sh->su[sb][1][lane][0]);
-        const float pv[4] = {x.x, x.y, x.z, x.w}, mv[4] = {y.x, y.y, y.z, y.w};
-        const float uiv[4] = {ui.x, ui.y, ui.z, ui.w}, uqv[4] = {uq.x, uq.y, uq.z, uq.w};
-        float o_pbm[4], o_mm[4], o_mag2[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (FULL || t < cnt) {
-            pbm = (pbm * kS) + (fabsf(pv[t]) * kI);
-            mm = (mm * kS) + (fabsf(mv[t]) * kI);
-            pi_ = (pi_ * kS) + uiv[t];
-            pq = (pq * kS) + uqv[t];
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[kt % PLL_NINP][lrow][4 * q]);
+          const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[sb][lrow][4 * q]);
+          const float4 ui = *reinterpret_cast<const float4 *>(&sh->su[sb][0][lrow][4 * q]);
+          const float4 uq = *reinterpret_cast<const float4 *>(&sh->su[sb][1][lrow][4 * q]);
+          const float pv[4] = {x.x, x.y, x.z, x.w}, mv[4] = {y.x, y.y, y.z, y.w};
+          const float uiv[4] = {ui.x, ui.y, ui.z, ui.w}, uqv[4] = {uq.x, uq.y, uq.z, uq.w};
+          float o_pbm[4], o_mm[4], o_mag2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            pbm = (pbm * kS) + (fabsf(pv[u]) * kI);
+            mm = (mm * kS) + (fabsf(mv[u]) * kI);
+            pi_ = (pi_ * kS) + uiv[u];
+            pq = (pq * kS) + uqv[u];
+            o_pbm[u] = pbm;
+            o_mm[u] = mm;
+            o_mag2[u] = (pi_ * pi_) + (pq * pq);
           }
-          o_pbm[t] = pbm;
-          o_mm[t] = mm;
-          o_mag2[t] = (pi_ * pi_) + (pq * pq);
+          if (own) {
+            const int t = 4 * q;
+            *reinterpret_cast<float4 *>(&sh->sr[sb][F_PBM][lane][t]) = make_float4(o_pbm[0], o_pbm[1], o_pbm[2], o_pbm[3]);
+            *reinterpret_cast<float4 *>(&sh->sr[sb][F_MM][lane][t]) = make_float4(o_mm[0], o_mm[1], o_mm[2], o_mm[3]);
+            *reinterpret_cast<float4 *>(&sh->sr[sb][F_MAG2][lane][t]) = make_float4(o_mag2[0], o_mag2[1], o_mag2[2], o_mag2[3]);
+          }
         }
-        *reinterpret_cast<float4 *>(&sh->sr[sb][F_PBM][lane][0]) = make_float4(o_pbm[0], o_pbm[1], o_pbm[2], o_pbm[3]);
-        *reinterpret_cast<float4 *>(&sh->sr[sb][F_MM][lane][0]) = make_float4(o_mm[0], o_mm[1], o_mm[2], o_mm[3]);
-        *reinterpret_cast<float4 *>(&sh->sr[sb][F_MAG2][lane][0]) = make_float4(o_mag2[0], o_mag2[1], o_mag2[2], o_mag2[3]);
       };
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
-        if (cnt == PLL_T) tile(std::true_type{}, cnt);
-        else tile(std::false_type{}, cnt);
+        if (cnt == PLL_T) {
+          tile_full();
+        } else {
+          const int sb = kt & 1;
+#pragma unroll 1
+          for (int t = 0; t < cnt; ++t) {
+            pbm = (pbm * kS) + (fabsf(sh->inp[kt % PLL_NINP][lrow][t]) * kI);
+            mm = (mm * kS) + (fabsf(sh->inm[sb][lrow][t]) * kI);
+            pi_ = (pi_ * kS) + sh->su[sb][0][lrow][t];
+            pq = (pq * kS) + sh->su[sb][1][lrow][t];
+            if (own) {
+              sh->sr[sb][F_PBM][lane][t] = pbm;
+              sh->sr[sb][F_MM][lane][t] = mm;
+              sh->sr[sb][F_MAG2][lane][t] = (pi_ * pi_) + (pq * pq);
+            }
+          }
+        }
       }
+      PLL_SUB(1)
       PLL_SYNC()
     };
     for (int k = 0; k < PLL_NIT(NT); k += 2) {
       iter(k, std::integral_constant<int, 0>{});
       if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
     }
-    fin[0][lane] = pbm;
-    fin[1][lane] = mm;
-    fin[2][lane] = pi_;
-    fin[3][lane] = pq;
+    if (own) {
+      fin[0][lane] = pbm;
+      fin[1][lane] = mm;
+      fin[2][lane] = pi_;
+      fin[3][lane] = pq;
+    }
     PLL_SYNC()
     PLL_STAMP_OUT()
   } else if (wave == PLL_W3) {
-    // ---------------- W3: blend recursion + outputs; loader ----------------
+    // ---------------- W3: blend recursion + outputs; pilot loader ----------------
     const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
     float blend = s0.blend;
-    const int mode = sh->s2_flags[lane] >> 8;
+    const int mode = sh->s2_flags[lrow] >> 8;
     const float attack = D->blend_attack[mode], release = D->blend_release[mode];
     // pilot tiles staged in registers TWO iterations ahead, across the
     // barriers: iteration k stores tile k+2 (W0 reads it ahead at k+1), then
@@ -1430,46 +1504,41 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
       }
       stp.issue(rp, a.pilot_stride, (k + 4) * PLL_T, lane);
       const int kt = k - 4;
-      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
-        constexpr bool FULL = decltype(full_c)::value;
+      // full tiles straight-line, a ragged last tile per sample (as W1)
+      auto tile_full = [&]() __attribute__((always_inline)) {
         const int sb = kt & 1;
-        const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lane][0]);
-        const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lane][0]);
-        const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lane][0]);
-        const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lane][0]);
-        const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
-        const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
-        float ov[2][4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (FULL || t < cnt) {
+        for (int q = 0; q < PLL_T / 4; ++q) {
+          const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lrow][4 * q]);
+          const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lrow][4 * q]);
+          const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lrow][4 * q]);
+          const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lrow][4 * q]);
+          const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
+          const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
+          float ov[2][4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
             // blend += (tgt - blend) * (tgt > blend ? attack : release),
             // select-free: exactly one of the two products is nonzero and
             // adding the other (+0 / -0) leaves the sum unchanged
-            const float d = tga[t] - blend;
+            const float d = tga[u] - blend;
             blend = (blend + fmaxf(d, 0.0f) * attack) + fminf(d, 0.0f) * release;
-            ov[0][t] = moa[t] + (dla[t] * blend);
-            ov[1][t] = moa[t] + (dra[t] * blend);
-          } else {
-            ov[0][t] = ov[1][t] = 0.0f;
+            ov[0][u] = moa[u] + (dla[u] * blend);
+            ov[1][u] = moa[u] + (dra[u] * blend);
           }
-        }
-        if (act) {
-          // octet tiles (lr_tile_idx): the 8 lanes of a channel octet fill
-          // one 128-B line, a store instruction writes 8 whole lines
-          const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T, a.lr_stride)
-                                       : (size_t)c * a.lr_stride + kt * PLL_T;
-          float *ol = a.lraw + ob;
-          float *orr = a.rraw + ob;
-          if (FULL && ((((uintptr_t)ol) | ((uintptr_t)orr)) & 15) == 0) {
-            *reinterpret_cast<float4 *>(ol) = make_float4(ov[0][0], ov[0][1], ov[0][2], ov[0][3]);
-            *reinterpret_cast<float4 *>(orr) = make_float4(ov[1][0], ov[1][1], ov[1][2], ov[1][3]);
-          } else {
+          if (act) {
+            // octet tiles (lr_tile_idx): the 8 lanes of a channel octet fill
+            // one 128-B line per 4 samples, a store instruction writes 8 whole lines
+            const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T + 4 * q, a.lr_stride)
+                                         : (size_t)c * a.lr_stride + kt * PLL_T + 4 * q;
+            if (a.lr_tiled) {
+              *reinterpret_cast<float4 *>(a.lraw + ob) = make_float4(ov[0][0], ov[0][1], ov[0][2], ov[0][3]);
+              *reinterpret_cast<float4 *>(a.rraw + ob) = make_float4(ov[1][0], ov[1][1], ov[1][2], ov[1][3]);
+            } else {
 #pragma unroll
-            for (int t = 0; t < PLL_T; ++t) {
-              if (t < cnt) {
-                ol[t] = ov[0][t];
-                orr[t] = ov[1][t];
+              for (int u = 0; u < 4; ++u) {
+                a.lraw[ob + u] = ov[0][u];
+                a.rraw[ob + u] = ov[1][u];
               }
             }
           }
@@ -1477,23 +1546,44 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
       };
       if (kt >= 0 && kt < NT) {
         const int cnt = min(PLL_T, n - kt * PLL_T);
-        if (cnt == PLL_T) tile(std::true_type{}, cnt);
-        else tile(std::false_type{}, cnt);
+        if (cnt == PLL_T) {
+          tile_full();
+        } else {
+          const int sb = kt & 1;
+#pragma unroll 1
+          for (int t = 0; t < cnt; ++t) {
+            const float d = sh->s2[sb][F_TGT][lrow][t] - blend;
+            blend = (blend + fmaxf(d, 0.0f) * attack) + fminf(d, 0.0f) * release;
+            const float mo = sh->s2[sb][F_MONO][lrow][t];
+            const float ol = mo + (sh->s2[sb][F_DL][lrow][t] * blend);
+            const float orr = mo + (sh->s2[sb][F_DR][lrow][t] * blend);
+            if (act) {
+              const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T + t, a.lr_stride)
+                                           : (size_t)c * a.lr_stride + kt * PLL_T + t;
+              a.lraw[ob] = ol;
+              a.rraw[ob] = orr;
+            }
+          }
+        }
       }
+      PLL_SUB(1)
       PLL_SYNC()
     };
     for (int k = 0; k < PLL_NIT(NT); k += 2) {
       iter(k, std::integral_constant<int, 0>{});
       if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
     }
-    fin[5][lane] = blend;
+    if (own) fin[5][lane] = blend;
     PLL_SYNC()
     PLL_STAMP_OUT()
   } else {
     // ---------------- P0..P3: the time-parallel stages ----------------
     const int pw = (wave == 2) ? 0 : (wave == 3) ? 1 : (wave == 4) ? 2 : 3;
-    const int row = (lane >> 2) + 16 * pw, tt = lane & 3;
-    const bool t3 = tt == 3;
+    const int item = lane + 64 * pw;
+    const int row = item / PLL_T, tt = item % PLL_T;
+    const bool tlast = tt == PLL_T - 1;
+    // ds_bpermute address of the previous sample's lane (t = 0: the row's last)
+    const int src_addr = 4 * ((tt == 0) ? lane + PLL_T - 1 : lane - 1);
     const int ch = c0 + row;
     const float nominal = D->nominal, fsf = (float)D->fs;
     const float pmin = D->pll_min, pmax = D->pll_max;
@@ -1530,7 +1620,8 @@ __global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))
       word_sincos(th, &sN, &cN);
       const float ph = d_nco_phase(th);
       // vco of this sample = sin / cos of the previous sample's phase
-      const float sP = quad_prev(sN, prev_s, t3), cP = quad_prev(cN, prev_c, t3), phP = quad_prev(ph, prev_ph, t3);
+      const float sP = item_prev(sN, prev_s, tlast, src_addr), cP = item_prev(cN, prev_c, tlast, src_addr);
+      const float phP = item_prev(ph, prev_ph, tlast, src_addr);
       const float uI = (pilot * cP) * kI, uQ = (pilot * sP) * kI;
       const float fr = __builtin_amdgcn_fmed3f(d_unwrap(ph - phP), pmin, pmax); // clamp(dphi, min, max)
       const float c2 = (cN * cN) - (sN * sN);
@@ -2754,10 +2845,13 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * ~58 KB of LDS per workgroup: two workgroups (8 waves) per CU leave room
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
-__host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
-#ifndef FMX_DEC_KS_UNROLL
-#define FMX_DEC_KS_UNROLL 7
+#ifndef FMX_DEC_I8
+#define FMX_DEC_I8 0
 #endif
+#ifndef FMX_DEC_UNROLL
+#define FMX_DEC_UNROLL 1
+#endif
+__host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
 
@@ -2812,7 +2906,10 @@ template <int M, int TPP> struct Fe8Layout {
 // every K step starts on an 8-sample boundary.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
 template <int M, int TPP>
-__global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
+#ifndef FE8_MINB
+#define FE8_MINB 1
+#endif
+__global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP>;
   constexpr int L = LY::L;
@@ -2841,14 +2938,22 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
 #ifdef FMX_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = (a.dbg && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0;
-#define FE_STAMP(k)                                              \
+#define FE_STAMP_RAW(k)                                          \
   if (a.dbg && threadIdx.x == 0) {                               \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
     st_acc[k] += t_ - st_last;                                   \
     st_last = t_;                                                \
   }
+#ifdef FMX_STAMPS_DECIM // decimator split: 0 staging, 1 RF sums, 2 MFMA loop, 3 dc + IQ FIR + discriminator
+#define FE_STAMP(k) FE_STAMP_RAW(((k) == 1 || (k) == 2) ? 3 : (k))
+#define FE_STAMP_D(k) FE_STAMP_RAW(k)
+#else
+#define FE_STAMP(k) FE_STAMP_RAW(k)
+#define FE_STAMP_D(k)
+#endif
 #else
 #define FE_STAMP(k)
+#define FE_STAMP_D(k)
 #endif
   SigAcc sig;
   const int c = blockIdx.x;
@@ -2859,6 +2964,30 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
   const FmxDesign *__restrict__ D = a.des;
   const int n = a.n;
   const FmxChanParam par = a.par[c];
+  // u8 IQ chunks arrive by LDS-DMA (the first one issued after the setup
+  // loads below: issued before them it costs 26 VGPRs, and vmcnt would make
+  // the setup loads wait for it) (16 B per lane, 1-KiB pieces, wave w
+  // moving pieces w, w+4, ...): the chunk [n0p*M - L, (n0p + FE8_T)*M) lands
+  // in raw while the previous chunk's pilot FIR and RDS resampler run.
+  // Bytes before the row (the first chunk's halo) read 0 (out of range) and
+  // are replaced by the carried decimator history.
+  const __amdgpu_buffer_rsrc_t riq = make_rsrc(a.iq + (size_t)c * a.iq_stride, (uint32_t)(2L * n * M));
+  auto dma_chunk = [&](int n0p, auto p_lo_c, auto p_hi_c) __attribute__((always_inline)) {
+    constexpr int P_LO = decltype(p_lo_c)::value, P_HI = decltype(p_hi_c)::value;
+    uint32_t off = (uint32_t)(2 * n0p * M - LY::HB + 1024 * (P_LO + wave)) + 16u * (uint32_t)lane;
+#pragma unroll
+    for (int j = 0; j < (P_HI - P_LO + 3) / 4; ++j) {
+      const int pc = P_LO + wave + 4 * j;
+      if (pc < P_HI)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, 0);
+      off += 4096u;
+      asm volatile("" : "+v"(off));
+    }
+  };
+  using PAll0 = std::integral_constant<int, 0>;
+  using PEarly = std::integral_constant<int, LY::NPC_EARLY>;
+  using PAll = std::integral_constant<int, LY::NPC>;
   const int iqL = D->iq_len[par.iqsel];
   const float iqscale = D->iq_scale[par.iqsel];
   const bool pilot = a.pilot_out != nullptr;
@@ -2926,30 +3055,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       rsb[pr][m] = f32x2{h0, h1};
     }
   }
-  int e_pos = 0;
-  // u8 IQ chunks arrive by LDS-DMA (16 B per lane, 1-KiB pieces, wave w
-  // moving pieces w, w+4, ...): the chunk [n0p*M - L, (n0p + FE8_T)*M) lands
-  // in raw while the previous chunk's pilot FIR and RDS resampler run.
-  // Bytes before the row (the first chunk's halo) read 0 (out of range) and
-  // are replaced by the carried decimator history.
-  const __amdgpu_buffer_rsrc_t riq = make_rsrc(a.iq + (size_t)c * a.iq_stride, (uint32_t)(2L * n * M));
-  auto dma_chunk = [&](int n0p, auto p_lo_c, auto p_hi_c) __attribute__((always_inline)) {
-    constexpr int P_LO = decltype(p_lo_c)::value, P_HI = decltype(p_hi_c)::value;
-    uint32_t off = (uint32_t)(2 * n0p * M - LY::HB + 1024 * (P_LO + wave)) + 16u * (uint32_t)lane;
-#pragma unroll
-    for (int j = 0; j < (P_HI - P_LO + 3) / 4; ++j) {
-      const int pc = P_LO + wave + 4 * j;
-      if (pc < P_HI)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, 0);
-      off += 4096u;
-      asm volatile("" : "+v"(off));
-    }
-  };
-  using PAll0 = std::integral_constant<int, 0>;
-  using PEarly = std::integral_constant<int, LY::NPC_EARLY>;
-  using PAll = std::integral_constant<int, LY::NPC>;
   dma_chunk(0, PAll0{}, PAll{});
+  int e_pos = 0;
 
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
     if (rds && tid == 0) sh->e_end = e_pos;
@@ -2976,8 +3083,87 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         }
       }
     }
+    FE_STAMP_D(1)
     float2 xv[8]; // decimator outputs of this thread
     {
+#if FMX_DEC_I8
+      // Decimator as v_mfma_i32_16x16x64_i8 tiles.  Output o = 16 B + r of
+      // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
+      // [M r + 1, M r + L], with tap L + M r - t: per block, Y[r] = sum_t
+      // T[r][t] X[t] with T[r][t] = q[t - M r] -- one 16 x 16 tile is 16
+      // outputs (rows, A = taps) of 16 blocks (columns, B = bytes), K = the
+      // block's 15 M + L + 1 input samples in steps of 64.  The bytes enter
+      // as they are (b ^ 0x80 is b - 128 as int8: one v_perm per 4 samples
+      // of a component and one xor per word, no conversion), the taps as the
+      // three int8 digits of q = tap * 2^s (FmxDesign::dec_frag8, 24
+      // significant bits); per component three i32 accumulators hold EXACT
+      // sums, combined once per output.  Each wave runs two tiles (512
+      // outputs); the C layout gives each lane 4 consecutive outputs, which
+      // reach the 8-per-thread layout of the stages below through LDS.
+      typedef int i32x4_t __attribute__((ext_vector_type(4)));
+      constexpr int KS8 = (15 * M + L + 1 + 63) / 64;
+      static_assert(KS8 <= FMX_DEC_KS8_MAX, "decimator K steps");
+      static_assert(32 * M * 111 + 96 + 512 * M + 128 * (KS8 - 1) + 32 <= LY::RAW_ALLOC, "decimator reads inside raw");
+      const int col = lane & 15, g = lane >> 4;
+      // A fragments (16 B per lane and digit) from the design, one K step ahead
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag8[0][0][0][0]) + lane;
+      const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 32 * g;
+      // the two tiles one after the other (24 accumulator VGPRs live, not 48);
+      // each tile's outputs are combined to f32 right away: 256 mid + lo fits
+      // int32 (|acc| <= 128 * 280 * 128), 65536 hi is exact in f32
+      const float dc = D->dec_dc8, sc = D->dec_scale8;
+      float yr[2][4], yi[2][4];
+#pragma unroll 1
+      for (int u = 0; u < 2; ++u) {
+        i32x4_t acc[2][3]; // [I, Q][hi, mid, lo digit]
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int dg = 0; dg < 3; ++dg) acc[q][dg] = i32x4_t{0, 0, 0, 0};
+        u32x4 fh = fa[0], fm = fa[64], fl = fa[128];
+        const unsigned char *ru = rb + 512 * M * u;
+#pragma unroll FMX_DEC_UNROLL
+        for (int ks = 0; ks < KS8; ++ks) {
+          const i32x4_t ah = __builtin_bit_cast(i32x4_t, fh), am = __builtin_bit_cast(i32x4_t, fm),
+                        al = __builtin_bit_cast(i32x4_t, fl);
+          if (ks + 1 < KS8) {
+            fh = fa[192 * (ks + 1)];
+            fm = fa[192 * (ks + 1) + 64];
+            fl = fa[192 * (ks + 1) + 128];
+          }
+          // 16 samples (32 bytes I0 Q0 I1 Q1 ...) of this lane's column
+          const u32x4 w0 = *reinterpret_cast<const u32x4 *>(ru + 128 * ks);
+          const u32x4 w1 = *reinterpret_cast<const u32x4 *>(ru + 128 * ks + 16);
+          const uint32_t w[8] = {w0.x ^ 0x80808080u, w0.y ^ 0x80808080u, w0.z ^ 0x80808080u, w0.w ^ 0x80808080u,
+                                 w1.x ^ 0x80808080u, w1.y ^ 0x80808080u, w1.z ^ 0x80808080u, w1.w ^ 0x80808080u};
+          i32x4_t bi, bq;
+#pragma unroll
+          for (int d4 = 0; d4 < 4; ++d4) {
+            bi[d4] = (int)__builtin_amdgcn_perm(w[2 * d4 + 1], w[2 * d4], 0x06040200u);
+            bq[d4] = (int)__builtin_amdgcn_perm(w[2 * d4 + 1], w[2 * d4], 0x07050301u);
+          }
+          acc[0][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bi, acc[0][0], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bq, acc[1][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(am, bi, acc[0][1], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(am, bq, acc[1][1], 0, 0, 0);
+          acc[0][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bi, acc[0][2], 0, 0, 0);
+          acc[1][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bq, acc[1][2], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float vi = (float)acc[0][0][i] * 65536.0f + (float)(acc[0][1][i] * 256 + acc[0][2][i]);
+          const float vq = (float)acc[1][0][i] * 65536.0f + (float)(acc[1][1][i] * 256 + acc[1][2][i]);
+          // u is uniform: select, not a dynamic register index
+          if (u == 0) {
+            yr[0][i] = (vi - dc) * sc;
+            yi[0][i] = (vq - dc) * sc;
+          } else {
+            yr[1][i] = (vi - dc) * sc;
+            yi[1][i] = (vq - dc) * sc;
+          }
+        }
+      }
+#else
       // Decimator as v_mfma_f32_16x16x32_f16 tiles.  Output o = 16 B + r of
       // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
       // [M r + 1, M r + L], with tap L + M r - t: per block, Y[r] = sum_t
@@ -2992,7 +3178,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
       typedef float f32x4_t __attribute__((ext_vector_type(4)));
       constexpr int KS = (15 * M + L + 1 + 31) / 32;
-      static_assert(32 * KS - 1 - FMX_DQ_MIN + 2 < FMX_DQ_N && -15 * M >= FMX_DQ_MIN && KS <= FMX_DEC_KS_MAX, "tap table range");
+      static_assert(KS <= FMX_DEC_KS_MAX, "decimator K steps");
       const int col = lane & 15, g = lane >> 4;
       const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0 (even)
       // A fragments from the design (FmxDesign::dec_frag, 16-B per lane, one
@@ -3010,7 +3196,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         return __builtin_bit_cast(f16x2_t, __builtin_amdgcn_perm(0x64646464u, w, sel)) -
                f16x2_t{(_Float16)1152.0f, (_Float16)1152.0f};
       };
-#pragma unroll FMX_DEC_KS_UNROLL
+#pragma unroll 7
       for (int ks = 0; ks < KS; ++ks) {
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, fh), alo = __builtin_bit_cast(f16x8_t, fl);
         if (ks + 1 < KS) {
@@ -3032,8 +3218,19 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
           acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bq, acc[u][1], 0, 0, 0);
         }
       }
+#endif
+      FE_STAMP_D(2)
       __syncthreads(); // every wave is past raw: its outputs go to the (aliased) staging area
       float4 *stg = reinterpret_cast<float4 *>(smem + LY::STG);
+#if FMX_DEC_I8
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
+        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g;
+        stg[o / 2] = make_float4(yr[u][0], yi[u][0], yr[u][1], yi[u][1]);
+        stg[o / 2 + 1] = make_float4(yr[u][2], yi[u][2], yr[u][3], yi[u][3]);
+      }
+#else
       const float dc = D->dec_dc16, sc = D->dec_scale16;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -3048,6 +3245,7 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
         stg[o / 2] = make_float4(yr[0], yi[0], yr[1], yi[1]);
         stg[o / 2 + 1] = make_float4(yr[2], yi[2], yr[3], yi[3]);
       }
+#endif
       __syncthreads();
       int myclip = 0;
 #pragma unroll
@@ -3233,6 +3431,16 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
     }
     __syncthreads(); // xin / yb are dead: the next chunk may land in raw (below uc)
+    // RDS schedule entries of this chunk, fetched before the early DMA and the
+    // resampler's window copy
+    FmxSched en[8];
+    if (rds) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e_pos + tid + 256 * k;
+        en[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
+      }
+    }
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
     if (rds) { // unpadded copy for the RDS resampler: its own window history first
 #pragma unroll
@@ -3243,15 +3451,54 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
     }
     FE_STAMP(3)
-    // RDS schedule entries of this chunk, fetched before the pilot FIR
-    FmxSched en[8];
+    // ================= RDS resampler 240k -> 171k =================
     if (rds) {
+      __syncthreads(); // uc complete
+      int last = -1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int e = e_pos + tid + 256 * k;
-        en[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
+        if (e < sched_n && (en[k].packed & 0xFFFF) < n0 + FE8_T) {
+          const int i = (en[k].packed & 0xFFFF) - n0;
+          const int b = (en[k].packed >> 16) & 0xFF;
+          const bool boundary = (en[k].packed >> 24) & 1;
+          // the window's oldest sample (one earlier at a boundary), as uc index
+          // LDS addresses kept opaque: the reads then use the instruction's
+          // offset field (m) instead of one address add per read pair
+          uint32_t xa = (uint32_t)(uintptr_t)(lds_f32 *)(uc + 32 + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1));
+          uint32_t ha = (uint32_t)(uintptr_t)(lds_f32x2 *)rsb[boundary ? FMX_NPFB : b];
+          asm volatile("" : "+v"(xa), "+v"(ha));
+          const lds_f32 *xu = (const lds_f32 *)(uintptr_t)xa;
+          const lds_f32x2 *hk = (const lds_f32x2 *)(uintptr_t)ha;
+          // two fused multiply-add chains, oldest sample first (the
+          // reference's branch dot products, each product fused into its
+          // sum: one rounding per tap instead of two, within the PCM / MPX
+          // bars of tests/test_gpu_parity.py).  Scalar v_fma_f32 as asm: the
+          // packed-FP32 form (v_pk_mul / v_pk_add, which the vectorizer
+          // makes of the pair) returned wrong upper-32-lane results,
+          // nondeterministically, with two k_fe8 workgroups per CU issuing
+          // MFMAs
+          float y0 = 0.0f, y1 = 0.0f;
+#pragma unroll
+          for (int m = 0; m < LY::RS_M; ++m) {
+            const float v = xu[m];
+            const f32x2 hm = hk[m];
+            asm("v_fma_f32 %0, %1, %2, %0" : "+v"(y0) : "v"(hm.x), "v"(v));
+            asm("v_fma_f32 %0, %1, %2, %0" : "+v"(y1) : "v"(hm.y), "v"(v));
+          }
+          const f32x2 y = {y0, y1};
+          const float w0f = (1.0f - en[k].mu) * y.x;
+          const float w1f = en[k].mu * y.y;
+          a.rds_out[(size_t)c * a.rds_stride + e] = w0f + w1f;
+          last = e;
+        }
       }
+      if (last >= 0) atomicMax(&sh->e_end, last + 1);
     }
+    __syncthreads(); // uc is dead: the rest of the next chunk may land (behind the pilot FIR)
+    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
+    if (rds) e_pos = sh->e_end;
+    FE_STAMP(5)
     // ================= 19 kHz pilot band-pass =================
     if (pilot) {
       // v_mfma_f32_16x16x32_f16 tiles as the decimator's: 16 outputs (rows,
@@ -3296,54 +3543,6 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
       }
     }
     FE_STAMP(4)
-    // ================= RDS resampler 240k -> 171k =================
-    if (rds) {
-      __syncthreads(); // uc complete
-      int last = -1;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = e_pos + tid + 256 * k;
-        if (e < sched_n && (en[k].packed & 0xFFFF) < n0 + FE8_T) {
-          const int i = (en[k].packed & 0xFFFF) - n0;
-          const int b = (en[k].packed >> 16) & 0xFF;
-          const bool boundary = (en[k].packed >> 24) & 1;
-          // the window's oldest sample (one earlier at a boundary), as uc index
-          // LDS addresses kept opaque: the reads then use the instruction's
-          // offset field (m) instead of one address add per read pair
-          uint32_t xa = (uint32_t)(uintptr_t)(lds_f32 *)(uc + 32 + (boundary ? i - 1 : i) - (FMX_RDS_RS_SUB - 1));
-          uint32_t ha = (uint32_t)(uintptr_t)(lds_f32x2 *)rsb[boundary ? FMX_NPFB : b];
-          asm volatile("" : "+v"(xa), "+v"(ha));
-          const lds_f32 *xu = (const lds_f32 *)(uintptr_t)xa;
-          const lds_f32x2 *hk = (const lds_f32x2 *)(uintptr_t)ha;
-          // scalar multiplies and adds (same rounding): the packed-FP32 form
-          // (v_pk_mul / v_pk_add) returned wrong upper-32-lane results,
-          // nondeterministically, with two k_fe8 workgroups per CU issuing
-          // MFMAs (tools/gpu_determinism.py with FMX_DIAG_RDS_DUMP=1)
-          float y0 = 0.0f, y1 = 0.0f;
-#pragma unroll
-          for (int m = 0; m < LY::RS_M; ++m) {
-            const float v = xu[m];
-            const f32x2 hm = hk[m];
-            // as asm so that the vectorizer cannot pair them into v_pk_* again
-            float p0, p1;
-            asm("v_mul_f32 %0, %1, %2" : "=v"(p0) : "v"(hm.x), "v"(v));
-            asm("v_mul_f32 %0, %1, %2" : "=v"(p1) : "v"(hm.y), "v"(v));
-            asm("v_add_f32 %0, %1, %2" : "=v"(y0) : "v"(y0), "v"(p0));
-            asm("v_add_f32 %0, %1, %2" : "=v"(y1) : "v"(y1), "v"(p1));
-          }
-          const f32x2 y = {y0, y1};
-          const float w0f = (1.0f - en[k].mu) * y.x;
-          const float w1f = en[k].mu * y.y;
-          a.rds_out[(size_t)c * a.rds_stride + e] = w0f + w1f;
-          last = e;
-        }
-      }
-      if (last >= 0) atomicMax(&sh->e_end, last + 1);
-    }
-    __syncthreads(); // uc is dead: the rest of the next chunk may land
-    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
-    if (rds) e_pos = sh->e_end;
-    FE_STAMP(5)
     // ================= carry halos to the next chunk =================
     {
       // the chunk's last FMX_HIST samples become the f16 images' history;
@@ -3405,6 +3604,8 @@ __global__ __launch_bounds__(256) void k_fe8(FeArgs a) {
     for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, st_acc[k]);
 #endif
 #undef FE_STAMP
+#undef FE_STAMP_D
+#undef FE_STAMP_RAW
   if (want_sig) fe_signal_sums(a, sig, sgp, c, lane, wave, tid);
 }
 

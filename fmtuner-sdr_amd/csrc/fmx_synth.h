@@ -43,6 +43,7 @@ typedef struct {
   float a_l, a_r;
   float ph_l, ph_r; /* initial tone phases, rad */
   int64_t rds_off;  /* RDS bit-clock offset in samples (stations are not synchronised) */
+  float amp;        /* carrier amplitude (cfg amplitude, spread over level_spread_db) */
 } fmx_synth_chan;
 
 #ifdef __cplusplus
@@ -82,6 +83,9 @@ FMX_HD fmx_synth_chan fmx_synth_channel(const fmx_synth_cfg *cfg, uint32_t ch) {
     c.ph_r = 6.2831853f * fmx_u01(h3 >> 29);
   }
   c.rds_off = (int64_t)(fmx_splitmix64(s ^ 4) % (uint64_t)(2 * cfg->iq_rate));
+  c.amp = cfg->amplitude;
+  if (cfg->level_spread_db > 0.0f)
+    c.amp = cfg->amplitude * powf(10.0f, -0.05f * cfg->level_spread_db * fmx_u01(fmx_splitmix64(s ^ 5)));
   return c;
 }
 
@@ -162,7 +166,7 @@ FMX_HD void fmx_synth_sample(const fmx_synth_cfg *cfg, uint32_t ch, const fmx_sy
   float si, co;
   si = sinf(phi);
   co = cosf(phi);
-  float i = cfg->amplitude * co, q = cfg->amplitude * si;
+  float i = c->amp * co, q = c->amp * si;
   if (cfg->noise_std > 0.0f) {
     uint64_t key = ((uint64_t)(cfg->seed_base + ch) << 40) ^ ((uint64_t)n << 1);
     i += cfg->noise_std * fmx_gauss(key);

@@ -60,7 +60,7 @@ class SynthConfig(C.Structure):
     _fields_ = [("iq_rate", C.c_int), ("kind", C.c_int), ("amplitude", C.c_float),
                 ("noise_std", C.c_float), ("seed_base", C.c_uint32),
                 ("max_offset_hz", C.c_int), ("rds_level", C.c_float),
-                ("n_bits", C.c_int)]
+                ("n_bits", C.c_int), ("level_spread_db", C.c_float)]
 
 
 _lib = None
@@ -129,9 +129,9 @@ def make_config(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=4096
 
 
 def make_synth(iq_rate=2_400_000, kind=2, amplitude=0.8, noise_std=0.0,
-               seed_base=0xF00D, max_offset_hz=5000, rds_level=0.05, n_bits=4096):
+               seed_base=0xF00D, max_offset_hz=5000, rds_level=0.05, n_bits=4096, level_spread_db=0.0):
     return SynthConfig(iq_rate, kind, amplitude, noise_std, seed_base, max_offset_hz,
-                       rds_level, n_bits)
+                       rds_level, n_bits, level_spread_db)
 
 
 class FmxError(RuntimeError):

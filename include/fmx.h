@@ -226,6 +226,9 @@ typedef struct {
   int max_offset_hz;
   float rds_level; /* 0.05                                                  */
   int n_bits;      /* RDS bit-table length per channel                      */
+  float level_spread_db; /* per-channel carrier level: amplitude * 10^(-u d / 20),
+                            u in (0, 1] from the channel seed, d this value
+                            (0 = every channel at `amplitude`)              */
 } fmx_synth_config;
 /* RDS test pattern: encoded (differential) bits [n_ch][n_bits] and, if
  * h_groups != NULL, the transmitted groups [n_ch][n_bits/104][4]. */

@@ -246,24 +246,23 @@ def test_unlocked_pilot_level_is_chaotic(fmx, oracle):
 
 @pytest.mark.parametrize("rates", CONFIGS)
 def test_mfma_decimator_tap_tables(fmx, rates):
-    """k_fe8's MFMA decimator takes the decimator taps as f16 hi + lo pairs
-    (scaled by 2^16, FmxDesign::dec_q16): both table copies give the float
-    taps back to 22 significant bits."""
+    """k_fe8's i8 MFMA decimator takes the decimator taps as integers (x 2^s,
+    24 significant bits) in three balanced int8 digits, laid out as per-lane
+    A fragments (FmxDesign::dec_frag8): row 0 and every row r = 1..15
+    (shifted by M r) give the float taps back to 2^-21 of the largest."""
     if rates["iq_rate"] == rates["dsp_rate"]:
         pytest.skip("no decimator")
     cfg = fmx.make_config(**rates)
     raw = fmx.design_taps(cfg, 0).astype(np.float64)
-    q = fmx.design_taps(cfg, 9).astype(np.float64)
-    assert q.size == 2 * raw.size
     scale = np.abs(raw).max()
-    for cp in range(2):
-        err = np.abs(q[cp * raw.size:(cp + 1) * raw.size] - raw)
-        # the taps pass through float32 (/127.5, then *127.5 here): a few ulp of the largest
-        assert err.max() <= scale * 2.0 ** -21, (cp, err.max() / scale)
-    # the per-lane A fragments k_fe8 reads (FmxDesign::dec_frag)
     fr = fmx.design_taps(cfg, 13).astype(np.float64)
     assert fr.size == raw.size
+    # the taps pass through float32 (/127.5, then *127.5 here): a few ulp of the largest
     assert np.abs(fr - raw).max() <= scale * 2.0 ** -21
+    rows = fmx.design_taps(cfg, 9).astype(np.float64)
+    assert rows.size == 16 * raw.size
+    for r in range(16):
+        assert np.array_equal(rows[r * raw.size:(r + 1) * raw.size], fr), r
 
 
 @pytest.mark.parametrize("rates", CONFIGS)

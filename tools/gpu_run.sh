@@ -59,10 +59,23 @@ for step in "$@"; do
       FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_diag.so timeout -k 10 120 python3 tools/fe_stamps.py > $O/stamps_$TAG.txt 2>&1 && \
       FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_diag.so FMX_SERIAL=1 timeout -k 10 120 python3 tools/fe_stamps.py > $O/stamps_serial_$TAG.txt 2>&1; rc=$?
       grep -v amdgpu.ids $O/stamps_$TAG.txt; echo "-- serial"; grep -v amdgpu.ids $O/stamps_serial_$TAG.txt ;;
+    stamps:*)
+      # stage clocks of another diagnostics library: stamps:diag_dec (decimator split), stamps:diag_t8
+      V=${step#stamps:}
+      EX=""
+      case $V in *dec*) EX="DECIM=1" ;; esac
+      case $V in *t8*) EX="$EX PLL_CH=32" ;; esac
+      env $EX FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_$V.so timeout -k 10 120 python3 tools/fe_stamps.py > $O/stamps_${V}_$TAG.txt 2>&1 && \
+      env $EX FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_$V.so FMX_SERIAL=1 timeout -k 10 120 python3 tools/fe_stamps.py > $O/stamps_serial_${V}_$TAG.txt 2>&1; rc=$?
+      grep -v amdgpu.ids $O/stamps_${V}_$TAG.txt; echo "-- serial"; grep -v amdgpu.ids $O/stamps_serial_${V}_$TAG.txt ;;
     iso)
       # isolated per-kernel times (diagnostics library, one stream)
       FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_diag.so FMX_SERIAL=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/iso_$TAG.json 2> $O/iso_$TAG.err; rc=$?
       python3 -c "import json,sys; r=json.load(open('$O/iso_$TAG.json')); print('isolated', r['ms_per_step'], {k: v['avg_ms'] for k, v in r['kernels'].items()})" ;;
+    ab:*)
+      # interleaved A/B of library variants: ab:cur,t16,t4 (tools/gpu_abn.sh, 3 reps x 20 steps)
+      timeout -k 10 900 bash tools/gpu_abn.sh 3 20 $(echo ${step#ab:} | tr ',' ' ') > $O/ab_$TAG.log 2>&1; rc=$?
+      tail -6 $O/ab_$TAG.log ;;
     sweep)
       bash tools/gpu_sweep.sh $TAG > $O/sweep_$TAG.log 2>&1; rc=$?
       cat $O/sweep_$TAG.log ;;
