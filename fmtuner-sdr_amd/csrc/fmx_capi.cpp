@@ -126,6 +126,7 @@ struct Handle {
   // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
   bool skip_rds = false, skip_pll = false, skip_audio = false;
 #endif
+  int pll_shape = 0; // k_pll tile shape (pll_shape_for)
   struct Pending {
     int k;
     hipEvent_t a, b;
@@ -358,6 +359,17 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
   if (max_count) *max_count = mx;
   return FMX_OK;
 }
+// k_pll tile shape for a handle of n channels: 64
+// channels x 4 samples halves the workgroups beside k_fe8; 32 x 8 halves the
+// serial pipeline iterations per workgroup
+// issue priorities (s_setprio) of the latency-bound kernels beside k_fe8
+#ifndef FMX_PLL_PRIO
+#define FMX_PLL_PRIO 1
+#endif
+#ifndef FMX_RDS_PRIO
+#define FMX_RDS_PRIO 1
+#endif
+static int pll_shape_for(int n) { return n >= FMX_PLL_WIDE_MIN ? 0 : 1; }
 static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
   // a copy kernel reading the mapped pinned image, not hipMemcpyAsync: the
@@ -592,6 +604,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   }
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') serial = true;
 #endif
+  h->pll_shape = pll_shape_for(n);
+#if FMX_DIAG
+  if (const char *e = std::getenv("FMX_PLL_SHAPE")) h->pll_shape = std::atoi(e) == 1 ? 1 : 0;
+#endif
   if (serial) {
     h->sB = h->sC = h->sD = h->sA;
   } else {
@@ -778,7 +794,8 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
-  a.prio = 1; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
+  a.prio = FMX_PLL_PRIO; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
+  a.shape = h->pll_shape;
   return a;
 }
 
@@ -793,7 +810,7 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
-  a.prio = 1; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
+  a.prio = FMX_RDS_PRIO; // s_setprio 2 beside the front end's waves
   return a;
 }
 

@@ -77,6 +77,11 @@ struct FeArgs {
   int rds_sched_stride;
 };
 
+// k_pll shape policy: handles of at least this many channels take the 64 x 4
+// tiles (fmx_capi.cpp pll_shape_for)
+#ifndef FMX_PLL_WIDE_MIN
+#define FMX_PLL_WIDE_MIN 4096
+#endif
 struct PllArgs {
   const FmxDesign *des;
   const FmxChanParam *par;
@@ -94,6 +99,7 @@ struct PllArgs {
   int *indicator_out;      // [C] XDR stereo indicator (main.cpp:1298-1300), may be null
   unsigned long long *dbg; // [16] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
   int prio;                // raise the waves' issue priority (s_setprio)
+  int shape;               // tile shape: 0 = 64 channels x 4 samples, 1 = 32 x 8 (launch_pll)
 };
 
 struct AudioArgs {

@@ -1016,130 +1016,11 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
  * iterations (each costs a barrier and an LDS round trip) and runs 0.45 ms
  * alone against 0.60 for 64 x 4, but occupies twice the CUs beside k_fe8,
  * which the pipelined step pays for. */
-#ifndef PLL_CH
-#define PLL_CH 64
-#endif
-#ifndef PLL_T
-#define PLL_T 4
-#endif
-#define PLL_TS PLL_T
-#define PLL_WAVES 7
-#define PLL_W1 1
-#define PLL_W3 5
-#define PLL_NINP 5                         // pilot tile ring: tiles k-2 .. k+2 live at iteration k
-#define PLL_NIT(NT) ((NT) + 4)             // pipeline iterations (tile k of W0 .. tile k-4 of W3)
-static_assert(PLL_CH * PLL_T == 256 && PLL_T % 4 == 0 && 64 % PLL_T == 0 && PLL_CH <= 64, "k_pll tile shape");
-
-struct alignas(16) PllShared {
-  float inp[PLL_NINP][PLL_CH][PLL_TS];     // pilot tiles: k+2 stored (W3), k+1 read ahead (W0), k-1 (P), k-2 (W1)
-  float inm[2][PLL_CH][PLL_TS];            // mpx tiles (k-1 loading, k-2 in W1)
-  uint32_t s0t[2][PLL_CH][PLL_TS];         // W0 -> P: NCO words after each step
-  float su[2][2][PLL_CH][PLL_TS];          // P -> W1: (pilot * vcoI) * kI, (pilot * vcoQ) * kI
-  float sf[3][2][PLL_CH][PLL_TS];          // P phase (k-1) -> P target (k-3): FREQ, COS2
-  float sr[2][3][PLL_CH][PLL_TS];          // W1 -> P target: PBM, MM, MAG2
-  float s2[2][4][PLL_CH][PLL_TS];          // P target -> W3: TGT, MONO, DL, DR
-  float dly[2][PLL_CH][PLL_TS];            // delay-line output tiles
-  int s2_flags[PLL_CH];                    // bit0 fmono, bit1 fstereo, bit2 detected, bits 8.. blend mode
-  float s2_gate[PLL_CH];
-};
-enum { F_FREQ = 0, F_COS2 = 1 };                      // sf
-enum { F_PBM = 0, F_MM = 1, F_MAG2 = 2 };             // sr
-enum { F_TGT = 0, F_MONO = 1, F_DL = 2, F_DR = 3 };  // s2
-
-// One row-tile (PLL_CH rows x PLL_T samples from t0) of a [rows][stride]
-// array, staged through registers: issue() starts 16-B buffer loads (one
-// VGPR offset, the tile position in SGPRs; rows past C read 0), store()
-// writes them to an LDS tile after the next barrier.  Needs 16-B aligned
-// rows and a full tile; pll_load_sync covers the rest.
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-struct PllStage {
-  static constexpr int J = PLL_CH * PLL_T / 4 / 64; // float4 per lane
-  float4 v[J];
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t r, int stride, int t0, int lane) {
-    const uint32_t voff = (uint32_t)(((lane / (PLL_T / 4)) * stride + 4 * (lane % (PLL_T / 4))) * 4);
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-      v[j] = bload4(r, voff, (uint32_t)((t0 + j * (64 / (PLL_T / 4)) * stride) * 4));
-  }
-  __device__ __forceinline__ void store(float (*dst)[PLL_TS], int lane) const {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int idx = lane + 64 * j;
-      const int row = idx / (PLL_T / 4), q = idx % (PLL_T / 4);
-      *reinterpret_cast<float4 *>(&dst[row][4 * q]) = v[j];
-    }
-  }
-};
-__device__ __forceinline__ void pll_load_sync(const float *src, int stride, int C, float (*dst)[PLL_TS], int c0,
-                                              int t0, int cnt, int lane) {
-  for (int idx = lane; idx < PLL_CH * PLL_T; idx += 64) {
-    const int row = idx / PLL_T, col = idx % PLL_T;
-    const int ch = c0 + row;
-    dst[row][col] = (ch < C && col < cnt) ? src[(size_t)ch * stride + t0 + col] : 0.0f;
-  }
-}
-
-// delay-line outputs of tile (t0, cnt): mpx[t - Dly], or the previous call's
-// history (stereo_decoder.cpp delayLine) for t < Dly, staged through
-// registers.  The source is wave-uniform except in the one tile that
-// straddles t = Dly.
-struct PllDlyStage {
-  static constexpr int J = PLL_CH * PLL_T / 64;
-  float v[J];
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rm, int mstride, __amdgpu_buffer_rsrc_t rh, int t0,
-                                        int cnt, int lane, int Dly) {
-    const int row0 = lane / PLL_T, col = lane % PLL_T;
-    const bool colok = col < cnt;
-    // columns past cnt: an offset past the buffer range, read as 0 (no select
-    // after the load, so nothing waits for it before the next barrier)
-    const uint32_t vm = colok ? (uint32_t)((row0 * mstride + col) * 4) : 0x80000000u;
-    const uint32_t vh = colok ? (uint32_t)((row0 * FMX_HIST + col) * 4) : 0x80000000u;
-    const int d0 = t0 - Dly; // delay index of column 0
-    if (d0 >= 0) {
-#pragma unroll
-      for (int j = 0; j < J; ++j) v[j] = bload1(rm, vm, (uint32_t)((d0 + j * (64 / PLL_T) * mstride) * 4));
-    } else if (d0 + PLL_T <= 0) {
-#pragma unroll
-      for (int j = 0; j < J; ++j)
-        v[j] = bload1(rh, vh, (uint32_t)((FMX_HIST + d0 + j * (64 / PLL_T) * FMX_HIST) * 4));
-    } else {
-      const bool from_m = d0 + col >= 0;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const uint32_t om = (uint32_t)(((j * (64 / PLL_T)) * mstride + (from_m ? d0 : 0)) * 4);
-        const uint32_t oh = (uint32_t)(((j * (64 / PLL_T)) * FMX_HIST + FMX_HIST + (from_m ? 0 : d0)) * 4);
-        // columns past cnt read 0 through their out-of-range offset (no
-        // select here either, nothing waits for these loads before the store)
-        v[j] = from_m ? bload1(rm, vm + om, 0) : bload1(rh, vh + oh, 0);
-      }
-    }
-  }
-  __device__ __forceinline__ void store(float (*dst)[PLL_TS], int lane) const {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int idx = lane + 64 * j;
-      dst[idx / PLL_T][idx % PLL_T] = v[j];
-    }
-  }
-};
-
-// the value of the previous sample of this lane's item: lane t of a row
-// reads lane t - 1; t = 0 reads the row's t = PLL_T - 1 of the PREVIOUS
-// iteration (lanes with t = PLL_T - 1 offer `prev`, the others `cur`)
-__device__ __forceinline__ float item_prev(float cur, float prev, bool tlast, int src_addr) {
-  const float x = tlast ? prev : cur;
-  if constexpr (PLL_T == 4) {
-    // quad_perm [3, 0, 1, 2]: lane 0 <- 3, lane 1 <- 0, lane 2 <- 1, lane 3 <- 2
-    (void)src_addr;
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x93, 0xF, 0xF, false));
-  } else {
-    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_addr, __builtin_bit_cast(int, x)));
-  }
 }
 // sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
 // which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
@@ -1149,530 +1030,23 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
   *c = __builtin_amdgcn_cosf(r);
 }
 
-// <= 88 VGPRs: two k_pll waves (P0 + P3 on SIMD 2) beside two k_fe8 waves (168 each) in 512
-__global__ __launch_bounds__(64 * PLL_WAVES) __attribute__((amdgpu_num_vgpr(88))) void k_pll(PllArgs a) {
-  if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
-  else if (a.prio) __builtin_amdgcn_s_setprio(2);
-  __shared__ PllShared shm;
-  PllShared *sh = &shm;
-  // Stage barrier: LDS writes complete (lgkmcnt) + s_barrier.  Not
-  // __syncthreads(): its fence would also drain W3's register-staged global
-  // loads (vmcnt), which are meant to stay in flight across the barrier.
-#define PLL_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
-#ifdef FMX_STAMPS
-  unsigned long long pw_work = 0, pw_wait = 0, pw_last = __builtin_amdgcn_s_memtime();
-  const unsigned long long pw_rt0 = __builtin_amdgcn_s_memrealtime();
-#define PLL_SYNC()                                                   \
-  {                                                                  \
-    unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
-    pw_work += t_ - pw_last;                                         \
-    PLL_BARRIER();                                                   \
-    pw_last = __builtin_amdgcn_s_memtime();                          \
-    pw_wait += pw_last - t_;                                         \
-  }
-  // sub-stage clocks of a wave's work (W1: loads | tile), a.dbg[16 + 4 w + i]
-  unsigned long long pw_sub[2] = {0, 0}, pw_s0 = pw_last;
-#define PLL_SUB(i)                                                   \
-  {                                                                  \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
-    pw_sub[i] += t_ - ((i) == 0 ? pw_last : pw_s0);                  \
-    pw_s0 = t_;                                                      \
-  }
-#define PLL_STAMP_OUT()                                              \
-  if (a.dbg && (threadIdx.x & 63) == 0) {                            \
-    atomicAdd(a.dbg + 2 * (threadIdx.x >> 6), pw_work);              \
-    atomicAdd(a.dbg + 2 * (threadIdx.x >> 6) + 1, pw_wait);          \
-    if ((threadIdx.x >> 6) < 4) {                                    \
-      atomicAdd(a.dbg + 16 + 4 * (threadIdx.x >> 6), pw_sub[0]);     \
-      atomicAdd(a.dbg + 17 + 4 * (threadIdx.x >> 6), pw_sub[1]);     \
-    }                                                                \
-  }
-#else
-#define PLL_SUB(i)
-#define PLL_SYNC() PLL_BARRIER();
-#define PLL_STAMP_OUT()
-#endif
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int c0 = blockIdx.x * PLL_CH;
-  const FmxDesign *__restrict__ D = a.des;
-  const int n = a.n;
-  const int NT = (n + PLL_T - 1) / PLL_T;
-  const int Dly = D->delay_len;
-  constexpr float kS = 0.9995f;
-  constexpr float kI = 1.0f - 0.9995f;
-  if (n <= 0) {  // processAudio(n == 0) returns before touching state
-    const int ch = c0 + tid;
-    if (tid < PLL_CH && ch < a.C) {
-      if (a.stereo_out) a.stereo_out[ch] = a.st[ch].detected;
-      if (a.pilot_tenths_out) a.pilot_tenths_out[ch] = a.st[ch].level;
-      if (a.indicator_out) a.indicator_out[ch] = a.st[ch].detected || (a.par[ch].force_mono && a.st[ch].level >= 20);
-    }
-    return;
-  }
-  const bool vec = ((((uintptr_t)a.pilot) | ((uintptr_t)a.mpx)) & 15) == 0 && (a.pilot_stride & 3) == 0 &&
-                   (a.mpx_stride & 3) == 0;
-
-  if (tid < PLL_CH) {
-    const int ch = c0 + tid;
-    int f = 0;
-    float g = 1.0f;
-    if (ch < a.C) {
-      const FmxChanParam par = a.par[ch];
-      f = (par.force_mono ? 1 : 0) | (par.force_stereo ? 2 : 0) | (a.st[ch].detected ? 4 : 0) | (par.blend << 8);
-      g = D->gate[par.blend];
-    }
-    sh->s2_flags[tid] = f;
-    sh->s2_gate[tid] = g;
-  }
-  if (wave == PLL_W3) {
-    pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[0], c0, 0, min(PLL_T, n), lane);
-    if (n > PLL_T) pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[1], c0, PLL_T, min(PLL_T, n - PLL_T), lane);
-  }
-  __syncthreads();
-
-  // serial waves: lane = row (channel c0 + lane); lanes >= PLL_CH idle (they
-  // read row lrow and store nothing)
-  const int lrow = lane < PLL_CH ? lane : PLL_CH - 1;
-  const int c = c0 + lane;
-  const bool act = lane < PLL_CH && c < a.C;
-  const bool own = lane < PLL_CH;
-  // block-end values gathered for W0, after the loop (aliases the pilot tiles)
-  float(*fin)[PLL_CH] = reinterpret_cast<float(*)[PLL_CH]>(&sh->inp[0][0][0]);
-  static_assert(6 * PLL_CH <= PLL_NINP * PLL_CH * PLL_TS, "fin inside the pilot tiles");
-  if (wave == 0) {
-    // ---------------- W0: the PLL feedback chain ----------------
-    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
-    uint32_t theta = s0.theta, dtheta = s0.dtheta, tprev = s0.theta;
-    // liquid pll_step: dtheta += constrain(e alpha), theta += constrain(e
-    // beta) (then step: theta += dtheta), constrain(x) = frac(x / 2 pi) 2^32
-    const float ka = D->pll_alpha * 0.159154943091895f, kb = D->pll_beta * 0.159154943091895f;
-    float vcoQ;
-    {
-      float cq;
-      word_sincos(theta, &vcoQ, &cq);
-    }
-    // the pilot tile is read one iteration ahead (W3 stores tile k+2 during
-    // iteration k), so its LDS latency overlaps the chain of the current tile
-    float4 pcur[PLL_T / 4], pnxt[PLL_T / 4];
-#pragma unroll
-    for (int q = 0; q < PLL_T / 4; ++q) pnxt[q] = pcur[q] = *reinterpret_cast<const float4 *>(&sh->inp[0][lrow][4 * q]);
-    for (int k = 0; k < PLL_NIT(NT); ++k) {
-      if (k + 1 < NT) {
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q)
-          pnxt[q] = *reinterpret_cast<const float4 *>(&sh->inp[(k + 1) % PLL_NINP][lrow][4 * q]);
-      }
-      // full tiles run without per-sample guards (a compile-time case)
-      auto tile = [&](auto full_c, int cnt) __attribute__((always_inline)) {
-        constexpr bool FULL = decltype(full_c)::value;
-        float pv[PLL_T];
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          pv[4 * q] = pcur[q].x; pv[4 * q + 1] = pcur[q].y; pv[4 * q + 2] = pcur[q].z; pv[4 * q + 3] = pcur[q].w;
-        }
-        uint32_t tw[PLL_T];
-#pragma unroll
-        for (int t = 0; t < PLL_T; ++t) {
-          if (FULL || t < cnt) {
-            const float err = pv[t] * vcoQ; // pilot * sin(phase)
-            const uint32_t ca = (uint32_t)(__builtin_amdgcn_fractf(err * ka) * 4294967296.0f);
-            const uint32_t cb = (uint32_t)(__builtin_amdgcn_fractf(err * kb) * 4294967296.0f);
-            const uint32_t T = theta + dtheta; // off the chain
-            tprev = theta;
-            dtheta += ca;
-            theta = T + (ca + cb);
-            vcoQ = __builtin_amdgcn_sinf((float)(int32_t)theta * 2.3283064365386963e-10f);
-          }
-          tw[t] = theta;
-        }
-        if (own) {
-#pragma unroll
-          for (int q = 0; q < PLL_T / 4; ++q)
-            *reinterpret_cast<uint4 *>(&sh->s0t[k & 1][lane][4 * q]) =
-                make_uint4(tw[4 * q], tw[4 * q + 1], tw[4 * q + 2], tw[4 * q + 3]);
-        }
-      };
-      if (k < NT) {
-        const int cnt = min(PLL_T, n - k * PLL_T);
-        if (cnt == PLL_T) tile(std::true_type{}, cnt);
-        else tile(std::false_type{}, cnt);
-      }
-#pragma unroll
-      for (int q = 0; q < PLL_T / 4; ++q) pcur[q] = pnxt[q];
-      PLL_SYNC()
-    }
-    PLL_SYNC() // W1 / W3 block-end values in sh->fin
-    PLL_STAMP_OUT()
-#ifdef FMX_STAMPS
-    if (a.dbg && lane == 0) {
-      atomicAdd(a.dbg + 14, __builtin_amdgcn_s_memrealtime() - pw_rt0);
-      atomicMax(a.dbg + 15, __builtin_amdgcn_s_memrealtime() - pw_rt0);
-    }
-#endif
-    if (!act) return;
-    // ---- block-end stereo detection (stereo_decoder.cpp:243-285) ----
-    FmxStereoState s = s0;
-    s.theta = theta;
-    s.dtheta = dtheta;
-    s.pll_phase = d_nco_phase(theta);
-    // m_pllFreq of the last sample: clamp(unwrap(phaseNext - phaseNow))
-    s.pll_freq = d_clamp(d_unwrap(s.pll_phase - d_nco_phase(tprev)), D->pll_min, D->pll_max);
-    s.pilot_band_mag = fin[0][lane];
-    s.mpx_mag = fin[1][lane];
-    s.pilot_i = fin[2][lane];
-    s.pilot_q = fin[3][lane];
-    s.blend = fin[5][lane];
-    const float nominal = D->nominal;
-    const FmxChanParam par = a.par[c];
-    const bool fstereo = par.force_stereo != 0;
-    const float fsf = (float)D->fs;
-    bool detected = s.detected != 0;
-    const float mag = sqrtf((s.pilot_i * s.pilot_i) + (s.pilot_q * s.pilot_q));
-    s.pilot_magnitude = (s.pilot_magnitude * 0.9f) + (mag * 0.1f);
-    const float mpxThr = detected ? 0.0028f : 0.005f;
-    const float ratio = s.pilot_band_mag / fmaxf(s.mpx_mag, 1e-3f);
-    const float coh = s.pilot_magnitude / fmaxf(s.pilot_band_mag, 1e-4f);
-    const float ratioThr = detected ? 0.022f : 0.040f;
-    const float cohThr = detected ? 0.11f : 0.18f;
-    const float errHz = fabsf(s.pll_freq - nominal) * fsf / (2.0f * kPiF);
-    const float pllThr = detected ? 320.0f : 180.0f;
-    const bool present = (s.mpx_mag > mpxThr) && (ratio > ratioThr) && (coh > cohThr) && (errHz < pllThr);
-    if (!fstereo) {
-      if (!detected) {
-        if (present) {
-          s.pilot_count++;
-          s.loss_count = 0;
-          if (s.pilot_count >= 6) detected = true;
-        } else {
-          s.pilot_count = 0;
-        }
-      } else if (present) {
-        s.loss_count = 0;
-      } else if (++s.loss_count >= 24) {
-        detected = false;
-        s.pilot_count = 0;
-        s.loss_count = 0;
-      }
-    }
-    const float calibrated = s.pilot_magnitude * 8.0f;
-    int lvl = (int)roundf(calibrated * 750.0f);
-    s.level = lvl < 0 ? 0 : (lvl > 750 ? 750 : lvl);
-    s.detected = detected ? 1 : 0;
-    a.st[c] = s;
-    if (a.stereo_out) a.stereo_out[c] = s.detected;
-    if (a.pilot_tenths_out) a.pilot_tenths_out[c] = s.level;
-    // XDR stereo indicator: stereoDetected || (forceMono && stereo && pilot >= 20)
-    // (main.cpp:1298-1300; k_pll runs only with processing.stereo)
-    if (a.indicator_out) a.indicator_out[c] = (s.detected || (par.force_mono && s.level >= 20)) ? 1 : 0;
-  } else if (wave == PLL_W1) {
-    // ---------------- W1: envelopes and pilot I/Q integrators; MPX / delay loader ----------------
-    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
-    float pbm = s0.pilot_band_mag, mm = s0.mpx_mag, pi_ = s0.pilot_i, pq = s0.pilot_q;
-    // loads staged in registers across the barriers (as W3's pilot tiles):
-    // iteration k stores mpx tile k-1 (read here at k+1) and delay tile k-2
-    // (the P targets at k+1), then issues mpx k+1 and delay k
-    PllStage stm0, stm1;
-    PllDlyStage sd0, sd1;
-    auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
-    auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
-    const int rows_valid = min(PLL_CH, a.C - c0);
-    const __amdgpu_buffer_rsrc_t rm4 =
-        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, vec ? (uint32_t)((size_t)rows_valid * a.mpx_stride * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t rm =
-        make_rsrc(a.mpx + (size_t)c0 * a.mpx_stride, (uint32_t)((size_t)rows_valid * a.mpx_stride * 4));
-    const __amdgpu_buffer_rsrc_t rh =
-        make_rsrc(a.st_hist_rd + (size_t)c0 * FMX_HIST, (uint32_t)((size_t)rows_valid * FMX_HIST * 4));
-    __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0): the state loads retired before the staged loads
-    stm0.issue(rm4, a.mpx_stride, 0, lane);
-    auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
-      constexpr int P = decltype(par_c)::value; // k & 1
-      PllStage &stm = P ? stm0 : stm1;          // mpx tile k-1, then k+1
-      PllDlyStage &std_ = P ? sd1 : sd0;        // delay tile k-2, then k
-      if (k - 1 >= 0 && k - 1 < NT) {
-        if (full(k - 1)) stm.store(sh->inm[(k - 1) & 1], lane);
-        else pll_load_sync(a.mpx, a.mpx_stride, a.C, sh->inm[(k - 1) & 1], c0, (k - 1) * PLL_T, tcnt(k - 1), lane);
-      }
-      if (k - 2 >= 0 && k - 2 < NT) std_.store(sh->dly[(k - 2) & 1], lane);
-      stm.issue(rm4, a.mpx_stride, (k + 1) * PLL_T, lane);
-      std_.issue(rm, a.mpx_stride, rh, k * PLL_T, tcnt(k), lane, Dly);
-      PLL_SUB(0)
-      const int kt = k - 2;
-      // full tiles: straight-line code, 16-B LDS reads and writes, four
-      // samples at a time (short live ranges); a ragged last tile (n not a
-      // multiple of PLL_T) takes the rolled per-sample loop below, kept
-      // structurally apart so that the compiler does not merge the two into
-      // one per-sample-branching body
-      auto tile_full = [&]() __attribute__((always_inline)) {
-        const int sb = kt & 1;
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 x = *reinterpret_cast<const float4 *>(&sh->inp[kt % PLL_NINP][lrow][4 * q]);
-          const float4 y = *reinterpret_cast<const float4 *>(&sh->inm[sb][lrow][4 * q]);
-          const float4 ui = *reinterpret_cast<const float4 *>(&sh->su[sb][0][lrow][4 * q]);
-          const float4 uq = *reinterpret_cast<const float4 *>(&sh->su[sb][1][lrow][4 * q]);
-          const float pv[4] = {x.x, x.y, x.z, x.w}, mv[4] = {y.x, y.y, y.z, y.w};
-          const float uiv[4] = {ui.x, ui.y, ui.z, ui.w}, uqv[4] = {uq.x, uq.y, uq.z, uq.w};
-          float o_pbm[4], o_mm[4], o_mag2[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            pbm = (pbm * kS) + (fabsf(pv[u]) * kI);
-            mm = (mm * kS) + (fabsf(mv[u]) * kI);
-            pi_ = (pi_ * kS) + uiv[u];
-            pq = (pq * kS) + uqv[u];
-            o_pbm[u] = pbm;
-            o_mm[u] = mm;
-            o_mag2[u] = (pi_ * pi_) + (pq * pq);
-          }
-          if (own) {
-            const int t = 4 * q;
-            *reinterpret_cast<float4 *>(&sh->sr[sb][F_PBM][lane][t]) = make_float4(o_pbm[0], o_pbm[1], o_pbm[2], o_pbm[3]);
-            *reinterpret_cast<float4 *>(&sh->sr[sb][F_MM][lane][t]) = make_float4(o_mm[0], o_mm[1], o_mm[2], o_mm[3]);
-            *reinterpret_cast<float4 *>(&sh->sr[sb][F_MAG2][lane][t]) = make_float4(o_mag2[0], o_mag2[1], o_mag2[2], o_mag2[3]);
-          }
-        }
-      };
-      if (kt >= 0 && kt < NT) {
-        const int cnt = min(PLL_T, n - kt * PLL_T);
-        if (cnt == PLL_T) {
-          tile_full();
-        } else {
-          const int sb = kt & 1;
-#pragma unroll 1
-          for (int t = 0; t < cnt; ++t) {
-            pbm = (pbm * kS) + (fabsf(sh->inp[kt % PLL_NINP][lrow][t]) * kI);
-            mm = (mm * kS) + (fabsf(sh->inm[sb][lrow][t]) * kI);
-            pi_ = (pi_ * kS) + sh->su[sb][0][lrow][t];
-            pq = (pq * kS) + sh->su[sb][1][lrow][t];
-            if (own) {
-              sh->sr[sb][F_PBM][lane][t] = pbm;
-              sh->sr[sb][F_MM][lane][t] = mm;
-              sh->sr[sb][F_MAG2][lane][t] = (pi_ * pi_) + (pq * pq);
-            }
-          }
-        }
-      }
-      PLL_SUB(1)
-      PLL_SYNC()
-    };
-    for (int k = 0; k < PLL_NIT(NT); k += 2) {
-      iter(k, std::integral_constant<int, 0>{});
-      if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
-    }
-    if (own) {
-      fin[0][lane] = pbm;
-      fin[1][lane] = mm;
-      fin[2][lane] = pi_;
-      fin[3][lane] = pq;
-    }
-    PLL_SYNC()
-    PLL_STAMP_OUT()
-  } else if (wave == PLL_W3) {
-    // ---------------- W3: blend recursion + outputs; pilot loader ----------------
-    const FmxStereoState s0 = act ? a.st[c] : FmxStereoState{};
-    float blend = s0.blend;
-    const int mode = sh->s2_flags[lrow] >> 8;
-    const float attack = D->blend_attack[mode], release = D->blend_release[mode];
-    // pilot tiles staged in registers TWO iterations ahead, across the
-    // barriers: iteration k stores tile k+2 (W0 reads it ahead at k+1), then
-    // issues tile k+4 into the registers just stored.  Two register sets by
-    // tile parity; the loop is unrolled by two so every set is static.
-    PllStage stp0, stp1;
-    auto tcnt = [&](int tile) { return min(PLL_T, n - tile * PLL_T); };
-    auto full = [&](int tile) { return vec && tile < NT && tcnt(tile) == PLL_T; };
-    const int rows_valid = min(PLL_CH, a.C - c0);
-    // the staged 16-B tile loads are issued unconditionally (a fixed count
-    // per iteration keeps the waitcnt pass from draining them at the stores);
-    // tiles past the block or an unaligned layout read zeros (empty range)
-    // and are replaced by pll_load_sync at the store
-    const __amdgpu_buffer_rsrc_t rp =
-        make_rsrc(a.pilot + (size_t)c0 * a.pilot_stride, vec ? (uint32_t)((size_t)rows_valid * a.pilot_stride * 4) : 0u);
-    // retire every load made so far (blend, attack, release): otherwise the
-    // waitcnt pass, merging states at the loop header, drains the staged
-    // tile loads (vmcnt(0)) at their first use inside the loop
-    __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
-    stp0.issue(rp, a.pilot_stride, 2 * PLL_T, lane);
-    stp1.issue(rp, a.pilot_stride, 3 * PLL_T, lane);
-    auto iter = [&](int k, auto par_c) __attribute__((always_inline)) {
-      constexpr int P = decltype(par_c)::value; // k & 1
-      PllStage &stp = P ? stp1 : stp0;          // pilot tile k+2, then k+4
-      if (k + 2 < NT) {
-        const int sl = (k + 2) % PLL_NINP;
-        if (full(k + 2)) stp.store(sh->inp[sl], lane);
-        else pll_load_sync(a.pilot, a.pilot_stride, a.C, sh->inp[sl], c0, (k + 2) * PLL_T, tcnt(k + 2), lane);
-      }
-      stp.issue(rp, a.pilot_stride, (k + 4) * PLL_T, lane);
-      const int kt = k - 4;
-      // full tiles straight-line, a ragged last tile per sample (as W1)
-      auto tile_full = [&]() __attribute__((always_inline)) {
-        const int sb = kt & 1;
-#pragma unroll
-        for (int q = 0; q < PLL_T / 4; ++q) {
-          const float4 tg = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_TGT][lrow][4 * q]);
-          const float4 mo = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_MONO][lrow][4 * q]);
-          const float4 dl = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DL][lrow][4 * q]);
-          const float4 dr = *reinterpret_cast<const float4 *>(&sh->s2[sb][F_DR][lrow][4 * q]);
-          const float tga[4] = {tg.x, tg.y, tg.z, tg.w}, moa[4] = {mo.x, mo.y, mo.z, mo.w};
-          const float dla[4] = {dl.x, dl.y, dl.z, dl.w}, dra[4] = {dr.x, dr.y, dr.z, dr.w};
-          float ov[2][4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            // blend += (tgt - blend) * (tgt > blend ? attack : release),
-            // select-free: exactly one of the two products is nonzero and
-            // adding the other (+0 / -0) leaves the sum unchanged
-            const float d = tga[u] - blend;
-            blend = (blend + fmaxf(d, 0.0f) * attack) + fminf(d, 0.0f) * release;
-            ov[0][u] = moa[u] + (dla[u] * blend);
-            ov[1][u] = moa[u] + (dra[u] * blend);
-          }
-          if (act) {
-            // octet tiles (lr_tile_idx): the 8 lanes of a channel octet fill
-            // one 128-B line per 4 samples, a store instruction writes 8 whole lines
-            const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T + 4 * q, a.lr_stride)
-                                         : (size_t)c * a.lr_stride + kt * PLL_T + 4 * q;
-            if (a.lr_tiled) {
-              *reinterpret_cast<float4 *>(a.lraw + ob) = make_float4(ov[0][0], ov[0][1], ov[0][2], ov[0][3]);
-              *reinterpret_cast<float4 *>(a.rraw + ob) = make_float4(ov[1][0], ov[1][1], ov[1][2], ov[1][3]);
-            } else {
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                a.lraw[ob + u] = ov[0][u];
-                a.rraw[ob + u] = ov[1][u];
-              }
-            }
-          }
-        }
-      };
-      if (kt >= 0 && kt < NT) {
-        const int cnt = min(PLL_T, n - kt * PLL_T);
-        if (cnt == PLL_T) {
-          tile_full();
-        } else {
-          const int sb = kt & 1;
-#pragma unroll 1
-          for (int t = 0; t < cnt; ++t) {
-            const float d = sh->s2[sb][F_TGT][lrow][t] - blend;
-            blend = (blend + fmaxf(d, 0.0f) * attack) + fminf(d, 0.0f) * release;
-            const float mo = sh->s2[sb][F_MONO][lrow][t];
-            const float ol = mo + (sh->s2[sb][F_DL][lrow][t] * blend);
-            const float orr = mo + (sh->s2[sb][F_DR][lrow][t] * blend);
-            if (act) {
-              const size_t ob = a.lr_tiled ? lr_tile_idx(c, kt * PLL_T + t, a.lr_stride)
-                                           : (size_t)c * a.lr_stride + kt * PLL_T + t;
-              a.lraw[ob] = ol;
-              a.rraw[ob] = orr;
-            }
-          }
-        }
-      }
-      PLL_SUB(1)
-      PLL_SYNC()
-    };
-    for (int k = 0; k < PLL_NIT(NT); k += 2) {
-      iter(k, std::integral_constant<int, 0>{});
-      if (k + 1 < PLL_NIT(NT)) iter(k + 1, std::integral_constant<int, 1>{});
-    }
-    if (own) fin[5][lane] = blend;
-    PLL_SYNC()
-    PLL_STAMP_OUT()
-  } else {
-    // ---------------- P0..P3: the time-parallel stages ----------------
-    const int pw = (wave == 2) ? 0 : (wave == 3) ? 1 : (wave == 4) ? 2 : 3;
-    const int item = lane + 64 * pw;
-    const int row = item / PLL_T, tt = item % PLL_T;
-    const bool tlast = tt == PLL_T - 1;
-    // ds_bpermute address of the previous sample's lane (t = 0: the row's last)
-    const int src_addr = 4 * ((tt == 0) ? lane + PLL_T - 1 : lane - 1);
-    const int ch = c0 + row;
-    const float nominal = D->nominal, fsf = (float)D->fs;
-    const float pmin = D->pll_min, pmax = D->pll_max;
-    const int fl0 = sh->s2_flags[row];
-    const float gate = sh->s2_gate[row];
-    const int mode = fl0 >> 8;
-    // previous-iteration values of this lane's item (t = 3 offers them to
-    // the quad's t = 0): the state's phase word before the first tile
-    float prev_s, prev_c, prev_ph;
-    {
-      const uint32_t th0 = (ch < a.C) ? a.st[ch].theta : 0u;
-      word_sincos(th0, &prev_s, &prev_c);
-      prev_ph = d_nco_phase(th0);
-    }
-    for (int k = 0; k < PLL_NIT(NT); ++k) {
-      // both stages every iteration in one basic block (their LDS reads and
-      // dependent chains overlap); tiles outside the block compute on stale
-      // rows and store nothing
-      const int kp = k - 1, kt = k - 3; // phase stage tile, target stage tile
-      const bool dop = kp >= 0 && kp < NT;
-      const bool dot = kt >= 0 && kt < NT && tt < min(PLL_T, n - kt * PLL_T);
-      const int kpc = max(kp, 0), ktc = max(kt, 0);
-      const int sb = ktc & 1, sf3 = ktc % 3;
-      const uint32_t th = sh->s0t[kpc & 1][row][tt];
-      const float pilot = sh->inp[kpc % PLL_NINP][row][tt];
-      const float pbm = sh->sr[sb][F_PBM][row][tt];
-      const float mm = sh->sr[sb][F_MM][row][tt];
-      const float mag2 = sh->sr[sb][F_MAG2][row][tt];
-      const float pf = sh->sf[sf3][F_FREQ][row][tt];
-      const float cos2 = sh->sf[sf3][F_COS2][row][tt];
-      const float delayed = sh->dly[sb][row][tt];
-      // ---- phase stage (tile k-1) ----
-      float sN, cN;
-      word_sincos(th, &sN, &cN);
-      const float ph = d_nco_phase(th);
-      // vco of this sample = sin / cos of the previous sample's phase
-      const float sP = item_prev(sN, prev_s, tlast, src_addr), cP = item_prev(cN, prev_c, tlast, src_addr);
-      const float phP = item_prev(ph, prev_ph, tlast, src_addr);
-      const float uI = (pilot * cP) * kI, uQ = (pilot * sP) * kI;
-      const float fr = __builtin_amdgcn_fmed3f(d_unwrap(ph - phP), pmin, pmax); // clamp(dphi, min, max)
-      const float c2 = (cN * cN) - (sN * sN);
-      // ---- target stage (tile k-3): blend target (stereo_decoder.cpp:120-166)
-      // with hardware sqrt / reciprocal (~1 ulp) for the three quality ratios;
-      // divisions by constants as d_div_const (bit-identical to x / c for these
-      // divisors, all 2^32 words checked on the host); clamps as v_med3
-      const float magNow = __builtin_amdgcn_sqrtf(mag2);
-      const float ratioNow = pbm * __builtin_amdgcn_rcpf(fmaxf(mm, 1e-3f));
-      const float cohNow = magNow * __builtin_amdgcn_rcpf(fmaxf(pbm, 1e-4f));
-      const float errHzNow = d_div_const(fabsf(pf - nominal) * fsf, 2.0f * kPiF, 1.0f / (2.0f * kPiF));
-      constexpr float cR = 0.040f - 0.022f, cC = 0.18f - 0.11f, cPl = 320.0f - 180.0f;
-      const float ratioQ = __builtin_amdgcn_fmed3f(d_div_const(ratioNow - 0.022f, cR, 1.0f / cR), 0.0f, 1.0f);
-      const float cohQ = __builtin_amdgcn_fmed3f(d_div_const(cohNow - 0.11f, cC, 1.0f / cC), 0.0f, 1.0f);
-      const float pllQ = __builtin_amdgcn_fmed3f(d_div_const(320.0f - errHzNow, cPl, 1.0f / cPl), 0.0f, 1.0f);
-      const float q = fminf(ratioQ, fminf(cohQ, pllQ));
-      const bool gated = ratioNow < (0.022f * gate) || cohNow < (0.11f * gate) || errHzNow > (320.0f * 1.10f);
-      float shaped = q * q;
-      if (mode == 0) shaped = sqrtf(fmaxf(0.0f, q));
-      else if (mode == 2) shaped = shaped * q;
-      const float tg = gated ? 0.0f : __builtin_amdgcn_fmed3f(0.0f + ((1.0f - 0.0f) * shaped), 0.0f, 1.0f);
-      // force mono -> 0, force stereo -> 1, not detected -> 0 (computeBlendTarget's paths)
-      const float tgt = (fl0 & 1) ? 0.0f : ((fl0 & 2) ? 1.0f : ((fl0 & 4) ? tg : 0.0f));
-      const float monoNorm = delayed * 0.5f;
-      const float lr = 2.0f * delayed * cos2;
-      const float sl = (delayed + lr) * 0.5f;
-      const float sr = (delayed - lr) * 0.5f;
-      if (dop) {
-        prev_s = sN;
-        prev_c = cN;
-        prev_ph = ph;
-        sh->su[kp & 1][0][row][tt] = uI;
-        sh->su[kp & 1][1][row][tt] = uQ;
-        sh->sf[kp % 3][F_FREQ][row][tt] = fr;
-        sh->sf[kp % 3][F_COS2][row][tt] = c2;
-      }
-      if (dot) {
-        sh->s2[sb][F_TGT][row][tt] = tgt;
-        sh->s2[sb][F_MONO][row][tt] = monoNorm;
-        sh->s2[sb][F_DL][row][tt] = sl - monoNorm;
-        sh->s2[sb][F_DR][row][tt] = sr - monoNorm;
-      }
-      PLL_SYNC()
-    }
-    PLL_SYNC()
-    PLL_STAMP_OUT()
-  }
-#undef PLL_SYNC
-#undef PLL_STAMP_OUT
-#undef PLL_BARRIER
-}
+// k_pll in two tile shapes (fmx_pll.inc): 64 channels x 4 samples (half the
+// workgroups, fewer CUs beside k_fe8) and 32 channels x 8 samples (half the
+// pipeline iterations, twice the workgroups); launch_pll picks per handle.
+namespace pll64x4 {
+#define PLL_CH 64
+#define PLL_T 4
+#include "fmx_pll.inc"
+#undef PLL_CH
+#undef PLL_T
+} // namespace pll64x4
+namespace pll32x8 {
+#define PLL_CH 32
+#define PLL_T 8
+#include "fmx_pll.inc"
+#undef PLL_CH
+#undef PLL_T
+} // namespace pll32x8
 
 /* ================================================================== */
 /* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
@@ -3671,7 +3045,12 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
+  // shape: PllArgs::shape (0: 64 x 4, 1: 32 x 8), chosen by the handle (fmx_capi.cpp pll_shape)
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (a.shape == 1)
+    hipLaunchKernelGGL(pll32x8::k_pll, dim3((a.C + 31) / 32), dim3(64 * 7), 0, st, a);
+  else
+    hipLaunchKernelGGL(pll64x4::k_pll, dim3((a.C + 63) / 64), dim3(64 * 7), 0, st, a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {

@@ -1,0 +1,79 @@
+"""Register and LDS budgets of the built kernels (CPU: reads the gfx950 code
+object's metadata out of fmtuner-sdr_amd/libfmx.so).
+
+The pipelined step relies on co-residency: two k_fe8
+workgroups per CU (one wave of each per SIMD) must leave a SIMD room for a
+k_pll or k_rds wave, so k_fe8 stays within 168 VGPRs (2 x 168 + 176 = 512)
+and k_pll within 88 (two of its waves beside the two front-end waves), with
+no scratch spills.  A compiler-side change of a few lines once moved k_fe8
+from 162 to 189 VGPRs (an s_setprio branch at kernel entry), which silently
+cost the pipelined step 3 %: this test makes such a change fail loudly."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "fmtuner-sdr_amd", "libfmx.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernels(tmp_path):
+    if not os.path.exists(LIB):
+        pytest.skip("libfmx.so not built")
+    if not shutil.which("objcopy") or not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
+        pytest.skip("objcopy / clang-offload-bundler not available")
+    fat = str(tmp_path / "fatbin.bin")
+    co = str(tmp_path / "k.co")
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB, fat], check=True)
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--input=" + fat, "--output=" + co,
+                    "--unbundle"], check=True)
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True,
+                           capture_output=True, text=True).stdout
+    out = {}
+    for blk in re.split(r"\n\s+- \.", notes):
+        m = re.search(r"\.name:\s+(\S+)", blk)
+        if not m:
+            continue
+        f = {}
+        for key in ("vgpr_count", "agpr_count", "vgpr_spill_count", "sgpr_spill_count",
+                    "group_segment_fixed_size", "private_segment_fixed_size"):
+            mm = re.search(r"\." + key + r":\s+(\d+)", blk)
+            if mm:
+                f[key] = int(mm.group(1))
+        out[m.group(1)] = f
+    return out
+
+
+def _find(ks, pat):
+    hits = {k: v for k, v in ks.items() if re.search(pat, k)}
+    assert hits, (pat, sorted(ks))
+    return hits
+
+
+def test_front_end_register_budget(tmp_path):
+    ks = _kernels(tmp_path)
+    for name, f in _find(ks, r"k_fe8ILi10ELi28").items():
+        regs = f.get("vgpr_count", 0) + f.get("agpr_count", 0)
+        assert regs <= 168, (name, f)
+        assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
+
+
+def test_pll_register_and_lds_budget(tmp_path):
+    ks = _kernels(tmp_path)
+    hits = _find(ks, r"k_pllENS_7PllArgs")
+    assert len(hits) == 2  # the two tile shapes (fmx_pll.inc)
+    for name, f in hits.items():
+        assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 88, (name, f)
+        assert f.get("group_segment_fixed_size", 0) <= 36864, (name, f)
+        assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
+
+
+def test_rds_fits_beside_two_front_ends(tmp_path):
+    ks = _kernels(tmp_path)
+    for name, f in _find(ks, r"5k_rdsE").items():
+        assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 512 - 2 * 168, (name, f)
+        assert f.get("vgpr_spill_count", 0) == 0, (name, f)

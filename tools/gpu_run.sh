@@ -51,6 +51,19 @@ for step in "$@"; do
     pmc)
       bash tools/gpu_profile_pmc.sh "$TAG" > $O/pmc_$TAG.log 2>&1; rc=$?
       tail -12 $O/pmc_$TAG.log ;;
+    skips)
+      # pipelined step with kernels left out (diagnostics library, FMX_DIAG_SKIP):
+      # what each co-runner costs the front end's live time
+      for sk in none pll rds audio pll,rds,audio; do
+        FMX_LIB=$PWD/fmtuner-sdr_amd/libfmx_diag.so FMX_DIAG_SKIP=$sk timeout -k 10 200 python bench.py --steps 20 --warmup 5 \
+          --no-cpu-baseline > $O/skip_${sk}_$TAG.json 2> $O/skip_${sk}_$TAG.err || { rc=$?; break; }
+        python3 -c "import json,sys; r=json.load(open('$O/skip_${sk}_$TAG.json')); print('skip $sk', r['ms_per_step'], {k: v['avg_ms'] for k, v in r['kernels'].items()})"
+        rc=0
+      done ;;
+    counters)
+      # SQ counter passes (tools/gpu_counters.sh): instruction mix / waits per kernel
+      bash tools/gpu_counters.sh $TAG > $O/counters_$TAG.log 2>&1; rc=$?
+      cat $O/cnt_$TAG/summary.txt 2>/dev/null | head -80 ;;
     ubench)
       timeout -k 10 120 tools/ubench/chainlat > $O/chainlat_$TAG.txt 2>&1; rc=$?
       cat $O/chainlat_$TAG.txt ;;
