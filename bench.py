@@ -2,10 +2,11 @@
 """bench.py -- IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS).
 
 Workloads (BASELINE.json configs):
-  cfg3 (default)  4096 channels PER GPU of synthetic stereo FM + 57 kHz RDS
-                  (known groups), weak scaling over --gpus.
-  cfg4            16384 channels IN TOTAL sharded over the ranks with
-                  fmx_dist.shard (2048 per GPU at 8 GPUs), strong scaling.
+  cfg3 (default at N=1)  4096 channels PER GPU of synthetic stereo FM + 57 kHz
+                  RDS (known groups), weak scaling over --gpus.
+  cfg4 (default at N>1)  16384 channels IN TOTAL sharded over the ranks with
+                  fmx_dist.shard (2048 per GPU at 8 GPUs), strong scaling: the
+                  1/2/4/8-GPU curve BASELINE.json configs[3] names.
   --total-channels T overrides the total (sharded), --channels C the
   per-GPU count.
 Every channel: 2.4 MS/s u8 IQ, decimate-by-10 to 240 kHz, de-emphasis 50 us,
@@ -66,7 +67,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE or 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg3", "cfg4"], default="cfg3")
+    ap.add_argument("--workload", choices=["cfg3", "cfg4"], default=None,
+                    help="default: cfg3 on one GPU, cfg4 (BASELINE configs[3], the scaling curve) on N > 1")
     ap.add_argument("--channels", type=int, default=None, help="channels per GPU (cfg3 default 4096)")
     ap.add_argument("--total-channels", type=int, default=None, help="channels in total, sharded over ranks")
     ap.add_argument("--block", type=int, default=4096)
@@ -199,6 +201,8 @@ def cpu_baseline(fmx, d_iq, C, nblk, n_iq, B, seconds):
 def main():
     args = parse()
     world, spawn = resolve_world(args)
+    if args.workload is None:
+        args.workload = "cfg3" if world == 1 else "cfg4"
     if spawn:
         # no launcher: start the N ranks as children before any GPU call
         sys.exit(subprocess.run(launcher_cmd(world, sys.argv[1:])).returncode)

@@ -2271,6 +2271,12 @@ template <int M, int TPP> struct Fe8Layout {
   // (16-B aligned, above the complex image, inside the dead raw region)
   static constexpr int STG = (YB + 15) & ~15;
   static_assert(STG + FE8_T * 8 <= R0, "decimator staging inside the raw region");
+  // LDS-DMA targets (determinism): the early pieces of
+  // the next chunk land below uc while the RDS resampler reads uc; the late
+  // pieces cover uc only after the barrier that ends its reads, and no piece
+  // reaches the carried images, the resampler bank or the shared words
+  static_assert(NPC_EARLY * 1024 <= UOFF, "early DMA pieces end below uc");
+  static_assert(NPC * 1024 <= HX && HX <= MX && TL32 + 32 * 4 <= RST, "late DMA pieces end below the carried state");
   static_assert(XIN + 4 * IQW * 2 <= YB && (IQW * 2) % 16 == 0 && (FE_HALO_IQ * 2) % 16 == 0,
                 "IQ images below yb, 16-B aligned rows");
 };

@@ -40,7 +40,16 @@ def test_single_rank_dry_run():
     r = _run(["--dry-run"])
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["n_gpus"] == 1 and d["channels_summed"] == 4096
+    assert d["n_gpus"] == 1 and d["channels_summed"] == 4096 and d["scaling"] == "weak"
+
+
+def test_driver_scaling_invocation_defaults_to_cfg4():
+    """The driver's N>1 command names no workload: it gets BASELINE's Cfg4
+    curve (16384 channels sharded, 2048 per GPU at N=8)."""
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["total_channels"] == 16384 and d["channels_rank0"] == 8192 and d["scaling"] == "strong"
 
 
 def test_launcher_world_mismatch_fails():
