@@ -65,6 +65,12 @@ struct TimingSet {
   int *d_count[FMX_NBUF] = {};
   int *d_group[FMX_NBUF] = {};
   hipStream_t up_stream = nullptr; // stream of the last copy into the slots (the set's reader)
+  // one step of speculation (the RDS set of process_block): the next step's
+  // schedules for the same n, simulated into pinned image spec_img and copied
+  // into slot spec_slot by this step's front end (FeArgs::next_sched_*)
+  bool spec = false;
+  int spec_n = 0, spec_slot = -1, spec_G = 0, spec_img = -1;
+  std::vector<ResampTiming> spec_groups;
 };
 
 struct Handle {
@@ -389,10 +395,56 @@ static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
 // the stream of the set's reader.
 static int tset_advance(Handle *h, TimingSet &t, int n, int buf, hipStream_t s, int *max_count) {
   int rc;
+  t.spec = false; // any other advance voids a speculated next step
   if ((rc = tset_simulate(h, t, n, buf, max_count)) != FMX_OK) return rc;
   if ((rc = tset_upload(h, t, buf, s)) != FMX_OK) return rc;
   t.cur = buf;
   return FMX_OK;
+}
+
+// process_block's RDS set: take the schedules speculated last step when this
+// step has the same n (the slot was filled by the previous front end), else
+// simulate and upload as usual.
+static int tset_take_or_advance(Handle *h, TimingSet &t, int n, int buf, hipStream_t s) {
+  if (t.spec && t.spec_n == n && t.spec_slot == buf) {
+    t.groups = t.spec_groups;
+    t.G = t.spec_G;
+    t.hcur = t.spec_img;
+    t.cur = buf;
+    t.up_stream = s;
+    t.spec = false;
+    return FMX_OK;
+  }
+  return tset_advance(h, t, n, buf, s, nullptr);
+}
+// Simulate the NEXT step (same n) into a pinned image for slot `slot`; the
+// front end launched next copies it (one 16-B word per thread of its first
+// workgroups, grid of `threads` threads).  Returns the words to copy, 0 when
+// nothing is speculated (schedules that would not fit the slot or the grid).
+static unsigned tset_speculate(Handle *h, TimingSet &t, int n, int slot, size_t threads) {
+  t.spec = false;
+  const int G = static_cast<int>(t.groups.size());
+  const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * G;
+  const size_t n16 = (bytes + 15) / 16;
+  if (G > t.cap_groups || n16 > threads) return 0;
+  const int hb = t.hnext;
+  if (t.ev_h_set[hb] && hipEventSynchronize(t.ev_h[hb]) != hipSuccess) return 0;
+  t.spec_groups = t.groups;
+  FmxSched *hs = tset_hsched(h, t, hb);
+  int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
+  for (int g = 0; g < G; ++g) {
+    const int k = timing_run(t.spec_groups[static_cast<size_t>(g)], n, hs + static_cast<size_t>(g) * t.stride, t.stride);
+    if (k > t.stride) return 0;
+    hc[g] = k;
+  }
+  std::memcpy(t.h_slot[hb], t.chan_group.data(), sizeof(int) * h->C);
+  t.hnext = (hb + 1) % FMX_HSLOTS;
+  t.spec = true;
+  t.spec_n = n;
+  t.spec_slot = slot;
+  t.spec_G = G;
+  t.spec_img = hb;
+  return static_cast<unsigned>(n16);
 }
 
 // Make sA wait for everything queued on sB, sC and sD (used before resets,
@@ -865,8 +917,12 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   // step k-1's readers
   if (o->d_mpx && h->evD_set[prev]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[prev], 0));
   else if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
-  // RDS resampler schedule of this step (read by the front end only)
-  if (rds && (rc = tset_advance(h, h->t_rds, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
+  // RDS resampler schedule of this step (read by the front end only): the
+  // slot the previous front end filled when the speculation holds, else a
+  // copy kernel on sA; then the next step's, copied by this front end
+  if (rds && (rc = tset_take_or_advance(h, h->t_rds, n, buf, h->sA)) != FMX_OK) return rc;
+  const int nbuf = (buf + 1) % FMX_NBUF;
+  const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nbuf, static_cast<size_t>(h->C) * 256) : 0u;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
   // ---- front end (sA) ----
@@ -887,12 +943,21 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
     a.sig_sums = o->d_signal ? h->sig_sums[buf] : nullptr;
+    if (spec16) {
+      a.next_sched_src = h->t_rds.h_dev[h->t_rds.spec_img];
+      a.next_sched_dst = h->t_rds.d_slot[nbuf];
+      a.next_sched_n16 = spec16;
+    }
     KTimer t(h, FMX_K_FRONTEND, h->sA);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
       return rc;
     }
     dec_advance(h, n);
+  }
+  if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later
+    HIP_TRY(hipEventRecord(h->t_rds.ev_h[h->t_rds.spec_img], h->sA));
+    h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC) ----

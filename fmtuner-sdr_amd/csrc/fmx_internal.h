@@ -75,6 +75,12 @@ struct FeArgs {
   const int *rds_sched_n;    // [groups]
   const int *rds_group;      // [C]
   int rds_sched_stride;
+  // the NEXT step's RDS schedule slot, copied by the first workgroups of this
+  // launch from the mapped pinned image (fmx_capi.cpp process_block): no copy
+  // kernel on the front end's stream between two front ends; n16 = 0: none
+  const void *next_sched_src;
+  void *next_sched_dst;
+  unsigned next_sched_n16;
 };
 
 // k_pll shape policy: handles of at least this many channels take the 64 x 4

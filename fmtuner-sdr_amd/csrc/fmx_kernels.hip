@@ -494,9 +494,19 @@ template <int M, int TPP, bool VEC> struct FeLayout {
   static constexpr int NPF = (M > 1) ? (RAW_BYTES - 64 + 16 * 256 - 1) / (16 * 256) : 1;  // 16-B loads / thread
 };
 
+// The next step's RDS schedule slot (FeArgs::next_sched_*): one 16-B word
+// per thread of the first workgroups, from the mapped pinned image.  Readers
+// are the next front end launch on the same stream.
+__device__ __forceinline__ void fe_next_sched_copy(const FeArgs &a) {
+  if (a.next_sched_n16 == 0) return;
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i < a.next_sched_n16) static_cast<uint4 *>(a.next_sched_dst)[i] = static_cast<const uint4 *>(a.next_sched_src)[i];
+}
+
 template <int M, int TPP, bool VEC>
 __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  fe_next_sched_copy(a);
   using LY = FeLayout<M, TPP, VEC>;
   static_assert(!VEC || LY::HB >= 2 * LY::L, "VEC halo must hold L samples");
   static_assert(!VEC || 3 * M <= FMX_DEC_PAD, "dec_pad too short for this M");
@@ -2291,6 +2301,7 @@ template <int M, int TPP>
 #endif
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  fe_next_sched_copy(a);
   using LY = Fe8Layout<M, TPP>;
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
