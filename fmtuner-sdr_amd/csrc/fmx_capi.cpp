@@ -375,7 +375,15 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
 #ifndef FMX_RDS_PRIO
 #define FMX_RDS_PRIO 1
 #endif
-static int pll_shape_for(int n) { return n >= FMX_PLL_WIDE_MIN ? 0 : 1; }
+#ifndef FMX_PLL_SHAPE_BIG
+#define FMX_PLL_SHAPE_BIG 1   // handles of >= FMX_PLL_WIDE_MIN channels (r03f A/B at 4096 ch: 32 x 8
+                              // 0.841 ms/step, 64 x 4 0.854, 16 x 16 0.904: fewer iterations, and
+                              // 128 workgroups still leave most CUs two k_fe8 workgroups)
+#endif
+#ifndef FMX_PLL_SHAPE_SMALL
+#define FMX_PLL_SHAPE_SMALL 1 // smaller handles
+#endif
+static int pll_shape_for(int n) { return n >= FMX_PLL_WIDE_MIN ? FMX_PLL_SHAPE_BIG : FMX_PLL_SHAPE_SMALL; }
 static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
   // a copy kernel reading the mapped pinned image, not hipMemcpyAsync: the
@@ -658,7 +666,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
 #endif
   h->pll_shape = pll_shape_for(n);
 #if FMX_DIAG
-  if (const char *e = std::getenv("FMX_PLL_SHAPE")) h->pll_shape = std::atoi(e) == 1 ? 1 : 0;
+  if (const char *e = std::getenv("FMX_PLL_SHAPE")) h->pll_shape = std::clamp(std::atoi(e), 0, 2);
 #endif
   if (serial) {
     h->sB = h->sC = h->sD = h->sA;

@@ -496,7 +496,8 @@ template <int M, int TPP, bool VEC> struct FeLayout {
 
 // The next step's RDS schedule slot (FeArgs::next_sched_*): one 16-B word
 // per thread of the first workgroups, from the mapped pinned image.  Readers
-// are the next front end launch on the same stream.
+// are the next front end launch on the same stream (k_fe8 copies at its end,
+// k_frontend at its entry).
 __device__ __forceinline__ void fe_next_sched_copy(const FeArgs &a) {
   if (a.next_sched_n16 == 0) return;
   const unsigned i = blockIdx.x * 256u + threadIdx.x;
@@ -1057,6 +1058,13 @@ namespace pll32x8 {
 #undef PLL_CH
 #undef PLL_T
 } // namespace pll32x8
+namespace pll16x16 {
+#define PLL_CH 16
+#define PLL_T 16
+#include "fmx_pll.inc"
+#undef PLL_CH
+#undef PLL_T
+} // namespace pll16x16
 
 /* ================================================================== */
 /* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
@@ -1583,7 +1591,10 @@ struct RdsLds {
   float dmf[FMX_NPFB * FMX_SS_SUB];
   uint32_t esyn[5][52];
   uint32_t eerr[5][52];
-  f32x2 win[FMX_SS_SUB][RDS_CPW];  // symsync window ring per channel, newest at wp
+  // symsync window ring per channel, newest at wp, every sample written at
+  // wp and wp + FMX_SS_SUB: the window oldest-first is win[w0 .. w0 + 17],
+  // contiguous (constant read offsets, no wrap per tap)
+  f32x2 win[2 * FMX_SS_SUB][RDS_CPW];
   float symq[RDS_SYMQ][RDS_CPW];   // symbols (real part) awaiting biphase / block sync
   RdsCold cold[RDS_CPW];
 };
@@ -1795,7 +1806,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   float ss_rate = G.ss_rate, ss_del = G.ss_del, ss_tau = G.ss_tau, ss_q_hat = G.ss_q_hat, ss_v1 = G.ss_v1;
   int ss_b = G.ss_b, ss_decim = G.ss_decim, ss_valid = G.ss_mf_valid;
   if (lead)
-    for (int m = 0; m < FMX_SS_SUB; ++m) L.win[m][g] = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
+    for (int m = 0; m < FMX_SS_SUB; ++m) L.win[m][g] = L.win[m + FMX_SS_SUB][g] = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
   int wp = FMX_SS_SUB - 1; // newest window sample at wp
   int ng = 0;
   const f32x2 fscale2 = f32x2{D->rds_fir_scale, D->rds_fir_scale};
@@ -1918,12 +1929,12 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       if (agc_g > 1e6f) agc_g = 1e6f;
       // ---- symsync: push into both MF banks' window ----
       wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
-      if (lead) L.win[wp][g] = f32x2{yr, yi};
+      if (lead) L.win[wp][g] = L.win[wp + FMX_SS_SUB][g] = f32x2{yr, yi};
       if (ss_valid < FMX_SS_SUB) ss_valid++;
       const int w0 = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1; // oldest
       auto wat = [&](int m) __attribute__((always_inline)) {
         const int i = w0 + m;
-        return L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][g];
+        return L.win[i][g];
       };
       int ns = 0;
       f32x2 sym = f32x2{0.0f, 0.0f};
@@ -1938,7 +1949,11 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
           const f32x2 p = f32x2{h, h} * w;
           acm = acm + p;
         }
-        if (ns == 0) sym = f32x2{acm.x / 3.0f, acm.y / 3.0f};
+        // x / 3 as fmx_div_const (bit-identical for every normal x,
+        // tests/golden/divconst_exhaustive.json), the zero's sign restored
+        if (ns == 0)
+          sym = f32x2{copysignf(fmx_div_const(acm.x, 3.0f, 1.0f / 3.0f), acm.x),
+                      copysignf(fmx_div_const(acm.y, 3.0f, 1.0f / 3.0f), acm.y)};
         if (ss_decim == 1) {
           ss_decim = 0;
           const float *hd = L.dmf + ss_b * FMX_SS_SUB;
@@ -1971,9 +1986,17 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       if (ns == 1) {
         // ---- PSK2 modem phase error -> NCO PLL ----
         const float symr = sym.x, symi = sym.y;
-        float th = atan2f(symi, symr) - dphi_psk;
-        if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
-        const bool s1 = th > 0.0f;
+        // modem_demodulate (PSK2): th = atan2(symi, symr) - pi/2, wrapped
+        // below -pi; symbol 1 iff th > 0, i.e. iff the symbol lies left of
+        // the imaginary axis.  Away from the axis (|symr| > 1e-5 |symi|:
+        // the angle is >= 1e-5 from +-pi/2, far beyond atan2f's error) the
+        // sign of symr decides; on it the reference's arithmetic does
+        bool s1 = symr < 0.0f;
+        if (!(fabsf(symr) > 1e-5f * fabsf(symi))) {
+          float th = atan2f(symi, symr) - dphi_psk;
+          if ((double)th < -3.14159265358979323846) th = (float)((double)th + 2.0 * 3.14159265358979323846);
+          s1 = th > 0.0f;
+        }
         const float xr = s1 ? psk_xr1 : 1.0f, xi = s1 ? psk_xi1 : 0.0f;
         float pe = symi * xr - symr * xi;
         pe = d_clamp(pe, -kPiF, kPiF);
@@ -2028,7 +2051,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   out->agc_y2p = agc_y2p;
   for (int m = 0; m < FMX_SS_SUB; ++m) {
     const int i = wp + 1 + m;
-    const f32x2 w = L.win[(i >= FMX_SS_SUB) ? i - FMX_SS_SUB : i][g];
+    const f32x2 w = L.win[i][g];
     out->ss_win_re[m] = w.x;
     out->ss_win_im[m] = w.y;
   }
@@ -2301,7 +2324,6 @@ template <int M, int TPP>
 #endif
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  fe_next_sched_copy(a);
   using LY = Fe8Layout<M, TPP>;
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
@@ -2998,6 +3020,8 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
 #undef FE_STAMP_D
 #undef FE_STAMP_RAW
   if (want_sig) fe_signal_sums(a, sig, sgp, c, lane, wave, tid);
+  // at the end, where registers are free (at the entry it cost 28 VGPRs)
+  fe_next_sched_copy(a);
 }
 
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
@@ -3062,9 +3086,11 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  // shape: PllArgs::shape (0: 64 x 4, 1: 32 x 8), chosen by the handle (fmx_capi.cpp pll_shape)
+  // shape: PllArgs::shape (0: 64 x 4, 1: 32 x 8, 2: 16 x 16), chosen by the handle (fmx_capi.cpp pll_shape)
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (a.shape == 1)
+  if (a.shape == 2)
+    hipLaunchKernelGGL(pll16x16::k_pll, dim3((a.C + 15) / 16), dim3(64 * 7), 0, st, a);
+  else if (a.shape == 1)
     hipLaunchKernelGGL(pll32x8::k_pll, dim3((a.C + 31) / 32), dim3(64 * 7), 0, st, a);
   else
     hipLaunchKernelGGL(pll64x4::k_pll, dim3((a.C + 63) / 64), dim3(64 * 7), 0, st, a);

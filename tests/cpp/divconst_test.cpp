@@ -3,7 +3,8 @@
 // skipped) and each divisor the kernels use it for:
 //   cR = 0.040 - 0.022, cC = 0.18 - 0.11, cP = 320 - 180  (stereo blend target,
 //   stereo_decoder.cpp:142-147), 2 pi (PLL error Hz, :157), 57000 (RDS NCO
-//   quad-phase wrapper, liquid_wrappers.cpp:133).
+//   quad-phase wrapper, liquid_wrappers.cpp:133), 3 (RDS symsync output
+//   scale, liquid symsync_crcf, as k_rds restates it).
 // Prints JSON: per divisor the mismatches (all at |x| < 1e-30 -- "bad_ge_1e-30"
 // must be 0) among normal |x| <= 2^60 (and 0), the first few,
 // and whether every mismatch is a -0 / +0 sign (which the kernels absorb).
@@ -30,10 +31,10 @@ int main(int argc, char **argv) {
   // stride 1 = every bit pattern (exhaustive, ~3 min on 8 cores); the CPU
   // suite runs stride 7 (all exponents, a seventh of the mantissas)
   const long long stride = (argc > 1) ? std::atoll(argv[1]) : 1;
-  const float divs[5] = {0.040f - 0.022f, 0.18f - 0.11f, 320.0f - 180.0f, 2.0f * 3.14159265358979323846f, 57000.0f};
-  const char *names[5] = {"cR", "cC", "cP", "2pi", "57000"};
+  const float divs[6] = {0.040f - 0.022f, 0.18f - 0.11f, 320.0f - 180.0f, 2.0f * 3.14159265358979323846f, 57000.0f, 3.0f};
+  const char *names[6] = {"cR", "cC", "cP", "2pi", "57000", "3"};
   std::printf("{");
-  for (int d = 0; d < 5; ++d) {
+  for (int d = 0; d < 6; ++d) {
     const float c = divs[d];
     const float rc = 1.0f / c;
     unsigned long long bad = 0, zero_sign = 0, bad_ge = 0;

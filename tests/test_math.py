@@ -34,8 +34,8 @@ def test_near_clip_word_test_exhaustive(tmp_path):
 def test_div_const_matches_ieee_division(tmp_path):
     """fmx_div_const (the kernels' division by a constant) is bit-identical
     to IEEE x / c for every normal numerator 1e-30 <= |x| <= 2^60 and zero,
-    for the five divisors it is used with (blend target cR / cC / cP, PLL
-    error 2 pi, RDS quad-phase 57000).  Mismatches exist only below 1e-30
+    for the six divisors it is used with (blend target cR / cC / cP, PLL
+    error 2 pi, RDS quad-phase 57000, RDS symsync scale 3).  Mismatches exist only below 1e-30
     (residual underflow), where the kernels' numerators never are.  The
     exhaustive sweep (stride 1) is committed in tests/golden/divconst_exhaustive.json;
     this runs every 7th bit pattern."""
@@ -43,12 +43,13 @@ def test_div_const_matches_ieee_division(tmp_path):
     subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17", "-o", exe,
                     os.path.join(ROOT, "tests", "cpp", "divconst_test.cpp")], check=True, timeout=120)
     r = json.loads(subprocess.run([exe, "7"], check=True, capture_output=True, text=True, timeout=600).stdout)
-    for name in ("cR", "cC", "cP", "2pi", "57000"):
+    for name in ("cR", "cC", "cP", "2pi", "57000", "3"):
         assert r[name]["bad_ge_1e-30"] == 0, (name, r[name])
     with open(os.path.join(ROOT, "tests", "golden", "divconst_exhaustive.json")) as f:
         ex = json.load(f)
-    for name in ("cR", "cC", "cP", "2pi", "57000"):
+    for name in ("cR", "cC", "cP", "2pi", "57000", "3"):
         assert ex[name]["bad_ge_1e-30"] == 0 and ex[name]["max_bad_abs"] < 1e-30
+    assert ex["3"]["bad"] == 0  # division by 3: bit-identical for every normal numerator
 
 
 def test_pll_chain_sine_error_bounds(tmp_path):

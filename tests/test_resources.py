@@ -65,10 +65,13 @@ def test_front_end_register_budget(tmp_path):
 def test_pll_register_and_lds_budget(tmp_path):
     ks = _kernels(tmp_path)
     hits = _find(ks, r"k_pllENS_7PllArgs")
-    assert len(hits) == 2  # the two tile shapes (fmx_pll.inc)
+    assert len(hits) == 3  # the three tile shapes (fmx_pll.inc)
     for name, f in hits.items():
         assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 88, (name, f)
-        assert f.get("group_segment_fixed_size", 0) <= 36864, (name, f)
+        # LDS: the DMA tile rings (round 3) take 37.4 KB; two k_pll workgroups
+        # and a k_rds one still fit beside one k_fe8 workgroup (62.5 KB) in
+        # 160 KB (none fits beside two either way: 35 KB left)
+        assert f.get("group_segment_fixed_size", 0) <= 38 * 1024, (name, f)
         assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
 
 
