@@ -2291,8 +2291,10 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int XW = FMX_HIST + FE8_T + 32;
   static constexpr int MX = HX + FE_HALO_IQ * 8;                     // XH: f16 hi [XW]
   static constexpr int XLO = MX + XW * 2;                            // XL: f16 lo [XW]
-  static constexpr int TL = (XLO + XW * 2 + 15) & ~15;               // f32 [FMX_HIST]
-  static constexpr int TL32 = TL + FMX_HIST * 4;                     // f32 [32]
+  // (round 3: no f32 copy of the chunk's last FMX_HIST samples -- the call's
+  // last ones go straight to the history rows in HBM -- so that two k_fe8
+  // workgroups and a k_pll workgroup fit one CU's 160 KB)
+  static constexpr int TL32 = (XLO + XW * 2 + 15) & ~15;             // f32 [32]
   static constexpr int RS_PAIRS = FMX_NPFB + 1;                      // branch pairs (b, b+1), + the boundary pair
   static constexpr int RS_M = FMX_RDS_RS_SUB + 1;                    // 27 terms (leading / trailing zero)
   static constexpr int RST = (TL32 + 32 * 4 + 15) & ~15;             // RDS resampler bank [33][27] float2
@@ -2310,6 +2312,8 @@ template <int M, int TPP> struct Fe8Layout {
   // reaches the carried images, the resampler bank or the shared words
   static_assert(NPC_EARLY * 1024 <= UOFF, "early DMA pieces end below uc");
   static_assert(NPC * 1024 <= HX && HX <= MX && TL32 + 32 * 4 <= RST, "late DMA pieces end below the carried state");
+  // two k_fe8 workgroups beside a 32 x 8 k_pll workgroup (39168 B): 163840 B per CU
+  static_assert(M != 10 || 2 * BYTES + 39168 <= 163840, "two front ends and a k_pll workgroup per CU");
   static_assert(XIN + 4 * IQW * 2 <= YB && (IQW * 2) % 16 == 0 && (FE_HALO_IQ * 2) % 16 == 0,
                 "IQ images below yb, 16-B aligned rows");
 };
@@ -2331,7 +2335,6 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   float2 *hx = reinterpret_cast<float2 *>(smem + LY::HX);
   _Float16 *xh = reinterpret_cast<_Float16 *>(smem + LY::MX);  // MPX hi, index FMX_HIST + j
   _Float16 *xl = reinterpret_cast<_Float16 *>(smem + LY::XLO); // MPX lo
-  float *tl = reinterpret_cast<float *>(smem + LY::TL);         // the chunk's last FMX_HIST MPX samples
   float *tl32 = reinterpret_cast<float *>(smem + LY::TL32);     // the previous chunk's last 32
   f32x2(*rsb)[LY::RS_M] = reinterpret_cast<f32x2(*)[LY::RS_M]>(smem + LY::RST);
   float *uc = reinterpret_cast<float *>(smem + LY::UOFF); // uc[32 + j]: MPX sample j of the chunk
@@ -2835,7 +2838,6 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
         const _Float16 hv = (_Float16)m;
         xh[FMX_HIST + j] = hv;
         xl[FMX_HIST + j] = (_Float16)(m - (float)hv);
-        if (k >= (FE8_T - FMX_HIST) / 256) tl[j - (FE8_T - FMX_HIST)] = m;
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
       if (tid == 0) {
@@ -2855,9 +2857,12 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       }
     }
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
-    if (rds) { // unpadded copy for the RDS resampler: its own window history first
+    const bool last_chunk = n0 + FE8_T >= n;
+    if (rds || pilot) { // unpadded f32 copy: the RDS resampler's input (its own window history first), the history rows
 #pragma unroll
       for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
+    }
+    if (rds) {
       if (tid < 32) {
         uc[tid] = (n0 == 0) ? rds_keep : tl32[tid];
         uc[32 + FE8_T + tid] = 0.0f;
@@ -2908,6 +2913,23 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       }
       if (last >= 0) atomicMax(&sh->e_end, last + 1);
     }
+    if (!rds && pilot && last_chunk) __syncthreads(); // uc complete (the resampler's barrier otherwise)
+    // the call's last FMX_HIST samples: the next call's stereo history rows,
+    // its last 32 the next call's RDS resampler window (HBM); the chunk's last
+    // 32 the next chunk's window history (every read of tl32 for this chunk
+    // was before the "uc complete" barrier)
+    if (last_chunk) {
+      if (pilot) {
+        static_assert(FMX_HIST == 512, "two history words per thread");
+        const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.st_hist_wr + (size_t)c * FMX_HIST, FMX_HIST * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + FE8_T - FMX_HIST + tid]), rh,
+                                              4u * tid, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + FE8_T - 256 + tid]), rh,
+                                              4u * tid, 1024, 0);
+      }
+      if (rds && tid < 32) a.rds_hist[(size_t)c * 32 + tid] = uc[FE8_T + tid];
+    }
+    if (rds && tid < 32) tl32[tid] = uc[FE8_T + tid];
     __syncthreads(); // uc is dead: the rest of the next chunk may land (behind the pilot FIR)
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
     if (rds) e_pos = sh->e_end;
@@ -2958,16 +2980,13 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
     FE_STAMP(4)
     // ================= carry halos to the next chunk =================
     {
-      // the chunk's last FMX_HIST samples become the f16 images' history;
-      // its last 32 (f32) the next RDS window's history
+      // the chunk's last FMX_HIST samples become the f16 images' history
       static_assert(FMX_HIST == 2 * 256, "one f16 pair per thread");
       const uint32_t ch = reinterpret_cast<const uint32_t *>(xh)[FE8_T / 2 + tid];
       const uint32_t cl = reinterpret_cast<const uint32_t *>(xl)[FE8_T / 2 + tid];
-      const float t32 = (tid < 32) ? tl[FMX_HIST - 32 + tid] : 0.0f;
       __syncthreads();
       reinterpret_cast<uint32_t *>(xh)[tid] = ch;
       reinterpret_cast<uint32_t *>(xl)[tid] = cl;
-      if (tid < 32) tl32[tid] = t32;
       __syncthreads();
     }
   }
@@ -3002,14 +3021,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       a.agc[2 * c + 1] = agc_y2p;
     }
   }
-  if (pilot) {
-    float *hist = a.st_hist_wr + (size_t)c * FMX_HIST;
-    for (int h = tid; h < FMX_HIST; h += 256) hist[h] = tl[h];
-  }
-  if (rds) {
-    if (tid < 32) a.rds_hist[(size_t)c * 32 + tid] = tl[FMX_HIST - 32 + tid];
-    if (tid == 0) a.rds_count[c] = sched_n;
-  }
+  if (rds && tid == 0) a.rds_count[c] = sched_n;
   if (tid == 0 && a.clip_out) a.clip_out[c] = (float)sh->clip / (float)n;
   FE_STAMP(6)
 #ifdef FMX_STAMPS
