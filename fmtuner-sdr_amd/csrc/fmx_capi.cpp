@@ -121,6 +121,9 @@ struct Handle {
   // intermediates (double-buffered by step parity)
   float *mpx[FMX_NBUF] = {}, *pilot[FMX_NBUF] = {}, *rds_in[FMX_NBUF] = {};
   int *rds_count[FMX_NBUF] = {};
+  float *rds_win[FMX_NBUF] = {};  // [C][32] the previous call's last MPX samples, k_fe8 -> k_rs
+  hipEvent_t evR[FMX_NBUF] = {};  // after k_rs of the slot's step (it reads the RDS schedule slot)
+  bool evR_set[FMX_NBUF] = {};
   float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
   uint32_t block_index = 0;
@@ -601,7 +604,7 @@ static void destroy(Handle *h) {
   }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
-    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evR[b]})
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
@@ -760,6 +763,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rds_win[b], C * 32)) != FMX_OK) return rc;
+    HIP_TRY(hipEventCreateWithFlags(&h->evR[b], ev_flags(false)));
   }
   // construct every object (RS_CREATE) then apply main.cpp's configuration
   std::fill(h->hmask.begin(), h->hmask.end(), static_cast<int>(RS_CREATE));
@@ -931,8 +936,11 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if (rds && (rc = tset_take_or_advance(h, h->t_rds, n, buf, h->sA)) != FMX_OK) return rc;
   const int nbuf = (buf + 1) % FMX_NBUF;
   const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nbuf, static_cast<size_t>(h->C) * 256) : 0u;
+  // slot nbuf was last read by k_rs two steps ago (sC): the front end's copy waits for it
+  if (spec16 && h->evR_set[nbuf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evR[nbuf], 0));
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
+  bool use_rs = false;
   // ---- front end (sA) ----
   {
     FeArgs a = fe_args(h, n, h->M > 1 ? FE_IN_U8_DECIM : FE_IN_U8_DIRECT, buf);
@@ -949,6 +957,11 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.rds_out = h->rds_in[buf];
       a.rds_stride = h->rds_stride;
     }
+    // the RDS resampler of a k_fe8 step runs as k_rs (one schedule for the handle)
+    // (16 outputs' windows span <= 15 del + 31 samples: inside k_rs's 64 for del <= 2.1)
+    use_rs = rds && h->t_rds.G == 1 && h->hdes->rds_del <= 2.1f &&
+             frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
+    if (use_rs) a.rds_win_out = h->rds_win[buf];
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
     a.sig_sums = o->d_signal ? h->sig_sums[buf] : nullptr;
     if (spec16) {
@@ -970,6 +983,29 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC) ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
+  if (use_rs) {
+    RsArgs r{};
+    r.des = h->ddes;
+    r.C = h->C;
+    r.n = n;
+    r.mpx = mpx;
+    r.mpx_stride = mpx_stride;
+    r.win = h->rds_win[buf];
+    r.sched = h->t_rds.d_sched[h->t_rds.cur];
+    r.sched_n = h->t_rds.d_count[h->t_rds.cur];
+    r.group = h->t_rds.d_group[h->t_rds.cur];
+    r.sched_stride = h->t_rds.stride;
+    r.out = h->rds_in[buf];
+    r.out_stride = h->rds_stride;
+    // <= 24 output tiles per workgroup (k_rs RS_TMAX): 8 parts of 23 tiles at a 4096-sample block
+    r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + 23) / 24);
+    if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
+      h->err = "rds resampler launch failed";
+      return rc;
+    }
+    HIP_TRY(hipEventRecord(h->evR[buf], h->sC));
+    h->evR_set[buf] = true;
+  }
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;

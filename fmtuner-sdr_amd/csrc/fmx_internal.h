@@ -75,6 +75,9 @@ struct FeArgs {
   const int *rds_sched_n;    // [groups]
   const int *rds_group;      // [C]
   int rds_sched_stride;
+  // k_fe8 leaves the RDS resampler to k_rs: it writes the previous call's
+  // last 32 MPX samples here ([C][32]) instead of resampling (may be null)
+  float *rds_win_out;
   // the NEXT step's RDS schedule slot, copied by the first workgroups of this
   // launch from the mapped pinned image (fmx_capi.cpp process_block): no copy
   // kernel on the front end's stream between two front ends; n16 = 0: none
@@ -158,13 +161,33 @@ struct RdsArgs {
   int prio;                // raise the waves' issue priority (s_setprio)
 };
 
+// k_rs: the 240k -> 171k RDS resampler of a process_block step (liquid
+// resamp_rrrf, host timing schedule), 16 channels per workgroup on FP32 MFMA
+struct RsArgs {
+  const FmxDesign *des;
+  int C, n;
+  const float *mpx;     // this step's MPX rows (the front end's output)
+  int mpx_stride;
+  const float *win;     // [C][32] the previous call's last 32 MPX samples
+  const FmxSched *sched; // [groups][sched_stride]
+  const int *sched_n;   // [groups]
+  const int *group;     // [C]
+  int sched_stride;
+  float *out;           // RDS-rate rows
+  int out_stride;
+  int parts;            // workgroups per 16 channels (each a contiguous run of output tiles)
+};
+
 // launchers (fmx_kernels.hip); stream is a hipStream_t
 // vec: the caller guarantees every channel's decimator history is full
 // (dec_valid == L-1); 16-B row alignment is checked here.
 int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec = false);
+// whether launch_frontend_m would run k_fe8 for these arguments
+bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec);
 int launch_pll(const PllArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);
+int launch_rs(const RsArgs &a, void *stream);
 int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
                  const uint8_t *bits, uint8_t *out, size_t out_stride, void *stream);
 struct ResetArgs {

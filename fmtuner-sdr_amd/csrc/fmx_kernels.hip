@@ -2262,7 +2262,9 @@ __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
 typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
 
-template <int M, int TPP> struct Fe8Layout {
+// RS: the RDS resampler runs in k_fe8 (its pair bank in LDS); without it
+// (k_rs resamples) the layout is 7 KB smaller
+template <int M, int TPP, bool RS = true> struct Fe8Layout {
   static constexpr int L = M * TPP;
   static constexpr int G = (7 * M + L + 1 + 7) / 8;                 // 8-sample groups per thread window
   static constexpr int HB = 2 * L;                                   // halo bytes (L samples)
@@ -2298,7 +2300,7 @@ template <int M, int TPP> struct Fe8Layout {
   static constexpr int RS_PAIRS = FMX_NPFB + 1;                      // branch pairs (b, b+1), + the boundary pair
   static constexpr int RS_M = FMX_RDS_RS_SUB + 1;                    // 27 terms (leading / trailing zero)
   static constexpr int RST = (TL32 + 32 * 4 + 15) & ~15;             // RDS resampler bank [33][27] float2
-  static constexpr int SG = (RST + RS_PAIRS * RS_M * 8 + 15) & ~15;
+  static constexpr int SG = (RST + (RS ? RS_PAIRS * RS_M * 8 : 0) + 15) & ~15;
   static constexpr int SH = SG + 4 * 6 * 8;
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
@@ -2322,13 +2324,13 @@ template <int M, int TPP> struct Fe8Layout {
 // rounded up to 8k + 1 (up to 7 zero taps at the oldest end, same sums), so
 // every K step starts on an 8-sample boundary.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
-template <int M, int TPP>
+template <int M, int TPP, bool RS>
 #ifndef FE8_MINB
 #define FE8_MINB 1
 #endif
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  using LY = Fe8Layout<M, TPP>;
+  using LY = Fe8Layout<M, TPP, RS>;
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
@@ -2408,6 +2410,9 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   const float iqscale = D->iq_scale[par.iqsel];
   const bool pilot = a.pilot_out != nullptr;
   const bool rds = a.rds_out != nullptr;
+  // rs: the resampler runs here (else k_rs does it, from the MPX and the
+  // previous call's window this kernel hands over in rds_win_out)
+  const bool rs = RS && rds; // the launcher picks RS = false when rds_win_out is set
   const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
   const float dc_c = -dc_a1;
 
@@ -2453,6 +2458,9 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
     sched = a.rds_sched + (size_t)g * a.rds_sched_stride;
     sched_n = a.rds_sched_n[g];
     if (tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
+    if (!rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
+  }
+  if (rs) {
     // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
     // (boundary): branch 31 on the window, branch 0 on the window shifted by
     // one -- 27 terms, oldest sample first, so every lane runs one chain
@@ -2475,7 +2483,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   int e_pos = 0;
 
   for (int n0 = 0; n0 < n; n0 += FE8_T) {
-    if (rds && tid == 0) sh->e_end = e_pos;
+    if (rs && tid == 0) sh->e_end = e_pos;
     // ================= decimator =================
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
@@ -2849,7 +2857,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
     // RDS schedule entries of this chunk, fetched before the early DMA and the
     // resampler's window copy
     FmxSched en[8];
-    if (rds) {
+    if (rs) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int e = e_pos + tid + 256 * k;
@@ -2862,7 +2870,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
     }
-    if (rds) {
+    if (rs) {
       if (tid < 32) {
         uc[tid] = (n0 == 0) ? rds_keep : tl32[tid];
         uc[32 + FE8_T + tid] = 0.0f;
@@ -2870,7 +2878,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
     }
     FE_STAMP(3)
     // ================= RDS resampler 240k -> 171k =================
-    if (rds) {
+    if (rs) {
       __syncthreads(); // uc complete
       int last = -1;
 #pragma unroll
@@ -2913,7 +2921,7 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       }
       if (last >= 0) atomicMax(&sh->e_end, last + 1);
     }
-    if (!rds && pilot && last_chunk) __syncthreads(); // uc complete (the resampler's barrier otherwise)
+    if (!rs && last_chunk) __syncthreads(); // uc complete (the resampler's barrier otherwise)
     // the call's last FMX_HIST samples: the next call's stereo history rows,
     // its last 32 the next call's RDS resampler window (HBM); the chunk's last
     // 32 the next chunk's window history (every read of tl32 for this chunk
@@ -2929,10 +2937,10 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       }
       if (rds && tid < 32) a.rds_hist[(size_t)c * 32 + tid] = uc[FE8_T + tid];
     }
-    if (rds && tid < 32) tl32[tid] = uc[FE8_T + tid];
+    if (rs && tid < 32) tl32[tid] = uc[FE8_T + tid];
     __syncthreads(); // uc is dead: the rest of the next chunk may land (behind the pilot FIR)
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
-    if (rds) e_pos = sh->e_end;
+    if (rs) e_pos = sh->e_end;
     FE_STAMP(5)
     // ================= 19 kHz pilot band-pass =================
     if (pilot) {
@@ -3036,21 +3044,25 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   fe_next_sched_copy(a);
 }
 
-template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
+template <int M, int TPP, bool RS> static int fe8_launch_rs(const FeArgs &a, hipStream_t st) {
   // 160 KB per CU: two k_fe8 workgroups (512-B allocation granules) beside one
   // k_pll or k_rds workgroup (36 KB each, 36 864 B allocated)
-  static_assert(Fe8Layout<M, TPP>::BYTES <= (160 * 1024 - 36864) / 2, "k_fe8: two workgroups per CU plus a k_pll / k_rds workgroup");
-  static_assert(Fe8Layout<M, TPP>::UOFF >= Fe8Layout<M, TPP>::YB, "RDS copy above the IQ image");
-  const size_t smem = (size_t)Fe8Layout<M, TPP>::BYTES;
+  static_assert(Fe8Layout<M, TPP, RS>::BYTES <= (160 * 1024 - 36864) / 2, "k_fe8: two workgroups per CU plus a k_pll / k_rds workgroup");
+  static_assert(Fe8Layout<M, TPP, RS>::UOFF >= Fe8Layout<M, TPP, RS>::YB, "RDS copy above the IQ image");
+  const size_t smem = (size_t)Fe8Layout<M, TPP, RS>::BYTES;
   static bool configured = false;
   if (!configured) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fe8<M, TPP>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fe8<M, TPP, RS>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
       return FMX_E_HIP;
     configured = true;
   }
-  hipLaunchKernelGGL((k_fe8<M, TPP>), dim3(a.C), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((k_fe8<M, TPP, RS>), dim3(a.C), dim3(256), smem, st, a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+// the resampler in the kernel, or (rds_win_out set) left to k_rs
+template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
+  return (a.rds_out && a.rds_win_out) ? fe8_launch_rs<M, TPP, false>(a, st) : fe8_launch_rs<M, TPP, true>(a, st);
 }
 
 /* ================================================================== */
@@ -3074,16 +3086,25 @@ template <int M, int TPP, bool VEC> static int fe_launch(const FeArgs &a, hipStr
 // The decimation factor is a host-known constant of the handle; expose
 // explicit launchers so fmx_capi can pick the instantiation.
 namespace fmx {
+// steady state: whole 2048-sample chunks, full history, no complex
+// decimator output, 16-B pilot rows, RDS rate ratio < 0.9 (<= 8 resampler
+// outputs per thread and chunk) -> k_fe8
+static bool fe8_ok(const FeArgs &a, int M, bool vec) {
+  if (a.in_mode != FE_IN_U8_DECIM) return false;
+  vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
+  return vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
+         (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
+         a.des_fs >= 190000;
+}
+bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec) {
+  return fe8_ok(a, M, vec) && ((M == 10 && tpp == 28) || (M == 8 && tpp == 28) || (M == 4 && tpp == 20) ||
+                               (M == 2 && tpp == 12));
+}
 int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1, false>(a, st);
+  const bool fe8 = fe8_ok(a, M, vec);
   vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
-  // steady state: whole 2048-sample chunks, full history, no complex
-  // decimator output, 16-B pilot rows, RDS rate ratio < 0.9 (<= 8 resampler
-  // outputs per thread and chunk) -> k_fe8
-  const bool fe8 = vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
-                   (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
-                   a.des_fs >= 190000;
   if (fe8) {
     if (M == 10 && tpp == 28) return fe8_launch<10, 28>(a, st);
     if (M == 8 && tpp == 28) return fe8_launch<8, 28>(a, st);
@@ -3110,6 +3131,162 @@ int launch_pll(const PllArgs &a, void *stream) {
 }
 int launch_audio(const AudioArgs &a, void *stream) {
   hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+/* ================================================================== */
+/* k_rs: the RDS resampler 240k -> 171k (subcarrier.cpp:117-147) on MFMA */
+/* ================================================================== */
+/* Output e of a call is y_e = (1 - mu_e) y0_e + mu_e y1_e, with y0 / y1 the
+ * 27-term dot products of the MPX window x[s_e .. s_e + 26] (s_e = i_e - 25,
+ * one earlier at a boundary) with the entry's (branch, next branch) taps
+ * (the pair table k_fe8 used).  Every channel of a handle follows one RDS
+ * timing schedule (the RDS set is never reset per channel), so the windows
+ * of 16 consecutive outputs form one band matrix A (16 rows, 27 nonzero
+ * taps each) shared by all channels: v_mfma_f32_16x16x4f32 multiplies it,
+ * 4 columns per K step, with the MPX of 16 channels (B = 4 samples x 16
+ * channels).  FP32 products, sums in blocks of 4 (the reference sums
+ * sequentially; k_fe8's FMA chains it replaces differed the same way, by a
+ * few ulp).  One wave per workgroup; workgroup (x, y) takes channels
+ * 16 x .. 16 x + 15 and the y-th contiguous run of 16-output tiles.  With it,
+ * k_fe8 leaves out the resampler: a front end without it ran 0.777 against
+ * 0.847 ms per pipelined step (profiles/r03h_ab_lds_history_nors.txt). */
+#define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
+#define RS_TMAX 24 // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
+#define RS_XP 68   // padded window row: 16 channel rows 68 floats apart read conflict-free
+__global__ __launch_bounds__(64) void k_rs(RsArgs a) {
+  __shared__ float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
+  __shared__ FmxSched ssch[RS_TMAX * 16];
+  // the tile's MPX window [buffer][channel][sample - k0]: 15.3 KB in all, so
+  // a k_rs workgroup fits beside two k_fe8 and one k_pll workgroup on a CU
+  __shared__ __align__(16) float xs[2][16][RS_XP];
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x;
+  const int c0 = blockIdx.x * 16;
+  const FmxDesign *__restrict__ D = a.des;
+  // row b < 32: branch b on the window; row 32: branch 0 on the window
+  // shifted by one (the boundary pair's second branch)
+  for (int idx = lane; idx < (FMX_NPFB + 1) * (FMX_RDS_RS_SUB + 1); idx += 64) {
+    const int b = idx / (FMX_RDS_RS_SUB + 1), m = idx % (FMX_RDS_RS_SUB + 1);
+    const float *hs = D->rds_rs_h; // [branch][26]
+    float h;
+    if (b < FMX_NPFB) h = m < FMX_RDS_RS_SUB ? hs[b * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
+    else h = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
+    tab[b][m] = h;
+  }
+  const int g = a.group[c0]; // the handle's one schedule (fmx_capi.cpp launches k_rs only then)
+  const FmxSched *sched = a.sched + (size_t)g * a.sched_stride;
+  const int ns = a.sched_n[g];
+  const int ntile = (ns + 15) / 16;
+  const int per = (ntile + a.parts - 1) / a.parts;
+  const int ta = blockIdx.y * per, tb = min(ntile, ta + per);
+  // this workgroup's schedule entries (rows past the call repeat the last)
+  for (int idx = lane; idx < (tb - ta) * 16; idx += 64) ssch[idx] = sched[min(16 * ta + idx, ns - 1)];
+  __syncthreads();
+  const int r = lane & 15, kk = lane >> 4; // A: row r, K column kk; B: K row kk, channel column r
+  // window loads: lane (channel lc, quarter lq) moves samples k0 + 16 lq .. + 15
+  const int lc = lane >> 2, lq = lane & 3;
+  const int cl = c0 + lc;
+  const bool lcv = cl < a.C;
+  const float *mrow = a.mpx + (size_t)(lcv ? cl : c0) * a.mpx_stride; // mrow[k], 0 <= k < n
+  const float *wrow = a.win + (size_t)(lcv ? cl : c0) * 32 + 32;       // wrow[k], -32 <= k < 0
+  auto tile_k0 = [&](int T) __attribute__((always_inline)) {
+    const FmxSched e0 = ssch[16 * (T - ta)];
+    const int i0 = e0.packed & 0xFFFF;
+    return ((((e0.packed >> 24) & 1) ? i0 - 1 : i0) - (FMX_RDS_RS_SUB - 1)) & ~3;
+  };
+  // 16 samples of this lane's channel as four 16-B loads (4-sample groups lie
+  // wholly in the history, the block or past it: k0 and n are multiples of 4)
+  auto load_w = [&](int T, float4 (&v)[4]) __attribute__((always_inline)) {
+    const int k0 = tile_k0(T);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + 16 * lq + 4 * j;
+      // unconditional load (a branch here would make the compiler wait for it
+      // at the join); lanes past the block or the channels read mrow[0] and
+      // are zeroed when written to LDS
+      const float *p = (!lcv || k >= a.n) ? mrow : (k < 0 ? wrow + k : mrow + k);
+      v[j] = *reinterpret_cast<const float4 *>(p);
+    }
+  };
+  auto store_w = [&](int T, int buf, const float4 (&v)[4]) __attribute__((always_inline)) {
+    const int k0 = tile_k0(T);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = lcv && k0 + 16 * lq + 4 * j < a.n;
+      *reinterpret_cast<float4 *>(&xs[buf][lc][16 * lq + 4 * j]) =
+          ok ? v[j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  };
+  auto tile = [&](int T, int buf) __attribute__((always_inline)) {
+    const FmxSched en = ssch[16 * (T - ta) + r];
+    const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
+    const bool bnd = (en.packed >> 24) & 1;
+    const int s_r = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // the window's oldest sample
+    // pair (branch b, branch b + 1) on one window, or at the boundary branch
+    // 31 and branch 0 shifted by one
+    const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
+    const int k0 = tile_k0(T);
+    const int m0 = k0 + kk - s_r; // this lane's tap index at K step 0
+    // all operands first (LDS latency paid once), then 32 MFMAs back to back
+    f32x2 hv[RS_KS];
+    float xv[RS_KS];
+#pragma unroll
+    for (int st = 0; st < RS_KS; ++st) {
+      const int m = m0 + 4 * st;
+      const int mc = min(max(m, 0), FMX_RDS_RS_SUB);
+      hv[st] = f32x2{tab[row0][mc], tab[row1][mc]};
+      xv[st] = xs[buf][r][4 * st + kk];
+    }
+    f32x4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int st = 0; st < RS_KS; ++st) {
+      const int m = m0 + 4 * st;
+      const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(in ? hv[st].x : 0.0f, xv[st], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(in ? hv[st].y : 0.0f, xv[st], acc1, 0, 0, 0);
+    }
+    // D: lane (channel column r, output rows 4 kk .. 4 kk + 3); the
+    // reference's interpolation (1 - mu) y0 + mu y1
+    const int cb = c0 + r;
+    if (cb < a.C) {
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float mu = ssch[16 * (T - ta) + 4 * kk + q].mu;
+        const float w0f = (1.0f - mu) * acc0[q];
+        const float w1f = mu * acc1[q];
+        o[q] = w0f + w1f;
+      }
+      float *dst = a.out + (size_t)cb * a.out_stride + 16 * T + 4 * kk;
+      if (16 * T + 4 * kk + 3 < ns) {
+        *reinterpret_cast<float4 *>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (16 * T + 4 * kk + q < ns) dst[q] = o[q];
+      }
+    }
+  };
+  // tile T's window is loaded at tile T-2 (registers), written to LDS at the
+  // end of tile T-1: two register sets alternating (static indices)
+  float4 wa[4], wb[4];
+  if (ta < tb) load_w(ta, wa);
+  if (ta + 1 < tb) load_w(ta + 1, wb);
+  if (ta < tb) store_w(ta, 0, wa);
+  for (int T = ta; T < tb; T += 2) {
+    if (T + 2 < tb) load_w(T + 2, wa);
+    tile(T, 0);
+    if (T + 1 < tb) store_w(T + 1, 1, wb);
+    if (T + 1 < tb) {
+      if (T + 3 < tb) load_w(T + 3, wb);
+      tile(T + 1, 1);
+      if (T + 2 < tb) store_w(T + 2, 0, wa);
+    }
+  }
+}
+
+int launch_rs(const RsArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), 0, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_rds(const RdsArgs &a, void *stream) {
