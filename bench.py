@@ -50,13 +50,23 @@ ALG_FLOP_PER_IQ = 290.0
 # per-kernel DESIGN figures: HBM bytes the design moves
 # per IQ sample including its own intermediates (MPX, pilot, RDS-rate, raw
 # L/R), and the kernel's share of the 290 FLOP
+# The RDS stream runs the 240k -> 171k resampler (k_rs: MPX in, RDS-rate
+# samples out) before k_rds (RDS-rate samples in).
 PER_IQ = {
-    "frontend": (2.0 + 0.4 + 0.4 + 4.0 * 0.7125 / 10.0, 112.0 + 32.4 + 61.0 + 7.4),
+    "frontend": (2.0 + 0.4 + 0.4, 112.0 + 32.4 + 61.0),
     "stereo": (0.4 + 0.8 + 0.8, 20.0),
     "audio": (0.8 + 0.107, 48.0 + 3.0),
-    "rds": (4.0 * 0.7125 / 10.0, 15.0),
+    "rds": (0.4 + 2 * 4.0 * 0.7125 / 10.0, 15.0 + 7.4),
 }
-KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds"}
+KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rs+k_rds"}
+
+
+def pmc_bytes(pmc, k):
+    """Counted HBM bytes per launch of the kernel(s) behind timer k, or None."""
+    names = KNAME[k].split("+")
+    if not pmc or not all(n in pmc for n in names):
+        return None
+    return sum(pmc[n]["hbm_bytes_per_launch"] for n in names)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # dense FP32 VALU
 METRIC = "IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS) at 1/2/4/8 MI355X"
@@ -368,12 +378,10 @@ def main():
             pmc = None
     alg_bytes = ALG_BYTES_PER_IQ * units
     achieved = alg_bytes / dom_s / 1e9
-    traffic = None
-    if pmc and KNAME[dom] in pmc:
-        traffic = pmc[KNAME[dom]].get("hbm_bytes_per_launch")
+    traffic = pmc_bytes(pmc, dom)
     step_traffic = None
-    if pmc and all(KNAME[k] in pmc for k in avg):
-        step_traffic = sum(pmc[KNAME[k]]["hbm_bytes_per_launch"] for k in avg)
+    if all(pmc_bytes(pmc, k) is not None for k in avg):
+        step_traffic = sum(pmc_bytes(pmc, k) for k in avg)
     path_tflops = ALG_FLOP_PER_IQ * units / (ms_per_step * 1e-3) / 1e12
     roof = {"bound": "hbm", "kernel": KNAME[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -399,8 +407,8 @@ def main():
                "design_bytes_per_launch": bpi * units,
                "design_hbm_gbs": round(bpi * units / avg_s / 1e9, 1),
                "fp32_tflops": round(fpi * units / avg_s / 1e12, 3)}
-        if pmc and KNAME[k] in pmc:
-            pb = pmc[KNAME[k]]["hbm_bytes_per_launch"]
+        pb = pmc_bytes(pmc, k)
+        if pb is not None:
             ent["pmc_bytes_per_launch"] = pb
             ent["pmc_over_design"] = round(pb / (bpi * units), 3)
         kern[k] = ent

@@ -983,35 +983,35 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC) ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
-  if (use_rs) {
-    RsArgs r{};
-    r.des = h->ddes;
-    r.C = h->C;
-    r.n = n;
-    r.mpx = mpx;
-    r.mpx_stride = mpx_stride;
-    r.win = h->rds_win[buf];
-    r.sched = h->t_rds.d_sched[h->t_rds.cur];
-    r.sched_n = h->t_rds.d_count[h->t_rds.cur];
-    r.group = h->t_rds.d_group[h->t_rds.cur];
-    r.sched_stride = h->t_rds.stride;
-    r.out = h->rds_in[buf];
-    r.out_stride = h->rds_stride;
-    // <= 24 output tiles per workgroup (k_rs RS_TMAX): 8 parts of 23 tiles at a 4096-sample block
-    r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + 23) / 24);
-    if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
-      h->err = "rds resampler launch failed";
-      return rc;
-    }
-    HIP_TRY(hipEventRecord(h->evR[buf], h->sC));
-    h->evR_set[buf] = true;
-  }
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
-    KTimer t(h, FMX_K_RDS, h->sC);
+    KTimer t(h, FMX_K_RDS, h->sC);  // k_rs + k_rds: the RDS stream's live time
+    if (use_rs) {
+      RsArgs r{};
+      r.des = h->ddes;
+      r.C = h->C;
+      r.n = n;
+      r.mpx = mpx;
+      r.mpx_stride = mpx_stride;
+      r.win = h->rds_win[buf];
+      r.sched = h->t_rds.d_sched[h->t_rds.cur];
+      r.sched_n = h->t_rds.d_count[h->t_rds.cur];
+      r.group = h->t_rds.d_group[h->t_rds.cur];
+      r.sched_stride = h->t_rds.stride;
+      r.out = h->rds_in[buf];
+      r.out_stride = h->rds_stride;
+      // <= 24 output tiles per workgroup (k_rs RS_TMAX): 8 parts of 23 tiles at a 4096-sample block
+      r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + 23) / 24);
+      if (!FMX_SKIP(rds) && (rc = launch_rs(r, h->sC)) != FMX_OK) {
+        h->err = "rds resampler launch failed";
+        return rc;
+      }
+      HIP_TRY(hipEventRecord(h->evR[buf], h->sC));
+      h->evR_set[buf] = true;
+    }
     if (!FMX_SKIP(rds) && (rc = launch_rds(a, h->sC)) != FMX_OK) {
       h->err = "rds launch failed";
       return rc;

@@ -1005,11 +1005,11 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
  *                 integrator inputs (pilot * vco) * kI, the PLL frequency
  *                 (unwrap, clamp) and cos(2 phase)                  :176-199,219-221
  *   W1 (serial)   the four linear recurrences (pilot / MPX envelopes, the
- *                 pilot I/Q integrators) and |I, Q|^2; loads the MPX and
- *                 delay-line tiles                                  :172-177,196-200
- *   P target      tile k-3: blend target and the L/R matrix terms :120-166,201-225
- *   W3 (serial)   the blend recursion, the outputs, and the loads of the
- *                 pilot tiles (register-staged two iterations ahead) :227-234
+ *                 pilot I/Q integrators) and |I, Q|^2; issues the LDS-DMA of
+ *                 the pilot tiles (three ahead) and the MPX tiles :172-177,196-200
+ *   P target      tile k-3: blend target; each P wave also DMAs its items'
+ *                 delay-line MPX samples one iteration ahead     :120-166,201-208
+ *   W3 (serial)   the L/R matrix, the blend recursion, the outputs :209-234
  * At iteration k: W0 tile k, P phase k-1, W1 k-2, P target k-3, W3 k-4.
  * Waves w and w + 4 share a SIMD (tools/ubench/hwid.hip): SIMD 0 W0 + P2,
  * SIMD 1 W1 + W3, SIMD 2 P0 + P3, SIMD 3 P1.  Every value except the
@@ -1763,16 +1763,16 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     const int jj = idx / (FMX_RDS_NACC * 4), i = (idx / 4) % FMX_RDS_NACC, q = idx % 4;
     L.hq[jj][i][q] = (q < 3) ? D->rds_fir[FMX_RDS_DECIM - 1 - (jj + 8 * q) + FMX_RDS_DECIM * i] : 0.0f;
   }
-  if (lane < 5) {
-    const uint32_t words[5] = {0x0FC, 0x198, 0x168, 0x350, 0x1B4};
-    int idx = 0;
-    for (int bits = 1; bits <= 3; bits += 2)
-      for (uint32_t sh = 0; sh < 26; ++sh) {
-        const uint32_t e = ((uint32_t)bits << sh) & ((1u << 26) - 1u);
-        L.esyn[lane][idx] = bs_syndrome(e ^ words[lane]);
-        L.eerr[lane][idx] = e;
-        idx++;
-      }
+  // burst-error syndromes per offset word: entry idx < 26 a single-bit error
+  // at bit idx, idx >= 26 a two-bit burst at bit idx - 26 (all lanes; five
+  // serial lanes cost ~10 us at every launch)
+  for (int k = lane; k < 5 * 52; k += 64) {
+    const int w = k / 52, idx = k % 52;
+    const uint32_t word = w == 0 ? 0x0FCu : w == 1 ? 0x198u : w == 2 ? 0x168u : w == 3 ? 0x350u : 0x1B4u;
+    const uint32_t bits = idx < 26 ? 1u : 3u, sh = idx < 26 ? idx : idx - 26;
+    const uint32_t e = (bits << sh) & ((1u << 26) - 1u);
+    L.esyn[w][idx] = bs_syndrome(e ^ word);
+    L.eerr[w][idx] = e;
   }
   RdsBits &S = L.cold[g].s;
   const FmxRdsState G = act ? a.st[c] : FmxRdsState{}; // the compiler loads only the fields used
@@ -2324,11 +2324,17 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
 // rounded up to 8k + 1 (up to 7 zero taps at the oldest end, same sums), so
 // every K step starts on an 8-sample boundary.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
-template <int M, int TPP, bool RS>
 #ifndef FE8_MINB
 #define FE8_MINB 1
 #endif
+#ifndef FMX_FE_PRIO
+#define FMX_FE_PRIO 0 // k_fe8's issue priority (s_setprio); A/B variants only
+#endif
+template <int M, int TPP, bool RS>
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
+#if FMX_FE_PRIO
+  __builtin_amdgcn_s_setprio(FMX_FE_PRIO);
+#endif
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP, RS>;
   constexpr int L = LY::L;

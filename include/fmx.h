@@ -204,15 +204,18 @@ int fmx_memset(void *handle, void *d_ptr, int value, size_t bytes);
  * stream it runs on; fmx_kernel_times returns the summed milliseconds and
  * launch counts per kernel id since the last reset. */
 enum {
-  FMX_K_FRONTEND = 0, /* decimate + DC + IQ FIR + AGC + discriminator + pilot BPF + RDS resample */
+  FMX_K_FRONTEND = 0, /* decimate + DC + IQ FIR + AGC + discriminator + pilot BPF (+ RDS resample
+                         when process_block does not run it as its own kernel, k_rs)            */
   FMX_K_STEREO = 1,   /* pilot PLL + blend + L-R matrix (one lane per channel)                 */
   FMX_K_AUDIO = 2,    /* L/R 15 kHz FIRs + 32 kHz resampler + de-emphasis + DC + clamp         */
-  FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync + biphase + block sync                     */
+  FMX_K_RDS = 3,      /* (k_rs: 240k -> 171k resample +) 57 kHz BPSK demod + symsync + biphase +
+                         block sync: the RDS stream's kernels                                   */
   FMX_K_COUNT = 4
 };
 int fmx_timing_enable(void *handle, int enable);
-/* diagnostic: frontend per-stage clocks, 8 values (handle created with the
- * environment variable FMX_STAMPS=1; FMX_E_INVALID otherwise) */
+/* diagnostic: frontend per-stage clocks, 8 values (diagnostics library
+ * libfmx_diag.so, handle created with FMX_STAMPS=1 in the environment;
+ * FMX_E_INVALID otherwise -- the product libfmx.so reads no environment) */
 int fmx_debug_stamps(void *handle, unsigned long long *out, int n);
 int fmx_kernel_times(void *handle, double *ms, int *launches, int n);
 

@@ -25,7 +25,7 @@ if len(fe) > 4:
 # per kernel: mean duration and mean idle gap between consecutive launches
 import statistics
 print("kernel            n    dur_us   median gap_us (start[k+1] - end[k])")
-for key in ("k_fe8", "k_pll", "k_rds", "k_audio"):
+for key in ("k_fe8", "k_pll", "k_rs", "k_rds", "k_audio"):
     ks_ = [e for e in ev if key in e[2]]
     if len(ks_) < 3:
         continue
