@@ -1003,8 +1003,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       r.sched_stride = h->t_rds.stride;
       r.out = h->rds_in[buf];
       r.out_stride = h->rds_stride;
-      // <= 24 output tiles per workgroup (k_rs RS_TMAX): 8 parts of 23 tiles at a 4096-sample block
-      r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + 23) / 24);
+      // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
+      r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
       if (!FMX_SKIP(rds) && (rc = launch_rs(r, h->sC)) != FMX_OK) {
         h->err = "rds resampler launch failed";
         return rc;

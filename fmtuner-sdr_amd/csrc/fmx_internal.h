@@ -187,6 +187,9 @@ bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec);
 int launch_pll(const PllArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);
+#ifndef FMX_RS_TMAX
+#define FMX_RS_TMAX 24 // k_rs: output tiles (of 16) per workgroup at most; parts = ceil(tiles / FMX_RS_TMAX)
+#endif
 int launch_rs(const RsArgs &a, void *stream);
 int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
                  const uint8_t *bits, uint8_t *out, size_t out_stride, void *stream);

@@ -3157,7 +3157,7 @@ int launch_audio(const AudioArgs &a, void *stream) {
  * k_fe8 leaves out the resampler: a front end without it ran 0.777 against
  * 0.847 ms per pipelined step (profiles/r03h_ab_lds_history_nors.txt). */
 #define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
-#define RS_TMAX 24 // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
+#define RS_TMAX FMX_RS_TMAX // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
 #define RS_XP 68   // padded window row: 16 channel rows 68 floats apart read conflict-free
 __global__ __launch_bounds__(64) void k_rs(RsArgs a) {
   __shared__ float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
