@@ -1282,12 +1282,21 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       if (tid < AU_HALO) cx = X[au_xi(tid + cnt)];
       __syncthreads(); // X is read: F takes its place
       if (af && tid < AU_RHALO) F[tid] = S.fh[tid];
+      // the 8 outputs as four 16-B writes (8-B writes 64 B apart across the
+      // lanes met 8-way bank conflicts); F[AU_RHALO + 8 tid] is 16-B aligned
+      static_assert(AU_RHALO % 2 == 0 && AU2_PT == 8, "k_audio FIR output writes");
+      if (af && j0 + AU2_PT <= cnt) {
+        float4 *fw = reinterpret_cast<float4 *>(F + AU_RHALO + j0);
+#pragma unroll
+        for (int r = 0; r < AU2_PT; r += 2)
+          fw[r / 2] = make_float4(acc[r].x * sc, acc[r].y * sc, acc[r + 1].x * sc, acc[r + 1].y * sc);
+      }
 #pragma unroll
       for (int r = 0; r < AU2_PT; ++r) {
         const int j = j0 + r;
         if (j < cnt) {
           const float2 y = make_float2(acc[r].x * sc, acc[r].y * sc);
-          if (af) F[AU_RHALO + j] = y;
+          if (af && j0 + AU2_PT > cnt) F[AU_RHALO + j] = y;
           if (a.lr_out_l) {
             a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
             a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
