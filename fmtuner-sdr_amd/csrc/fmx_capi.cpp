@@ -957,9 +957,10 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.rds_out = h->rds_in[buf];
       a.rds_stride = h->rds_stride;
     }
-    // the RDS resampler of a k_fe8 step runs as k_rs (one schedule for the handle)
+    // the RDS resampler of a k_fe8 step runs as k_rs (MFMA tiles where a
+    // workgroup's 16 channels share one timing group, else per channel)
     // (16 outputs' windows span <= 15 del + 31 samples: inside k_rs's 64 for del <= 2.1)
-    use_rs = rds && h->t_rds.G == 1 && h->hdes->rds_del <= 2.1f &&
+    use_rs = rds && h->hdes->rds_del <= 2.1f &&
              frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
     if (use_rs) a.rds_win_out = h->rds_win[buf];
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;

@@ -3188,7 +3188,47 @@ __global__ __launch_bounds__(64) void k_rs(RsArgs a) {
     else h = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
     tab[b][m] = h;
   }
-  const int g = a.group[c0]; // the handle's one schedule (fmx_capi.cpp launches k_rs only then)
+  // channels of different timing groups in this workgroup (some of them
+  // reset since the others): one lane per (channel, output phase), 27-term
+  // dot products in the reference's order -- the MFMA tile needs one
+  // schedule for its 16 channel columns
+  {
+    const int cm = c0 + (lane & 15);
+    const int gm = cm < a.C ? a.group[cm] : a.group[c0];
+    if (__any(gm != a.group[c0])) {
+      __syncthreads(); // tab written
+      if (cm < a.C) {
+        const FmxSched *sc = a.sched + (size_t)gm * a.sched_stride;
+        const int nsm = a.sched_n[gm];
+        const int ntm = (nsm + 15) / 16, pm = (ntm + a.parts - 1) / a.parts;
+        const int e1 = min(nsm, 16 * (blockIdx.y * pm + pm));
+        const float *mrow = a.mpx + (size_t)cm * a.mpx_stride;
+        const float *wrow = a.win + (size_t)cm * 32 + 32;
+        float *orow = a.out + (size_t)cm * a.out_stride;
+#pragma unroll 1
+        for (int e = 16 * blockIdx.y * pm + (lane >> 4); e < e1; e += 4) {
+          const FmxSched en = sc[e];
+          const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
+          const bool bnd = (en.packed >> 24) & 1;
+          const int s0 = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // >= -27: inside the 32-sample history
+          const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
+          float y0 = 0.0f, y1 = 0.0f;
+#pragma unroll 1
+          for (int m = 0; m <= FMX_RDS_RS_SUB; ++m) {
+            const int k = s0 + m;
+            const float x = k < 0 ? wrow[k] : (k < a.n ? mrow[k] : 0.0f);
+            y0 = y0 + tab[row0][m] * x;
+            y1 = y1 + tab[row1][m] * x;
+          }
+          const float w0f = (1.0f - en.mu) * y0;
+          const float w1f = en.mu * y1;
+          orow[e] = w0f + w1f;
+        }
+      }
+      return;
+    }
+  }
+  const int g = a.group[c0]; // one schedule for the workgroup's 16 channels
   const FmxSched *sched = a.sched + (size_t)g * a.sched_stride;
   const int ns = a.sched_n[g];
   const int ntile = (ns + 15) / 16;

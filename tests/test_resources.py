@@ -80,3 +80,16 @@ def test_rds_fits_beside_two_front_ends(tmp_path):
     for name, f in _find(ks, r"5k_rdsE").items():
         assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 512 - 2 * 168, (name, f)
         assert f.get("vgpr_spill_count", 0) == 0, (name, f)
+
+
+def test_rs_fits_beside_two_front_ends_and_pll(tmp_path):
+    """k_rs (round 3) shares a CU with two k_fe8 (53.7 KB each) and one k_pll
+    (37.1 KB) workgroup: LDS <= 16 KB, and its wave fits a SIMD's registers
+    beside two front-end waves and a k_pll wave."""
+    ks = _kernels(tmp_path)
+    hits = _find(ks, r"4k_rsENS_6RsArgs")
+    assert len(hits) == 1
+    for name, f in hits.items():
+        assert f.get("group_segment_fixed_size", 0) <= 16 * 1024, (name, f)
+        assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 512 - 2 * 168 - 88, (name, f)
+        assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
