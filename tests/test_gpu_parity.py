@@ -250,6 +250,22 @@ def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
               pilot_tol=PILOT_UNLOCKED_TOL if narrow else 0, narrow=narrow)
 
 
+def test_rds_resampler_mixed_timing_groups(fmx, oracle, torch_cuda):
+    """k_rs (the 240k -> 171k RDS resampler of process_block) when the 16
+    channels of one MFMA workgroup sit in different timing groups: channels
+    3, 17 and 18 reset at different blocks put both workgroups of 20 channels
+    in two or three groups (per-channel path), while the other channels keep
+    their schedule; every channel against the oracle, RDS groups bit-exact."""
+    C, nblk = 20, 20
+    iq, _ = make_iq(fmx, 2, C, nblk, ch0=200)
+    resets = {5: 3, 8: 17, 11: 18}
+    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, resets=resets)
+    ngroups = 0
+    for c in range(C):
+        ngroups += len(check(g, outs[c], c, nblk, "rs_mixed")["groups_oracle"])
+    assert ngroups >= C
+
+
 def test_custom_deemphasis_and_deviation(fmx, oracle, torch_cuda):
     """setDeemphasis(tau_us) with any tau on both FMDemod and AFPostProcessor
     (fm_demod.cpp:50-62, af_post_processor.cpp:31-45: alpha = dt / (tau + dt),
