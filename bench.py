@@ -89,6 +89,8 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=None,
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc (tools/pmc_traffic.py); "
                          "default: the newest profiles/r*_pmc*.json")
+    ap.add_argument("--kernel-timing-every", type=int, default=2,
+                    help="time the kernel launches of every N-th timed step (roofline / kernels figures)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel HIP-event timing in the timed region (no roofline / kernels)")
     ap.add_argument("--no-signal-level", action="store_true",
@@ -310,7 +312,10 @@ def main():
         step(b)
     h.sync()
     groups_warm = int(gcnt.sum().item())
-    h.timing_enable(not args.no_kernel_timing)
+    # per-kernel live times from HIP events around the launches of every
+    # --kernel-timing-every-th timed step (a sample; timing all of them costs
+    # the step ~1.4 %: two event packets per kernel per stream)
+    h.timing_enable(not args.no_kernel_timing, every=args.kernel_timing_every)
     if world > 1:
         dist.barrier()
     h.sync()
@@ -443,6 +448,8 @@ def main():
         "realtime_channels_per_gpu": round(value / world / 2.4, 1),
         "roofline": roof,
         "kernels": kern,
+        "kernel_timing": None if args.no_kernel_timing else
+        f"HIP events around the launches of every {max(1, args.kernel_timing_every)}. timed step",
         "dominant_kernel": dom,
         "cpu_baseline": cpu,
         "scan": scan,

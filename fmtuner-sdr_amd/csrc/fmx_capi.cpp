@@ -130,6 +130,7 @@ struct Handle {
   TimingSet t_af, t_mono, t_rds;
   // kernel timing
   bool timing = false;
+  int timing_every = 1; // time the launches of every timing_every-th step (fmx_timing_enable)
 #if FMX_DIAG
   // diagnostics build only (make variant V=diag KDEFS=-DFMX_DIAG=1): kernels
   // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
@@ -185,15 +186,17 @@ struct KTimer {
   int k;
   hipStream_t s;
   hipEvent_t a = nullptr, b = nullptr;
-  KTimer(Handle *hh, int kk, hipStream_t ss) : h(hh), k(kk), s(ss) {
-    if (h->timing) {
+  bool on;
+  KTimer(Handle *hh, int kk, hipStream_t ss)
+      : h(hh), k(kk), s(ss), on(hh->timing && hh->step % static_cast<uint64_t>(hh->timing_every) == 0) {
+    if (on) {
       a = ev_get(h);
       b = ev_get(h);
       hipEventRecord(a, s);
     }
   }
   ~KTimer() {
-    if (h->timing) {
+    if (on) {
       hipEventRecord(b, s);
       h->pending.push_back({k, a, b});
     }
@@ -1542,6 +1545,7 @@ int fmx_timing_enable(void *handle, int enable) {
     collect_timing(h);
   }
   h->timing = enable != 0;
+  h->timing_every = enable > 1 ? enable : 1;
   // events for the timed region up front (creating them on the way stalls the host)
   while (h->timing && h->pool.size() < 256) {
     hipEvent_t e;

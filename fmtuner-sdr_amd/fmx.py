@@ -224,8 +224,9 @@ class Handle:
                                          C.c_void_p(d_bits), C.c_void_p(d_out), out_stride),
                  "fmx_synth_device")
 
-    def timing_enable(self, on=True):
-        self._ck(self.L.fmx_timing_enable(self.h, 1 if on else 0), "fmx_timing_enable")
+    def timing_enable(self, on=True, every=1):
+        """Per-kernel HIP-event timing; every=N times the launches of every N-th step only."""
+        self._ck(self.L.fmx_timing_enable(self.h, max(1, int(every)) if on else 0), "fmx_timing_enable")
 
     def kernel_times(self):
         ms = (C.c_double * 4)()

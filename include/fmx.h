@@ -212,6 +212,8 @@ enum {
                          block sync: the RDS stream's kernels                                   */
   FMX_K_COUNT = 4
 };
+/* enable: 0 off, 1 every step's launches, N > 1 the launches of every N-th
+ * step only (a sample: fewer event packets on the streams in the timed region) */
 int fmx_timing_enable(void *handle, int enable);
 /* diagnostic: frontend per-stage clocks, 8 values (diagnostics library
  * libfmx_diag.so, handle created with FMX_STAMPS=1 in the environment;
