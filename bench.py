@@ -89,7 +89,7 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=None,
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc (tools/pmc_traffic.py); "
                          "default: the newest profiles/r*_pmc*.json")
-    ap.add_argument("--kernel-timing-every", type=int, default=2,
+    ap.add_argument("--kernel-timing-every", type=int, default=1,
                     help="time the kernel launches of every N-th timed step (roofline / kernels figures)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel HIP-event timing in the timed region (no roofline / kernels)")
@@ -313,8 +313,9 @@ def main():
     h.sync()
     groups_warm = int(gcnt.sum().item())
     # per-kernel live times from HIP events around the launches of every
-    # --kernel-timing-every-th timed step (a sample; timing all of them costs
-    # the step ~1.4 %: two event packets per kernel per stream)
+    # --kernel-timing-every-th timed step (default: all of them; timing off
+    # altogether measured 0.772 against 0.782 ms, timing every 2nd step showed
+    # no gain over the run-to-run spread: profiles/r03x_kernel_timing.txt)
     h.timing_enable(not args.no_kernel_timing, every=args.kernel_timing_every)
     if world > 1:
         dist.barrier()
