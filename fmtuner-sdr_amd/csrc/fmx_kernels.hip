@@ -2336,14 +2336,8 @@ __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
 #ifndef FE8_MINB
 #define FE8_MINB 1
 #endif
-#ifndef FMX_FE_PRIO
-#define FMX_FE_PRIO 0 // k_fe8's issue priority (s_setprio); A/B variants only
-#endif
 template <int M, int TPP, bool RS>
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
-#if FMX_FE_PRIO
-  __builtin_amdgcn_s_setprio(FMX_FE_PRIO);
-#endif
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP, RS>;
   constexpr int L = LY::L;
