@@ -210,6 +210,13 @@ def cpu_baseline(fmx, d_iq, C, nblk, n_iq, B, seconds):
             **{k: info[k] for k in ("cpu_model", "nproc", "affinity", "cgroup_cpus")}}
 
 
+def _sha16(path):
+    """First 16 hex digits of a file's SHA-256 (the bench line's library record)."""
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main():
     args = parse()
     world, spawn = resolve_world(args)
@@ -458,6 +465,8 @@ def main():
                            "max": round(1e3 * max(host_call), 4)},
         "check": {"rds_groups_last_step": ngroups, "rds_groups_warmup": groups_warm,
                   "stereo_fraction": stereo_frac},
+        # the library this run loaded (fmx.LIB_PATH; FMX_LIB selects A/B builds)
+        "library": {"path": os.path.relpath(fmx.LIB_PATH, ROOT), "sha256_16": _sha16(fmx.LIB_PATH)},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

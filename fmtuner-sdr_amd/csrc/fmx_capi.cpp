@@ -136,7 +136,6 @@ struct Handle {
   // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
   bool skip_rds = false, skip_pll = false, skip_audio = false;
 #endif
-  int pll_shape = 0; // k_pll tile shape (pll_shape_for)
   struct Pending {
     int k;
     hipEvent_t a, b;
@@ -371,26 +370,6 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
   if (max_count) *max_count = mx;
   return FMX_OK;
 }
-// k_pll tile shape for a handle of n channels: 64
-// channels x 4 samples halves the workgroups beside k_fe8; 32 x 8 halves the
-// serial pipeline iterations per workgroup
-// issue priorities (s_setprio) of the latency-bound kernels beside k_fe8
-#ifndef FMX_PLL_PRIO
-#define FMX_PLL_PRIO 1
-#endif
-#ifndef FMX_RDS_PRIO
-#define FMX_RDS_PRIO 1
-#endif
-#ifndef FMX_PLL_SHAPE_BIG
-#define FMX_PLL_SHAPE_BIG 1   // handles of >= FMX_PLL_WIDE_MIN channels (r03f A/B at 4096 ch: 32 x 8
-                              // 0.841 ms/step, 64 x 4 0.854, 16 x 16 0.904: fewer iterations, and
-                              // 128 workgroups still leave most CUs two k_fe8 workgroups)
-#endif
-#ifndef FMX_PLL_SHAPE_SMALL
-#define FMX_PLL_SHAPE_SMALL 1 // smaller handles (r03zz A/B at 2048 ch, the Cfg4 8-GPU shard: 32 x 8
-                              // 0.501 ms/step, 16 x 16 0.509, 64 x 4 0.672)
-#endif
-static int pll_shape_for(int n) { return n >= FMX_PLL_WIDE_MIN ? FMX_PLL_SHAPE_BIG : FMX_PLL_SHAPE_SMALL; }
 static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   const size_t bytes = tset_sched_off(h, t) + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.G;
   // a copy kernel reading the mapped pinned image, not hipMemcpyAsync: the
@@ -671,10 +650,6 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   }
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') serial = true;
 #endif
-  h->pll_shape = pll_shape_for(n);
-#if FMX_DIAG
-  if (const char *e = std::getenv("FMX_PLL_SHAPE")) h->pll_shape = std::clamp(std::atoi(e), 0, 2);
-#endif
   if (serial) {
     h->sB = h->sC = h->sD = h->sA;
   } else {
@@ -756,7 +731,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->pilot[b], C * B)) != FMX_OK) return rc;
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
-    // octet tiles: whole groups of 8 channels
+    // pair tiles (whole groups of 2 channels); k_audio's XCD order reads octets
     if ((rc = dalloc(h, &h->lraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
   }
@@ -843,8 +818,8 @@ static void audio_signal_level(Handle *h, AudioArgs &a, const fmx_block_out *o, 
   a.sig_smooth = h->sig_smooth;
 }
 
-// raw L/R (k_pll -> k_audio) in octet tiles when the block is whole 4-sample tiles
-static int lr_tiled(const Handle *h) { return (h->cfg.block % 4 == 0) ? 1 : 0; }
+// raw L/R (k_pll -> k_audio) in pair tiles when the block is whole 16-sample tiles
+static int lr_tiled(const Handle *h) { return (h->cfg.block % 16 == 0) ? 1 : 0; }
 
 static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
   PllArgs a{};
@@ -863,8 +838,6 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
-  a.prio = FMX_PLL_PRIO; // s_setprio 2 beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
-  a.shape = h->pll_shape;
   return a;
 }
 
@@ -879,7 +852,6 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
-  a.prio = FMX_RDS_PRIO; // s_setprio 2 beside the front end's waves
   return a;
 }
 
@@ -1718,22 +1690,22 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
-    case 13: // k_fe8 i8 MFMA decimator taps back from the int8 digit fragments (row 0 lanes), as dec_taps_raw
+    case 13: // k_fe8 MFMA decimator taps back from the f16 hi/lo A fragments (row 0 lanes), as dec_taps_raw
       for (int k = 0; k < d->dec_len; ++k) {
         const int dd = d->dec_len - k;
-        const int ks = dd / 64, gg = (dd % 64) / 16, j = dd % 16, l = 16 * gg;
-        const long q = 65536L * d->dec_frag8[ks][0][l][j] + 256L * d->dec_frag8[ks][1][l][j] + d->dec_frag8[ks][2][l][j];
-        v.push_back(static_cast<float>(std::ldexp(static_cast<double>(q), -d->dec_s8) * 127.5));
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->dec_frag[ks][0][l][j]) + f16_value(d->dec_frag[ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 65536.0 * 127.5));
       }
       break;
-    case 9: { // the i8 decimator's rows 1..15 (lane l = row r): every row holds the same taps shifted by M r
+    case 9: { // the same fragments' rows 1..15 (lane l = 16 g + r): every row holds the taps shifted by M r
       const int M = d->M;
       for (int r = 0; r < 16; ++r)
         for (int k = 0; k < d->dec_len; ++k) {
           const int dd = d->dec_len - k + M * r;
-          const int ks = dd / 64, gg = (dd % 64) / 16, j = dd % 16, l = 16 * gg + r;
-          const long q = 65536L * d->dec_frag8[ks][0][l][j] + 256L * d->dec_frag8[ks][1][l][j] + d->dec_frag8[ks][2][l][j];
-          v.push_back(static_cast<float>(std::ldexp(static_cast<double>(q), -d->dec_s8) * 127.5));
+          const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg + r;
+          const double q = f16_value(d->dec_frag[ks][0][l][j]) + f16_value(d->dec_frag[ks][1][l][j]);
+          v.push_back(static_cast<float>(q / 65536.0 * 127.5));
         }
       break;
     }

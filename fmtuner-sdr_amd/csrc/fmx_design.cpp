@@ -220,36 +220,14 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     double dc = 0.0;
     for (int i = 0; i < d->dec_len; ++i) dc += static_cast<double>(d->dec_taps[i]);
     d->dec_dc = static_cast<float>(127.5 * dc);
-    // i8 MFMA decimator tables (k_fe8): integer taps, reversed, as three
-    // balanced int8 digits in the A-fragment layout
+    // f16 MFMA decimator tables (k_fe8): taps x 2^16, reversed, as f16 hi +
+    // lo in the A-fragment layout
     const int L = d->dec_len;
-    double tmax = 0.0;
-    for (int i = 0; i < L; ++i) tmax = std::max(tmax, std::fabs(static_cast<double>(d->dec_taps[i])));
-    int s8 = 0;
-    while (s8 < 62 && tmax * std::ldexp(1.0, s8 + 1) <= FMX_DEC_Q8_MAX) ++s8;
-    std::vector<long> qi(static_cast<size_t>(L));
-    long qsum = 0;
-    for (int i = 0; i < L; ++i) {
-      qi[static_cast<size_t>(i)] = std::lrint(std::ldexp(static_cast<double>(d->dec_taps[i]), s8));
-      qsum += qi[static_cast<size_t>(i)];
-    }
-    const int KS8 = (15 * M + L + 1 + 63) / 64;
-    if (KS8 > FMX_DEC_KS8_MAX) {
+    const int KS = (15 * M + L + 1 + 31) / 32;
+    if (KS > FMX_DEC_KS_MAX) {
       *err = "decimator too long for the MFMA fragment table";
       return FMX_E_INVALID;
     }
-    for (int ks = 0; ks < FMX_DEC_KS8_MAX; ++ks)
-      for (int l = 0; l < 64; ++l)
-        for (int j = 0; j < 16; ++j) {
-          const int dd = 64 * ks + 16 * (l >> 4) + j - M * (l & 15);
-          long q = (ks < KS8 && dd >= 1 && dd <= L) ? qi[static_cast<size_t>(L - dd)] : 0;
-          for (int dg = 2; dg >= 0; --dg) { // lo, mid, hi
-            const long digit = ((q + 128) & 255) - 128;
-            d->dec_frag8[ks][dg][l][j] = static_cast<int8_t>(digit);
-            q = (q - digit) / 256;
-          }
-        }
-    const int KS = (15 * M + L + 1 + 31) / 32;
     for (int ks = 0; ks < FMX_DEC_KS_MAX; ++ks)
       for (int l = 0; l < 64; ++l)
         for (int j = 0; j < 8; ++j) {
@@ -261,9 +239,6 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
         }
     d->dec_dc16 = static_cast<float>(-0.5 * 65536.0 * dc);
     d->dec_scale16 = d->dec_scale * (1.0f / 65536.0f);
-    d->dec_s8 = s8;
-    d->dec_dc8 = static_cast<float>(-0.5 * static_cast<double>(qsum));
-    d->dec_scale8 = static_cast<float>(static_cast<double>(d->dec_scale) * std::ldexp(1.0, -s8));
   } else {
     d->dec_scale = 1.0f;
     d->dec_dc = 0.0f;

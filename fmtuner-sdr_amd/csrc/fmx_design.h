@@ -26,9 +26,7 @@
 #define FMX_HIST 512         // stereo MPX history (>= pilot taps - 1 and delay line)
 #define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
-#define FMX_DEC_KS_MAX 16    // K steps of the f16 MFMA decimator (FMX_DEC_I8 0 builds): ceil((15 M + L + 1) / 32)
-#define FMX_DEC_KS8_MAX 8    // K steps of the i8 MFMA decimator: ceil((15 M + L + 1) / 64) for M <= 10
-#define FMX_DEC_Q8_MAX 8355711 // largest |tap| in three balanced base-256 int8 digits: 127 * (65536 + 256 + 1)
+#define FMX_DEC_KS_MAX 16    // K steps of the f16 MFMA decimator: ceil((15 M + L + 1) / 32)
 #define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
 #define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
 
@@ -50,20 +48,12 @@ typedef struct {
   float dec_taps_raw[FMX_MAX_DEC];
   float dec_poly[FMX_MAX_DEC]; // [p][q] = dec_taps[q*M + p]  (phase-major)
   float dec_pad[FMX_MAX_DEC + 2 * FMX_DEC_PAD]; // [FMX_DEC_PAD + k] = dec_taps[k], zeros around
-  // k_fe8's MFMA decimator (16 outputs x 16 blocks per v_mfma_i32_16x16x64_i8):
-  // integer taps q[d] = round(dec_taps[L - d] * 2^dec_s8) for d in [1, L] (0
-  // elsewhere; 2^dec_s8 the largest power of two keeping |q| <= FMX_DEC_Q8_MAX,
-  // 24 significant bits), as three balanced int8 digits q = 65536 hi + 256 mid
-  // + lo, laid out as the per-lane A fragments:
-  //   dec_frag8[ks][digit][l][j] = digit of q[64 ks + 16 (l >> 4) + j - M (l & 15)]
-  // The bytes enter as b - 128 (b ^ 0x80 as int8); with acc_digit the exact
-  // integer sums, y = (65536 acc_hi + (256 acc_mid + acc_lo) - dec_dc8) * dec_scale8,
-  // dec_dc8 = -sum(q) / 2 (the 127.5 centre), dec_scale8 = dec_scale * 2^-dec_s8.
-  int8_t dec_frag8[FMX_DEC_KS8_MAX][3][64][16] __attribute__((aligned(16)));
-  int dec_s8;
-  float dec_dc8, dec_scale8;
-  // the f16 form (FMX_DEC_I8 0 builds): q * 2^16 / 2^s8... as f16 hi + lo,
-  // dec_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - M (l & 15)]
+  // k_fe8's MFMA decimator (16 outputs x 16 blocks per v_mfma_f32_16x16x32_f16):
+  // q[d] = dec_taps[L - d] * 2^16 for d in [1, L] (0 elsewhere) as f16 hi + lo
+  // (22 significant bits), laid out as the per-lane A fragments
+  //   dec_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - M (l & 15)]
+  // y = (acc - dec_dc16) * dec_scale16, dec_dc16 = -2^16 sum(taps) / 2 (the
+  // 127.5 centre of the bytes entering as b - 128), dec_scale16 = dec_scale 2^-16
   uint16_t dec_frag[FMX_DEC_KS_MAX][2][64][8] __attribute__((aligned(16)));
   float dec_dc16, dec_scale16;
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain

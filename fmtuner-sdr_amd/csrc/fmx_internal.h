@@ -86,11 +86,6 @@ struct FeArgs {
   unsigned next_sched_n16;
 };
 
-// k_pll shape policy: handles of at least this many channels take the 64 x 4
-// tiles (fmx_capi.cpp pll_shape_for)
-#ifndef FMX_PLL_WIDE_MIN
-#define FMX_PLL_WIDE_MIN 4096
-#endif
 struct PllArgs {
   const FmxDesign *des;
   const FmxChanParam *par;
@@ -102,13 +97,11 @@ struct PllArgs {
   const float *st_hist_rd; // [C][FMX_HIST] history the frontend of this call read
   float *lraw, *rraw;
   int lr_stride;
-  int lr_tiled;            // raw L/R in octet tiles (lr_tile_idx, fmx_kernels.hip), else [C][lr_stride]
+  int lr_tiled;            // raw L/R in pair tiles (lr_tile_idx, fmx_kernels.hip), else [C][lr_stride]
   FmxStereoState *st;
   int *stereo_out, *pilot_tenths_out;
   int *indicator_out;      // [C] XDR stereo indicator (main.cpp:1298-1300), may be null
   unsigned long long *dbg; // [16] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
-  int prio;                // raise the waves' issue priority (s_setprio)
-  int shape;               // tile shape: 0 = 64 channels x 4 samples, 1 = 32 x 8 (launch_pll)
 };
 
 struct AudioArgs {
@@ -118,7 +111,7 @@ struct AudioArgs {
   int cap;
   const float *in_l, *in_r;
   int in_stride;
-  int in_tiled;    // in_l / in_r in octet tiles (raw L/R from k_pll), else [C][in_stride]
+  int in_tiled;    // in_l / in_r in pair tiles (raw L/R from k_pll), else [C][in_stride]
   float *out_l, *out_r;
   int out_stride;
   int *out_count;
@@ -158,7 +151,6 @@ struct RdsArgs {
   int *group_count;
   uint32_t block_index;
   unsigned long long *dbg; // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
-  int prio;                // raise the waves' issue priority (s_setprio)
 };
 
 // k_rs: the 240k -> 171k RDS resampler of a process_block step (liquid

@@ -86,19 +86,21 @@ __device__ __forceinline__ float d_clamp(float v, float lo, float hi) {
 }
 
 /* ------------------------------------------------------------------ */
-// Raw L/R between k_pll and k_audio in octet tiles: sample t of channel c at
-// ((c / 8) * (stride / 4) + t / 4) * 32 + (c % 8) * 4 + t % 4, i.e. one
-// 128-B line holds 4 consecutive samples of 8 consecutive channels.  k_pll's
-// lane = channel stores of a 4-sample tile then write whole lines (with one
-// row per channel every store instruction wrote a 16-B piece of 64 lines,
-// and HBM saw ~1.8x the bytes); stride % 4 == 0.
+// Raw L/R between k_pll and k_audio in pair tiles: sample t of channel c at
+// ((c / 2) * (stride / 16) + t / 16) * 32 + (c % 2) * 16 + t % 16, i.e. one
+// 128-B line holds 16 consecutive samples of 2 consecutive channels.  A
+// k_pll P wave holds 4 channel rows x 16 samples, so each of its store
+// instructions writes 2 whole lines; k_audio's loads read 64-B pieces
+// (round 2-3: octet tiles of 4 samples x 8 channels for the one-lane-per-
+// channel W3; with one row per channel every store instruction wrote a 16-B
+// piece of 64 lines and HBM saw ~1.8x the bytes); stride % 16 == 0.
 __device__ __forceinline__ size_t lr_tile_idx(int c, int t, int stride) {
-  return ((size_t)(c >> 3) * (size_t)(stride >> 2) + (size_t)(t >> 2)) * 32 + (size_t)((c & 7) * 4 + (t & 3));
+  return ((size_t)(c >> 1) * (size_t)(stride >> 4) + (size_t)(t >> 4)) * 32 + (size_t)((c & 1) * 16 + (t & 15));
 }
 // k_audio's block -> channel order for tiled input: blocks b and b + 8 share
 // an XCD (observed round-robin dispatch, MI355X_MICROARCH.md "Workgroup
-// dispatch"), so the 8 channels of one octet go to blocks 8 apart and their
-// reads of each shared line hit that XCD's L2 after the first.  Channels past
+// dispatch"), so the 8 channels of one octet (4 line pairs) go to blocks 8
+// apart and their reads of each shared line hit that XCD's L2 after the first.  Channels past
 // the last whole 64 keep b -> b.  Placement only: any order is correct.
 __device__ __forceinline__ int au_channel(int b, int C, bool tiled) {
   if (!tiled || b >= (C & ~63)) return b;
@@ -991,42 +993,36 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 /* ================================================================== */
 /* k_pll: StereoDecoder per-sample recurrences                         */
 /* ================================================================== */
-/* k_pll is a seven-wave software pipeline over tiles of PLL_T samples for
- * PLL_CH channels (PLL_CH x PLL_T = 256 items per tile).  Serial waves hold
- * one channel per lane (lanes >= PLL_CH idle); the P waves hold one item
- * (row, t) of a tile per lane (items 64 p .. 64 p + 63, row = item / PLL_T,
- * t = item % PLL_T) and run two stages per iteration:
+/* k_pll (round 4): only the two recurrences the reference makes serial stay
+ * serial, one channel per lane; everything else runs one item (channel row,
+ * sample t) per lane.  A workgroup takes PLL_CH = 16 channels in tiles of
+ * PLL_T = 16 samples (256 items: one 16-lane DPP row per channel in each of
+ * the four P waves), so 2 048 channels are 128 workgroups and 4 096 are 256:
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
- *                 pll_step, step; it hands the NCO words on       stereo_decoder.cpp:178-186
- *   P phase       tile k-1: v_sin / v_cos of each word, the float phase of
- *                 the word (the reference's phase()), the previous
- *                 sample's values from the lane before (t = 0: the row's
- *                 t = PLL_T - 1 of the previous iteration); the pilot I/Q
- *                 integrator inputs (pilot * vco) * kI, the PLL frequency
- *                 (unwrap, clamp) and cos(2 phase)                  :176-199,219-221
- *   W1 (serial)   the four linear recurrences (pilot / MPX envelopes, the
- *                 pilot I/Q integrators) and |I, Q|^2; issues the LDS-DMA of
- *                 the pilot tiles (three ahead) and the MPX tiles :172-177,196-200
- *   P target      tile k-3: blend target; each P wave also DMAs its items'
- *                 delay-line MPX samples one iteration ahead     :120-166,201-208
- *   W3 (serial)   the L/R matrix, the blend recursion, the outputs :209-234
- * At iteration k: W0 tile k, P phase k-1, W1 k-2, P target k-3, W3 k-4.
- * Waves w and w + 4 share a SIMD (tools/ubench/hwid.hip): SIMD 0 W0 + P2,
- * SIMD 1 W1 + W3, SIMD 2 P0 + P3, SIMD 3 P1.  Every value except the
- * chain's sine / NCO constrain and the outputs' sines (below) is computed
- * with the reference's arithmetic in the reference's order; only WHERE it
- * runs moved.
- *
- * Round 3: the chain's NCO constrain is fract(err * beta/2pi) * 2^32 in f32
- * and its sine v_sin_f32 of the word in turns (tools/ubench/chainlat.hip:
- * 147 -> 72 ticks per sample); the outputs' sine / cosine are v_sin /
- * v_cos of the word (the reference takes cos / sin of the word's float
- * phase: |difference| <= 5e-7); the per-sample frequency, cos(2 phase) and
- * I/Q products moved off the serial W1.  The tile shape is a build switch
- * (PLL_CH channels x PLL_T samples, 256 items): 32 x 8 halves the pipeline
- * iterations (each costs a barrier and an LDS round trip) and runs 0.45 ms
- * alone against 0.60 for 64 x 4, but occupies twice the CUs beside k_fe8,
- * which the pipelined step pays for. */
+ *                 pll_step, step; hands the NCO words on        stereo_decoder.cpp:178-192
+ *   P stage A     tile k-1: v_sin / v_cos / float phase of each word, the
+ *                 previous sample's by DPP row_ror:1 (t = 0: the previous
+ *                 tile's t = 15); PLL frequency (unwrap, clamp), cos(2 phase),
+ *                 the pilot I/Q integrator inputs; the four linear recurrences
+ *                 x = kS x + u (pilot / MPX envelopes, pilot I / Q) as a
+ *                 16-lane inclusive scan (DPP row_shr 1, 2, 4, 8 with kS^d)
+ *                 plus kS^(t+1) times the row's carry (ds_bpermute of the
+ *                 tile's last sample); |I, Q|^2 and the blend target  :120-205
+ *   WB (serial)   the blend smoother (attack / release select)   :226-228
+ *   P stage B     tile k-3: the L/R matrix from the delayed MPX and cos(2
+ *                 phase) with the blend, the raw L/R stores      :207-231
+ * The P waves also move the pilot (3 tiles ahead), MPX and delay-line (1
+ * ahead) words into LDS by per-lane LDS-DMA with counted waits.  At
+ * iteration k: W0 tile k, A k-1, WB k-2, B k-3.  The chain's sine / NCO
+ * constrain are v_sin of the word in turns and an f32 fract (round 3:
+ * tools/ubench/chainlat.hip, 72 ticks per sample); the outputs' sine / cosine
+ * are v_sin / v_cos of the word (the reference takes cos / sin of the word's
+ * float phase: |difference| <= 5e-7); the scans sum the recurrences' terms in
+ * a tree instead of one sample at a time (relative differences of a few
+ * ulp).  Round 3's seven-wave form kept the envelopes / integrators (W1) and
+ * the matrix + blend + stores (W3) in one-lane-per-channel waves, which set
+ * its pace (W3 1.73 M, W1 1.67 M, the W0 chain 0.99 M ticks per launch-WG)
+ * and gave 2 048 channels only 64 workgroups. */
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
@@ -1041,30 +1037,7 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
   *c = __builtin_amdgcn_cosf(r);
 }
 
-// k_pll in two tile shapes (fmx_pll.inc): 64 channels x 4 samples (half the
-// workgroups, fewer CUs beside k_fe8) and 32 channels x 8 samples (half the
-// pipeline iterations, twice the workgroups); launch_pll picks per handle.
-namespace pll64x4 {
-#define PLL_CH 64
-#define PLL_T 4
 #include "fmx_pll.inc"
-#undef PLL_CH
-#undef PLL_T
-} // namespace pll64x4
-namespace pll32x8 {
-#define PLL_CH 32
-#define PLL_T 8
-#include "fmx_pll.inc"
-#undef PLL_CH
-#undef PLL_T
-} // namespace pll32x8
-namespace pll16x16 {
-#define PLL_CH 16
-#define PLL_T 16
-#include "fmx_pll.inc"
-#undef PLL_CH
-#undef PLL_T
-} // namespace pll16x16
 
 /* ================================================================== */
 /* k_audio: L/R FIRs, 32 kHz resampler, de-emphasis, DC block, clamp  */
@@ -1211,7 +1184,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   const bool tiled = a.in_tiled != 0;
   const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
   const float *inr = mono ? nullptr : a.in_r + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
-  auto ti = [&](int j) __attribute__((always_inline)) { return tiled ? (j >> 2) * 32 + (j & 3) : j; };
+  auto ti = [&](int j) __attribute__((always_inline)) { return tiled ? (j >> 4) * 32 + (j & 15) : j; };
   const float sc = D->lr_scale;
   // retune fade/mute of this call (main.cpp:1310-1337): outputs o < mrem
   // get the gain of position (mtot - mrem) + o of the fade-out/mute/fade-in
@@ -1735,8 +1708,7 @@ __device__ __forceinline__ float rds_sum8(float x) {
 }
 
 __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
-  if (a.prio == 3) __builtin_amdgcn_s_setprio(3);
-  else if (a.prio) __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(2); // beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
   // dynamic LDS (sizeof(RdsLds) at launch): with a static size the backend
   // sees an LDS-limited occupancy and pads every wave's register allocation
   // up to it
@@ -2261,9 +2233,6 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * ~58 KB of LDS per workgroup: two workgroups (8 waves) per CU leave room
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
-#ifndef FMX_DEC_I8
-#define FMX_DEC_I8 0
-#endif
 #ifndef FMX_DEC_UNROLL
 #define FMX_DEC_UNROLL 1
 #endif
@@ -2519,84 +2488,6 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
     FE_STAMP_D(1)
     float2 xv[8]; // decimator outputs of this thread
     {
-#if FMX_DEC_I8
-      // Decimator as v_mfma_i32_16x16x64_i8 tiles.  Output o = 16 B + r of
-      // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
-      // [M r + 1, M r + L], with tap L + M r - t: per block, Y[r] = sum_t
-      // T[r][t] X[t] with T[r][t] = q[t - M r] -- one 16 x 16 tile is 16
-      // outputs (rows, A = taps) of 16 blocks (columns, B = bytes), K = the
-      // block's 15 M + L + 1 input samples in steps of 64.  The bytes enter
-      // as they are (b ^ 0x80 is b - 128 as int8: one v_perm per 4 samples
-      // of a component and one xor per word, no conversion), the taps as the
-      // three int8 digits of q = tap * 2^s (FmxDesign::dec_frag8, 24
-      // significant bits); per component three i32 accumulators hold EXACT
-      // sums, combined once per output.  Each wave runs two tiles (512
-      // outputs); the C layout gives each lane 4 consecutive outputs, which
-      // reach the 8-per-thread layout of the stages below through LDS.
-      typedef int i32x4_t __attribute__((ext_vector_type(4)));
-      constexpr int KS8 = (15 * M + L + 1 + 63) / 64;
-      static_assert(KS8 <= FMX_DEC_KS8_MAX, "decimator K steps");
-      static_assert(32 * M * 111 + 96 + 512 * M + 128 * (KS8 - 1) + 32 <= LY::RAW_ALLOC, "decimator reads inside raw");
-      const int col = lane & 15, g = lane >> 4;
-      // A fragments (16 B per lane and digit) from the design, one K step ahead
-      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag8[0][0][0][0]) + lane;
-      const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 32 * g;
-      // the two tiles one after the other (24 accumulator VGPRs live, not 48);
-      // each tile's outputs are combined to f32 right away: 256 mid + lo fits
-      // int32 (|acc| <= 128 * 280 * 128), 65536 hi is exact in f32
-      const float dc = D->dec_dc8, sc = D->dec_scale8;
-      float yr[2][4], yi[2][4];
-#pragma unroll 1
-      for (int u = 0; u < 2; ++u) {
-        i32x4_t acc[2][3]; // [I, Q][hi, mid, lo digit]
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int dg = 0; dg < 3; ++dg) acc[q][dg] = i32x4_t{0, 0, 0, 0};
-        u32x4 fh = fa[0], fm = fa[64], fl = fa[128];
-        const unsigned char *ru = rb + 512 * M * u;
-#pragma unroll FMX_DEC_UNROLL
-        for (int ks = 0; ks < KS8; ++ks) {
-          const i32x4_t ah = __builtin_bit_cast(i32x4_t, fh), am = __builtin_bit_cast(i32x4_t, fm),
-                        al = __builtin_bit_cast(i32x4_t, fl);
-          if (ks + 1 < KS8) {
-            fh = fa[192 * (ks + 1)];
-            fm = fa[192 * (ks + 1) + 64];
-            fl = fa[192 * (ks + 1) + 128];
-          }
-          // 16 samples (32 bytes I0 Q0 I1 Q1 ...) of this lane's column
-          const u32x4 w0 = *reinterpret_cast<const u32x4 *>(ru + 128 * ks);
-          const u32x4 w1 = *reinterpret_cast<const u32x4 *>(ru + 128 * ks + 16);
-          const uint32_t w[8] = {w0.x ^ 0x80808080u, w0.y ^ 0x80808080u, w0.z ^ 0x80808080u, w0.w ^ 0x80808080u,
-                                 w1.x ^ 0x80808080u, w1.y ^ 0x80808080u, w1.z ^ 0x80808080u, w1.w ^ 0x80808080u};
-          i32x4_t bi, bq;
-#pragma unroll
-          for (int d4 = 0; d4 < 4; ++d4) {
-            bi[d4] = (int)__builtin_amdgcn_perm(w[2 * d4 + 1], w[2 * d4], 0x06040200u);
-            bq[d4] = (int)__builtin_amdgcn_perm(w[2 * d4 + 1], w[2 * d4], 0x07050301u);
-          }
-          acc[0][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bi, acc[0][0], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bq, acc[1][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(am, bi, acc[0][1], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(am, bq, acc[1][1], 0, 0, 0);
-          acc[0][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bi, acc[0][2], 0, 0, 0);
-          acc[1][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bq, acc[1][2], 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float vi = (float)acc[0][0][i] * 65536.0f + (float)(acc[0][1][i] * 256 + acc[0][2][i]);
-          const float vq = (float)acc[1][0][i] * 65536.0f + (float)(acc[1][1][i] * 256 + acc[1][2][i]);
-          // u is uniform: select, not a dynamic register index
-          if (u == 0) {
-            yr[0][i] = (vi - dc) * sc;
-            yi[0][i] = (vq - dc) * sc;
-          } else {
-            yr[1][i] = (vi - dc) * sc;
-            yi[1][i] = (vq - dc) * sc;
-          }
-        }
-      }
-#else
       // Decimator as v_mfma_f32_16x16x32_f16 tiles.  Output o = 16 B + r of
       // the chunk (block B, r < 16) uses raw samples 16 M B + t, t in
       // [M r + 1, M r + L], with tap L + M r - t: per block, Y[r] = sum_t
@@ -2651,19 +2542,9 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
           acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bq, acc[u][1], 0, 0, 0);
         }
       }
-#endif
       FE_STAMP_D(2)
       __syncthreads(); // every wave is past raw: its outputs go to the (aliased) staging area
       float4 *stg = reinterpret_cast<float4 *>(smem + LY::STG);
-#if FMX_DEC_I8
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
-        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g;
-        stg[o / 2] = make_float4(yr[u][0], yi[u][0], yr[u][1], yi[u][1]);
-        stg[o / 2 + 1] = make_float4(yr[u][2], yi[u][2], yr[u][3], yi[u][3]);
-      }
-#else
       const float dc = D->dec_dc16, sc = D->dec_scale16;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -2678,7 +2559,6 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
         stg[o / 2] = make_float4(yr[0], yi[0], yr[1], yi[1]);
         stg[o / 2 + 1] = make_float4(yr[2], yi[2], yr[3], yi[3]);
       }
-#endif
       __syncthreads();
       int myclip = 0;
 #pragma unroll
@@ -3128,14 +3008,7 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  // shape: PllArgs::shape (0: 64 x 4, 1: 32 x 8, 2: 16 x 16), chosen by the handle (fmx_capi.cpp pll_shape)
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (a.shape == 2)
-    hipLaunchKernelGGL(pll16x16::k_pll, dim3((a.C + 15) / 16), dim3(64 * 7), 0, st, a);
-  else if (a.shape == 1)
-    hipLaunchKernelGGL(pll32x8::k_pll, dim3((a.C + 31) / 32), dim3(64 * 7), 0, st, a);
-  else
-    hipLaunchKernelGGL(pll64x4::k_pll, dim3((a.C + 63) / 64), dim3(64 * 7), 0, st, a);
+  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_audio(const AudioArgs &a, void *stream) {

@@ -246,10 +246,11 @@ def test_unlocked_pilot_level_is_chaotic(fmx, oracle):
 
 @pytest.mark.parametrize("rates", CONFIGS)
 def test_mfma_decimator_tap_tables(fmx, rates):
-    """k_fe8's i8 MFMA decimator takes the decimator taps as integers (x 2^s,
-    24 significant bits) in three balanced int8 digits, laid out as per-lane
-    A fragments (FmxDesign::dec_frag8): row 0 and every row r = 1..15
-    (shifted by M r) give the float taps back to 2^-21 of the largest."""
+    """k_fe8's MFMA decimator takes the decimator taps as f16 hi + lo pairs
+    (x 2^16, 22 significant bits), laid out as per-lane A fragments
+    (FmxDesign::dec_frag, the table the shipped k_fe8 reads): row 0 and every
+    row r = 1..15 (shifted by M r) give the float taps back to 2^-21 of the
+    largest."""
     if rates["iq_rate"] == rates["dsp_rate"]:
         pytest.skip("no decimator")
     cfg = fmx.make_config(**rates)
