@@ -1023,12 +1023,6 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
  * the matrix + blend + stores (W3) in one-lane-per-channel waves, which set
  * its pace (W3 1.73 M, W1 1.67 M, the W0 chain 0.99 M ticks per launch-WG)
  * and gave 2 048 channels only 64 workgroups. */
-__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
 // sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
 // which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
 __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) {
@@ -1810,15 +1804,17 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   uint32_t thp = theta - (uint32_t)(FMX_RDS_DECIM - 1 - o0) * dtheta;
   int nq = 0;
   float last_symi = 0.0f;
-  // input: the channel rows of this workgroup, sample t of lane's channel at
-  // ((g * stride) + t) * 4; samples outside [0, count) read 0 (out of range)
-  const int rows_valid = min(RDS_CPW, a.C - c0);
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + (size_t)c0 * a.in_stride,
-                                               (uint32_t)((size_t)max(rows_valid, 0) * a.in_stride * sizeof(float)));
-  auto in_off = [&](int r, int q) __attribute__((always_inline)) {
+  // input: the channel rows of this workgroup, sample t of the lane's channel
+  // at inb[g * stride + t]; samples outside [0, count) read the row's first
+  // word (every use masks them: vq below).  Plain loads from a wave-uniform
+  // base (round 3 used a buffer descriptor, which the SGPR-bound kernel kept
+  // in VGPRs: a readfirstlane loop around every load)
+  const float *inb = a.in + (size_t)c0 * a.in_stride;
+  auto in_ld = [&](int r, int q) __attribute__((always_inline)) {
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
     const int t = base + j0 + 8 * q;
-    return (act && r < R && t >= 0 && t < count) ? (uint32_t)((g * a.in_stride + t) * 4) : 0x80000000u;
+    const bool v = act && r < R && t >= 0 && t < count;
+    return inb[(act ? g * a.in_stride : 0) + (v ? t : 0)];
   };
   // the round's three input samples, loaded RDS_PF rounds ahead (a round
   // is ~0.3 us; the input comes from the Infinity Cache or HBM)
@@ -1827,7 +1823,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
 #pragma unroll
   for (int p = 0; p < RDS_PF; ++p)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) xr[p][q] = bload1(rin, in_off(p, q), 0);
+    for (int q = 0; q < 3; ++q) xr[p][q] = in_ld(p, q);
   // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued
   // symbols, in the channel's first lane
   auto flush_symbols = [&]() __attribute__((always_inline)) {
@@ -1862,7 +1858,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   RDS_STAMP(0)
   for (int r = 0; r < rmax; ++r) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) xr[RDS_PF][q] = bload1(rin, in_off(r + RDS_PF, q), 0);
+    for (int q = 0; q < 3; ++q) xr[RDS_PF][q] = in_ld(r + RDS_PF, q);
     const bool live = r < R;
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
     // ---- mix-down and FIR products of this lane's samples (oldest first) ----
@@ -1921,15 +1917,23 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       f32x2 sym = f32x2{0.0f, 0.0f};
       while (ss_b < FMX_NPFB && ns < 16) {
         const float *hm = L.mf + ss_b * FMX_SS_SUB;
-        f32x2 acm = f32x2{0.0f, 0.0f};
-        // entries not pushed since the reset are the zeros k_reset wrote
-#pragma unroll 6
-        for (int m = 0; m < FMX_SS_SUB; ++m) {
-          const float h = hm[FMX_SS_SUB - 1 - m];
-          const f32x2 w = wat(m);
-          const f32x2 p = f32x2{h, h} * w;
-          acm = acm + p;
-        }
+        // the 18-tap matched filter split over the channel's 8 lanes (taps
+        // m = j0, j0 + 8, j0 + 16), summed by the DPP butterfly: every lane
+        // holds the same total (a tree instead of the reference's sequential
+        // sum: a few ulp)
+        auto mf_dot = [&](const float *hb) __attribute__((always_inline)) {
+          f32x2 p = f32x2{0.0f, 0.0f};
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int m = j0 + 8 * u;
+            if (u < 2 || m < FMX_SS_SUB) {
+              const float h = hb[FMX_SS_SUB - 1 - m];
+              p = __builtin_elementwise_fma(f32x2{h, h}, wat(m), p);
+            }
+          }
+          return f32x2{rds_sum8(p.x), rds_sum8(p.y)};
+        };
+        const f32x2 acm = mf_dot(hm);
         // x / 3 as fmx_div_const (bit-identical for every normal x,
         // tests/golden/divconst_exhaustive.json), the zero's sign restored
         if (ns == 0)
@@ -1938,13 +1942,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
         if (ss_decim == 1) {
           ss_decim = 0;
           const float *hd = L.dmf + ss_b * FMX_SS_SUB;
-          f32x2 acd = f32x2{0.0f, 0.0f};
-#pragma unroll 6
-          for (int m = 0; m < FMX_SS_SUB; ++m) {
-            const float h = hd[FMX_SS_SUB - 1 - m];
-            const f32x2 p = f32x2{h, h} * wat(m);
-            acd = acd + p;
-          }
+          const f32x2 acd = mf_dot(hd);
           float qe = acm.x * acd.x + acm.y * acd.y;
           if (qe > 1.0f) qe = 1.0f;
           else if (qe < -1.0f) qe = -1.0f;

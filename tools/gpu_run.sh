@@ -46,7 +46,7 @@ for step in "$@"; do
       head -30 $O/trace_$TAG.log ;;
     stats)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/stats_$TAG" -o run \
-        -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$ROOT/$O/stats_${TAG}_bench.json" 2> "$ROOT/$O/stats_$TAG.err"); rc=$?
+        -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline ${FMX_AB_ARGS:-} > "$ROOT/$O/stats_${TAG}_bench.json" 2> "$ROOT/$O/stats_$TAG.err"); rc=$?
       cat $O/stats_$TAG/*kernel_stats.csv 2>/dev/null | cut -c1-160 | head -8 ;;
     pmc)
       bash tools/gpu_profile_pmc.sh "$TAG" > $O/pmc_$TAG.log 2>&1; rc=$?
