@@ -113,6 +113,10 @@ def ref():
                                        C.c_double, C.POINTER(C.c_double)]
         L.ref_smooth_signal_level.restype = C.c_float
         L.ref_smooth_signal_level.argtypes = [C.c_float, C.POINTER(i), C.POINTER(C.c_float)]
+        L.ref_xdr_pi_state.restype = i
+        L.ref_xdr_pi_state.argtypes = [vp, vp, i, C.c_uint16]
+        L.ref_xdr_session.restype = i
+        L.ref_xdr_session.argtypes = [vp, vp, i, C.c_char_p, i, i, C.c_char_p, i]
         _ref = L
     return _ref
 
@@ -202,6 +206,35 @@ def ref_blocksync(bits):
     n = R.ref_blocksync_push(p, bits.ctypes.data, bits.size, g, cap)
     R.ref_blocksync_destroy(p)
     return groups_to_tuples(g, min(n, cap))
+
+
+def ref_xdr_pi_state(buf64, err8, fill, value):
+    """The reference's evaluatePiState (xdr_server.cpp:189-213), oracle/_ref."""
+    b = np.ascontiguousarray(buf64, dtype=np.uint16)
+    e = np.ascontiguousarray(err8, dtype=np.uint8)
+    return ref().ref_xdr_pi_state(b.ctypes.data, e.ctypes.data, int(fill), int(value))
+
+
+def ref_xdr_session(groups, scan_lines=(), port=None):
+    """The lines the reference's started XDRServer sends one authenticated
+    loopback client when `groups` ((a, b, c, d, errors) each) go through
+    updateRDS and `scan_lines` through pushScanLine (oracle/_ref,
+    refdrv/xdr_driver.cpp).  Returns the list of lines."""
+    import random
+    g = np.array([x[:4] for x in groups], dtype=np.uint16).reshape(-1, 4) if groups else np.zeros((0, 4), np.uint16)
+    e = np.array([x[4] for x in groups], dtype=np.uint8) if groups else np.zeros(0, np.uint8)
+    scan = b"".join(ln.encode() + b"\0" for ln in scan_lines)
+    cap = 40 * (len(groups) + 1) + sum(len(x) + 2 for x in scan_lines) + 64
+    out = C.create_string_buffer(cap)
+    for attempt in range(8):  # a busy port: another one
+        pt = port or random.randint(20000, 60000)
+        rc = ref().ref_xdr_session(g.ctypes.data, e.ctypes.data, len(groups), scan or None, len(scan_lines), pt,
+                                   out, cap)
+        if rc != -1 or port:
+            break
+    if rc < 0:
+        raise RuntimeError(f"ref_xdr_session failed ({rc})")
+    return out.value.decode().splitlines()
 
 
 def run_many(cfg, iq, n_blocks, threads):

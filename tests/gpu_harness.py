@@ -141,7 +141,7 @@ def _groups_of(grp_rows, gcnt_rows, GS):
     return out
 
 
-def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=False, warmup=5):
+def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=False, warmup=5, all_groups=None):
     """The bench's timed mode (bench.py step()): every block through
     fmx_process_block back to back, NO host synchronisation between blocks,
     kernel timing switched on after `warmup` blocks as the bench does, the
@@ -151,7 +151,9 @@ def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=Fals
     the last block has been submitted.  Channels [ch0, ch0 + C) of the
     synthetic plan (a rank's fmx_dist shard).  Returns (per-block results
     indexed by position in keep, host IQ rows of keep, transmitted groups of
-    keep, per-block stereo fraction over all C channels)."""
+    keep, per-block stereo fraction over all C channels).  all_groups: a list
+    that receives every channel's decoded groups over all blocks (full-size
+    property checks)."""
     B = cfg.block
     M = cfg.iq_rate // cfg.dsp_rate
     n_iq = B * M
@@ -195,6 +197,12 @@ def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=Fals
     SG = sel(sig)  # 40-byte fmx_signal_level records
     recs = [[fmx.SignalLevel.from_buffer_copy(SG[b, j].tobytes()) for j in range(len(keep))] for b in range(nblk)]
     stereo_all = ints[1].float().mean(dim=1).cpu().numpy()
+    if all_groups is not None:
+        ga = grp.cpu().numpy()  # [nblk][C][GS][4]
+        gca = ints[3].cpu().numpy()
+        per = [_groups_of(ga[b], gca[b], GS) for b in range(nblk)]
+        all_groups.extend([g for b in range(nblk) for g in per[b][c]] for c in range(C))
+        del ga
     res = []
     for b in range(nblk):
         d = dict(pcm_l=PL[b], pcm_r=PR[b], count=I[0, b], stereo=I[1, b], pilot=I[2, b], indicator=I[4, b],

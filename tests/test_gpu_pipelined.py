@@ -109,9 +109,10 @@ def test_cfg4_rank1_shard_pipelined(fmx, oracle, torch_cuda):
     assert stereo_all[-1] > 0.99
 
 
-def test_xdr_lines_from_gpu_groups(fmx, cfg3_pipelined):
+def test_xdr_lines_from_gpu_groups(fmx, oracle, cfg3_pipelined):
     """8f row 3 on the GPU path: HIP-decoded groups -> fmx_xdr_rds_lines,
-    byte for byte against the oracle's groups -> the restated updateRDS, over
+    byte for byte against the oracle's groups -> the restated updateRDS and
+    against the HIP groups -> the reference's XDRServer (oracle/_ref), over
     36 blocks per station, stations switched (PI changes) as a retune would:
     channel 0's groups, then channel 1's, then channel 0's again, into one
     server state each side."""
@@ -132,6 +133,11 @@ def test_xdr_lines_from_gpu_groups(fmx, cfg3_pipelined):
                 if (grp[4] >> 6) == 0:
                     n_pi.add(grp[0])
     assert got == want
+    # and the reference's own XDRServer (oracle/_ref, built in the build
+    # container and shipped as a library) over the HIP groups
+    if oracle.ref_available():
+        hip_groups = [grp for j in (0, 1, 0) for b in range(NBLK) for grp in g[b]["groups"][j]]
+        assert oracle.ref_xdr_session(hip_groups) == got
     # ~5 groups per station in 36 blocks (11.4 groups/s), three passes
     assert len(n_pi) == 2 and sum(1 for ln in got if ln.startswith("P")) >= 4
     assert sum(1 for ln in got if ln.startswith("R")) >= 10

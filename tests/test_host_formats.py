@@ -65,6 +65,71 @@ def test_xdr_rds_lines_match_server(fmx):
             assert x.lines(batch) == want
 
 
+def _xdr_fixture():
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "xdr_server.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("stream", ["clean", "bursts", "retunes"])
+def test_xdr_rds_lines_match_reference_fixture(fmx, stream):
+    """fmx_xdr_rds_lines against the lines the REFERENCE's XDRServer sent a
+    loopback client for the same groups (tests/golden/xdr_server.json, made by
+    tools/gen_golden.py from oracle/_ref): byte for byte, in ragged batches,
+    and the Python restatement (the GPU tests' checker) agrees as well."""
+    fx = {s["name"]: s for s in _xdr_fixture()["streams"]}[stream]
+    groups = [tuple(g) for g in fx["groups"]]
+    x = fmx.XdrRds()
+    got, k = [], 0
+    for m in (1, 5, 0, 64, 111, 333, 1000):
+        got += x.lines(groups[k:k + m])
+        k += m
+    assert k >= len(groups)
+    assert got == fx["lines"]
+    ref = PyXdr()
+    assert [ln for g in groups for ln in ref.update(*g)] == fx["lines"]
+
+
+def test_xdr_scan_line_framing_matches_reference_fixture(fmx):
+    """XDRServer::pushScanLine's framing ("U" + the line) as the reference
+    server sent it (fixture), against fmx_xdr_scan_line."""
+    sc = _xdr_fixture()["scan"]
+    for line, sent in zip(sc["lines"], sc["sent"]):
+        pts = [p.split("=") for p in line.split(",")]
+        freqs = [int(f) for f, _ in pts]
+        sums = [float(v) for _, v in pts]
+        assert fmx.xdr_scan_line(freqs, sums, [1] * len(pts)) == sent
+
+
+def test_xdr_rds_lines_match_reference_live(fmx, oracle):
+    """The same against the reference server compiled here (oracle/_ref),
+    on fresh seeded streams: random error masks, missing A / B blocks, PI
+    changes, and a long run past the server's 64-entry PI history."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(99)
+    for trial in range(3):
+        groups = _random_groups(rng, 700, [0x1234, 0xC0DE, 0x9ABC, 0x0001][: trial + 2])
+        x = fmx.XdrRds()
+        assert x.lines(groups) == oracle.ref_xdr_session(groups)
+
+
+def test_xdr_pi_state_restatement_matches_reference(oracle):
+    """evaluatePiState (xdr_server.cpp:189-213, the reference's own code in
+    oracle/_ref) against the tests' restatement, on random histories."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(5)
+    for _ in range(3000):
+        x = PyXdr()
+        x.fill = int(rng.integers(0, 65))
+        vals = rng.choice([0x1111, 0x2222, 0x3333], size=64)
+        x.buf = [int(v) for v in vals]
+        x.err = [int(v) for v in rng.integers(0, 256, size=8)]
+        v = int(rng.choice([0x1111, 0x2222, 0x3333, 0x4444]))
+        assert x.state(v) == oracle.ref_xdr_pi_state(np.array(x.buf), np.array(x.err), x.fill, v)
+
+
 def test_xdr_pi_debounce_known_answers(fmx):
     x = fmx.XdrRds()
     # first clean PI: one correct copy -> UNLIKELY, no P line; R line emitted

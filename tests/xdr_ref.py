@@ -1,6 +1,10 @@
 """Python restatement of the XDR server's RDS line formatting (the checker
 for fmx_xdr_rds_lines): XDRServer::updateRDS + evaluatePiState
-(src/xdr_server.cpp:189-213, 403-457).  Test infrastructure only."""
+(src/xdr_server.cpp:189-213, 403-457).  Test infrastructure only.  Pinned to
+the reference itself: tests/test_host_formats.py checks it (and
+fmx_xdr_rds_lines) against the lines the reference's XDRServer, compiled into
+oracle/_ref, sends a loopback client (tests/golden/xdr_server.json, and live
+when oracle/_ref is built)."""
 
 
 class PyXdr:

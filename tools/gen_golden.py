@@ -6,6 +6,12 @@
                   BlockStream (src/redsea_port/block_sync.cpp + group.cpp,
                   compiled by oracle/Makefile into oracle/_ref/libfmx_ref.so)
                   emits for them.  Pins the oracle's and the GPU's block sync.
+  xdr_server.json group streams (clean, burst errors, missing blocks, PI
+                  changes as retunes make them) and scan lines, with the lines
+                  the REFERENCE's own XDRServer (src/xdr_server.cpp, compiled
+                  into oracle/_ref by refdrv/xdr_driver.cpp) sends a loopback
+                  client for them (updateRDS / pushScanLine).  Pins
+                  fmx_xdr_rds_lines and the tests' Python restatement.
   oracle_regress.json
                   hashes / excerpts of the oracle pipeline on seeded synthetic
                   IQ (pins the oracle restatement and the IQ generator against
@@ -72,6 +78,35 @@ def streams():
     return out
 
 
+def xdr_streams():
+    """Seeded group streams for the XDR server fixture: (a, b, c, d, errors)."""
+    rng = np.random.default_rng(2024)
+    out = {}
+
+    def grp(pi, emask):
+        return (int(pi), int(rng.integers(0, 65536)), int(rng.integers(0, 65536)), int(rng.integers(0, 65536)),
+                int(emask))
+
+    # a locked station: clean groups, the odd corrected block
+    out["clean"] = [grp(0x54A8, 0 if rng.random() < 0.9 else int(rng.choice([0x40, 0x10, 0x04, 0x01])))
+                    for _ in range(300)]
+    # burst errors: every error level on every block, missing blocks (3)
+    out["bursts"] = [grp(int(rng.choice([0xC201, 0xC202])), int(rng.integers(0, 256))) for _ in range(400)]
+    # retunes: the PI changes every 25-60 groups, a few noisy copies of the old one
+    g, pis = [], [0x1000 + k for k in range(6)]
+    while len(g) < 500:
+        pi = int(rng.choice(pis))
+        for _ in range(int(rng.integers(25, 60))):
+            e = 0 if rng.random() < 0.7 else int(rng.integers(0, 256))
+            g.append(grp(pi if rng.random() < 0.95 else pi ^ 0x0100, e))
+    out["retunes"] = g[:500]
+    return out
+
+
+def xdr_scan_lines():
+    return ["87500=41.3,87600=0.0,87700=10.0", "100000=120.0", "87500=-4.0,107900=99.9"]
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     if not oracle.ref_available():
@@ -85,6 +120,17 @@ def main():
         json.dump({"source": "reference BlockStream (src/redsea_port/block_sync.cpp, group.cpp) via "
                              "oracle/_ref/libfmx_ref.so; generated by tools/gen_golden.py",
                    "streams": fx}, f, indent=0)
+
+    # the reference XDR server: one session per stream (a fresh server state)
+    xs = []
+    for name, groups in xdr_streams().items():
+        xs.append({"name": name, "groups": [list(x) for x in groups], "lines": oracle.ref_xdr_session(groups)})
+    scan = xdr_scan_lines()
+    with open(os.path.join(GOLD, "xdr_server.json"), "w") as f:
+        json.dump({"source": "reference XDRServer (src/xdr_server.cpp: updateRDS, pushScanLine) via "
+                             "oracle/_ref/libfmx_ref.so (refdrv/xdr_driver.cpp, loopback client); "
+                             "generated by tools/gen_golden.py",
+                   "streams": xs, "scan": {"lines": scan, "sent": oracle.ref_xdr_session([], scan)}}, f, indent=0)
 
     # oracle regression pin (stereo+RDS at 2.4 MS/s, and mono cfg1)
     reg = {}
