@@ -50,15 +50,16 @@ ALG_FLOP_PER_IQ = 290.0
 # per-kernel DESIGN figures: HBM bytes the design moves
 # per IQ sample including its own intermediates (MPX, pilot, RDS-rate, raw
 # L/R), and the kernel's share of the 290 FLOP
-# The RDS stream runs the 240k -> 171k resampler (k_rs: MPX in, RDS-rate
-# samples out) before k_rds (RDS-rate samples in).
+# The 240k -> 171k RDS resampler (k_rs: MPX in, RDS-rate samples out) runs on
+# the RDS stream ahead of k_rds, which reads the RDS-rate samples.
 PER_IQ = {
     "frontend": (2.0 + 0.4 + 0.4, 112.0 + 32.4 + 61.0),
     "stereo": (0.4 + 0.8 + 0.8, 20.0),
     "audio": (0.8 + 0.107, 48.0 + 3.0),
-    "rds": (0.4 + 2 * 4.0 * 0.7125 / 10.0, 15.0 + 7.4),
+    "rds": (4.0 * 0.7125 / 10.0, 15.0),
+    "rs": (0.4 + 4.0 * 0.7125 / 10.0, 7.4),
 }
-KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rs+k_rds"}
+KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs"}
 
 
 def pmc_bytes(pmc, k):

@@ -142,8 +142,8 @@ struct Handle {
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
-  double kms[FMX_K_COUNT] = {0, 0, 0, 0};
-  int klaunch[FMX_K_COUNT] = {0, 0, 0, 0};
+  double kms[FMX_K_COUNT] = {};
+  int klaunch[FMX_K_COUNT] = {};
   std::vector<void *> allocs;
 };
 
@@ -879,15 +879,18 @@ static void step_done(Handle *h, bool stereo_hist_written) {
 // streams: sA front end, sC RDS, sB stereo PLL, sD audio.  Per step k (slot
 // buf = k mod FMX_NBUF of the intermediates):
 //   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evA(k)
-//   sC: [wait evA(k)] k_rds -> evC(k)
+//   sC: [wait evA(k)] k_rs, k_rds -> evC(k)
 //   sB: [wait evA(k)] k_pll -> evB(k)
 //   sD: [wait evB(k), evC(k)] [audio schedule copy] k_audio -> evD(k)
 // evD(k) therefore marks every reader of slot buf done (k_audio waits for
 // k_rds as well as k_pll), so the front end of step k+3 -- the next writer of
 // the slot, and through evA of the raw L/R slot k_pll writes -- needs ONE
 // cross-stream wait.  The resampler schedules go on the stream of their only
-// reader, right before it.  Front end k+1 runs while k_pll / k_rds / k_audio
-// of step k (and k-1) still run.
+// reader, right before it.  Front end k+1 runs while k_pll / k_rs / k_rds /
+// k_audio of step k (and k-1) still run.  (Measured and rejected in round 4:
+// k_rs on sD ahead of k_audio, with k_audio no longer waiting for k_rds --
+// 0.427 -> 0.437 ms per step at 2 048 channels, 0.744 -> 0.753 at 4 096,
+// profiles/r04k_ab_rs_stream.txt.)
 static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n, const fmx_block_out *o) {
   int rc;
   if ((rc = check_n(h, n)) != FMX_OK) return rc;
@@ -933,10 +936,12 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.rds_out = h->rds_in[buf];
       a.rds_stride = h->rds_stride;
     }
-    // the RDS resampler of a k_fe8 step runs as k_rs (MFMA tiles where a
-    // workgroup's 16 channels share one timing group, else per channel)
+    // the RDS resampler of a k_fe8 step runs as k_rs (MFMA tiles of 16
+    // channels x 16 outputs on the handle's one RDS schedule)
     // (16 outputs' windows span <= 15 del + 31 samples: inside k_rs's 64 for del <= 2.1)
-    use_rs = rds && h->hdes->rds_del <= 2.1f &&
+    // k_rs takes one resampler schedule for all channels: the RDS timing set
+    // is never reset per channel (SubcarrierSet::reset, subcarrier.cpp:108)
+    use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 &&
              frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
     if (use_rs) a.rds_win_out = h->rds_win[buf];
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
@@ -958,14 +963,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
   HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
-  // ---- RDS (sC) ----
+  // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
-    KTimer t(h, FMX_K_RDS, h->sC);  // k_rs + k_rds: the RDS stream's live time
     if (use_rs) {
       RsArgs r{};
       r.des = h->ddes;
@@ -982,6 +986,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       r.out_stride = h->rds_stride;
       // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
       r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
+      KTimer t(h, FMX_K_RS, h->sC);
       if (!FMX_SKIP(rds) && (rc = launch_rs(r, h->sC)) != FMX_OK) {
         h->err = "rds resampler launch failed";
         return rc;
@@ -989,6 +994,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       HIP_TRY(hipEventRecord(h->evR[buf], h->sC));
       h->evR_set[buf] = true;
     }
+    KTimer t(h, FMX_K_RDS, h->sC);
     if (!FMX_SKIP(rds) && (rc = launch_rds(a, h->sC)) != FMX_OK) {
       h->err = "rds launch failed";
       return rc;

@@ -1023,6 +1023,28 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
  * the matrix + blend + stores (W3) in one-lane-per-channel waves, which set
  * its pace (W3 1.73 M, W1 1.67 M, the W0 chain 0.99 M ticks per launch-WG)
  * and gave 2 048 channels only 64 workgroups. */
+// One dword per lane from a per-lane global address into LDS m0 + 4 lane
+// (LDS-DMA as inline asm: the compiler's wait-count pass does not see it, so
+// the issuing wave's own counted s_waitcnt vmcnt are the only waits and the
+// moves stay in flight across loop iterations; k_pll, k_rds)
+__device__ __forceinline__ void dma_dword(const float *src, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+// the same from a wave-uniform base plus a per-lane byte offset (saddr form)
+__device__ __forceinline__ void dma_dword_s(const float *base, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p);
+}
 // sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
 // which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
 __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) {
@@ -1488,6 +1510,8 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 #define RDS_LPC 8                  // lanes per channel
 #define RDS_CPW (64 / RDS_LPC)     // channels per wave / workgroup
 #define RDS_SYMQ 12                // symbols queued per channel before the bit decoders run
+#define RDS_PF 3                   // input rounds moved ahead (LDS-DMA)
+#define RDS_NR 4                   // input ring slots (> RDS_PF, a power of two)
 static_assert(FMX_RDS_DECIM == 3 * RDS_LPC, "three samples per lane and decimation period");
 // The bit-decoder state of FmxRdsState (biphase, delta, block sync) -- the
 // only state k_rds keeps in LDS; the per-sample state lives in registers.
@@ -1572,6 +1596,7 @@ struct RdsLds {
   // contiguous (constant read offsets, no wrap per tap)
   f32x2 win[2 * FMX_SS_SUB][RDS_CPW];
   float symq[RDS_SYMQ][RDS_CPW];   // symbols (real part) awaiting biphase / block sync
+  float xin[RDS_NR][3][64];        // input ring: round r's sample j0 + 8 q of lane's channel at [r % RDS_NR][q][lane]
   RdsCold cold[RDS_CPW];
 };
 
@@ -1806,24 +1831,26 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   float last_symi = 0.0f;
   // input: the channel rows of this workgroup, sample t of the lane's channel
   // at inb[g * stride + t]; samples outside [0, count) read the row's first
-  // word (every use masks them: vq below).  Plain loads from a wave-uniform
-  // base (round 3 used a buffer descriptor, which the SGPR-bound kernel kept
-  // in VGPRs: a readfirstlane loop around every load)
+  // word (every use masks them: vq below).  Each round's three samples per
+  // lane are moved by LDS-DMA into the ring L.xin, RDS_PF rounds ahead, and
+  // read back when the round runs: the wave's only vector-memory loads, so a
+  // counted s_waitcnt finds them (round 3 rotated a register ring, and the
+  // rotation waited for the loads of the round before: one memory latency
+  // per round, half of the mix + FIR stage's clocks)
   const float *inb = a.in + (size_t)c0 * a.in_stride;
-  auto in_ld = [&](int r, int q) __attribute__((always_inline)) {
+  const uint32_t xin0 = lds_addr(&L.xin[0][0][0]);
+  auto dma_round = [&](int r) __attribute__((always_inline)) {
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
-    const int t = base + j0 + 8 * q;
-    const bool v = act && r < R && t >= 0 && t < count;
-    return inb[(act ? g * a.in_stride : 0) + (v ? t : 0)];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int t = base + j0 + 8 * q;
+      const bool v = act && r < R && t >= 0 && t < count;
+      dma_dword(inb + (act ? g * a.in_stride : 0) + (v ? t : 0),
+                xin0 + (uint32_t)(((r & (RDS_NR - 1)) * 3 + q) * 64 * 4));
+    }
   };
-  // the round's three input samples, loaded RDS_PF rounds ahead (a round
-  // is ~0.3 us; the input comes from the Infinity Cache or HBM)
-  constexpr int RDS_PF = 4;
-  float xr[RDS_PF + 1][3];
 #pragma unroll
-  for (int p = 0; p < RDS_PF; ++p)
-#pragma unroll
-    for (int q = 0; q < 3; ++q) xr[p][q] = in_ld(p, q);
+  for (int p = 0; p < RDS_PF; ++p) dma_round(p);
   // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued
   // symbols, in the channel's first lane
   auto flush_symbols = [&]() __attribute__((always_inline)) {
@@ -1857,8 +1884,13 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   __syncthreads(); // LDS tables and per-channel state written
   RDS_STAMP(0)
   for (int r = 0; r < rmax; ++r) {
+    dma_round(r + RDS_PF);
+    // the moves of rounds r + 1 .. r + RDS_PF may stay in flight (anything
+    // the compiler issued after them only makes the wait stricter)
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * RDS_PF)); // vmcnt(3 RDS_PF), lgkmcnt / expcnt untouched
+    float xr0[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) xr[RDS_PF][q] = in_ld(r + RDS_PF, q);
+    for (int q = 0; q < 3; ++q) xr0[q] = L.xin[r & (RDS_NR - 1)][q][lane];
     const bool live = r < R;
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
     // ---- mix-down and FIR products of this lane's samples (oldest first) ----
@@ -1874,7 +1906,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       const float sn = -__builtin_amdgcn_sinf(rr);
       const float cs = __builtin_amdgcn_cosf(rr);
       // samples outside the call contribute nothing (their input reads 0)
-      mq[q] = vq[q] ? f32x2{xr[0][q], xr[0][q]} * f32x2{cs, sn} : f32x2{0.0f, 0.0f};
+      mq[q] = vq[q] ? f32x2{xr0[q], xr0[q]} * f32x2{cs, sn} : f32x2{0.0f, 0.0f};
       if (vq[q] && t >= count - FMX_RDS_RING) {
         const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
         *reinterpret_cast<f32x2 *>(ring + 2 * idx) = mq[q];
@@ -1994,10 +2026,6 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       thp = thp + (uint32_t)(count - base) * dtheta;
     }
     RDS_STAMP(2)
-#pragma unroll
-    for (int p = 0; p < RDS_PF; ++p)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) xr[p][q] = xr[p + 1][q];
     // decoders every RDS_SYMQ - 2 rounds (at most one symbol per round)
     if (r % (RDS_SYMQ - 2) == RDS_SYMQ - 3) {
       flush_symbols();
@@ -3033,12 +3061,23 @@ int launch_audio(const AudioArgs &a, void *stream) {
 #define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
 #define RS_TMAX FMX_RS_TMAX // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
 #define RS_XP 68   // padded window row: 16 channel rows 68 floats apart read conflict-free
-__global__ __launch_bounds__(64) void k_rs(RsArgs a) {
-  __shared__ float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
-  __shared__ FmxSched ssch[RS_TMAX * 16];
+// <= 96 VGPRs (five waves per SIMD): a k_rs wave beside two k_fe8 waves (168
+// each) and a k_pll wave (80)
+struct RsLds {
+  float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
+  FmxSched ssch[RS_TMAX * 16];
   // the tile's MPX window [buffer][channel][sample - k0]: 15.3 KB in all, so
   // a k_rs workgroup fits beside two k_fe8 and one k_pll workgroup on a CU
-  __shared__ __align__(16) float xs[2][16][RS_XP];
+  float xs[2][16][RS_XP] __attribute__((aligned(16)));
+};
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_rs(RsArgs a) {
+  // dynamic LDS (as k_rds): with a static size the backend sees an
+  // LDS-limited occupancy and ignores the occupancy attribute's budget
+  extern __shared__ __align__(16) unsigned char rs_smem[];
+  RsLds &RL = *reinterpret_cast<RsLds *>(rs_smem);
+  auto &tab = RL.tab;
+  auto &ssch = RL.ssch;
+  auto &xs = RL.xs;
   typedef float f32x4_t __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x;
   const int c0 = blockIdx.x * 16;
@@ -3053,47 +3092,10 @@ __global__ __launch_bounds__(64) void k_rs(RsArgs a) {
     else h = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
     tab[b][m] = h;
   }
-  // channels of different timing groups in this workgroup (some of them
-  // reset since the others): one lane per (channel, output phase), 27-term
-  // dot products in the reference's order -- the MFMA tile needs one
-  // schedule for its 16 channel columns
-  {
-    const int cm = c0 + (lane & 15);
-    const int gm = cm < a.C ? a.group[cm] : a.group[c0];
-    if (__any(gm != a.group[c0])) {
-      __syncthreads(); // tab written
-      if (cm < a.C) {
-        const FmxSched *sc = a.sched + (size_t)gm * a.sched_stride;
-        const int nsm = a.sched_n[gm];
-        const int ntm = (nsm + 15) / 16, pm = (ntm + a.parts - 1) / a.parts;
-        const int e1 = min(nsm, 16 * (blockIdx.y * pm + pm));
-        const float *mrow = a.mpx + (size_t)cm * a.mpx_stride;
-        const float *wrow = a.win + (size_t)cm * 32 + 32;
-        float *orow = a.out + (size_t)cm * a.out_stride;
-#pragma unroll 1
-        for (int e = 16 * blockIdx.y * pm + (lane >> 4); e < e1; e += 4) {
-          const FmxSched en = sc[e];
-          const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
-          const bool bnd = (en.packed >> 24) & 1;
-          const int s0 = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // >= -27: inside the 32-sample history
-          const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
-          float y0 = 0.0f, y1 = 0.0f;
-#pragma unroll 1
-          for (int m = 0; m <= FMX_RDS_RS_SUB; ++m) {
-            const int k = s0 + m;
-            const float x = k < 0 ? wrow[k] : (k < a.n ? mrow[k] : 0.0f);
-            y0 = y0 + tab[row0][m] * x;
-            y1 = y1 + tab[row1][m] * x;
-          }
-          const float w0f = (1.0f - en.mu) * y0;
-          const float w1f = en.mu * y1;
-          orow[e] = w0f + w1f;
-        }
-      }
-      return;
-    }
-  }
-  const int g = a.group[c0]; // one schedule for the workgroup's 16 channels
+  // one schedule for every channel (the RDS timing set is never reset per
+  // channel: SubcarrierSet::reset leaves the resampler alone,
+  // subcarrier.cpp:108; process_block launches k_rs only with one group)
+  const int g = a.group[c0];
   const FmxSched *sched = a.sched + (size_t)g * a.sched_stride;
   const int ns = a.sched_n[g];
   const int ntile = (ns + 15) / 16;
@@ -3147,43 +3149,39 @@ __global__ __launch_bounds__(64) void k_rs(RsArgs a) {
     const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
     const int k0 = tile_k0(T);
     const int m0 = k0 + kk - s_r; // this lane's tap index at K step 0
-    // all operands first (LDS latency paid once), then 32 MFMAs back to back
-    f32x2 hv[RS_KS];
-    float xv[RS_KS];
+    // K steps the tile needs: up to the last row's window end (rows past the
+    // call repeat the last entry; the schedule's windows only move forward)
+    const FmxSched e15 = ssch[16 * (T - ta) + 15];
+    const int i15 = e15.packed & 0xFFFF;
+    const int s15 = ((((e15.packed >> 24) & 1) ? i15 - 1 : i15) - (FMX_RDS_RS_SUB - 1));
+    const int ks = min(RS_KS, (s15 + FMX_RDS_RS_SUB - k0 + 3) / 4); // wave-uniform
+    // row r's two branch filters combined with its interpolation weight:
+    // (1 - mu) h_b + mu h_b+1, one MFMA chain (the reference interpolates the
+    // two dot products, (1 - mu) y0 + mu y1: the same sum in another order)
+    const float mu = en.mu, mu1 = 1.0f - mu;
+    float hv[RS_KS], xv[RS_KS];
 #pragma unroll
     for (int st = 0; st < RS_KS; ++st) {
       const int m = m0 + 4 * st;
       const int mc = min(max(m, 0), FMX_RDS_RS_SUB);
-      hv[st] = f32x2{tab[row0][mc], tab[row1][mc]};
+      const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
+      hv[st] = in ? mu1 * tab[row0][mc] + mu * tab[row1][mc] : 0.0f;
       xv[st] = xs[buf][r][4 * st + kk];
     }
-    f32x4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int st = 0; st < RS_KS; ++st) {
-      const int m = m0 + 4 * st;
-      const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(in ? hv[st].x : 0.0f, xv[st], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(in ? hv[st].y : 0.0f, xv[st], acc1, 0, 0, 0);
-    }
-    // D: lane (channel column r, output rows 4 kk .. 4 kk + 3); the
-    // reference's interpolation (1 - mu) y0 + mu y1
+    for (int st = 0; st < RS_KS; ++st)
+      if (st < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[st], xv[st], acc, 0, 0, 0);
+    // D: lane (channel column r, output rows 4 kk .. 4 kk + 3)
     const int cb = c0 + r;
     if (cb < a.C) {
-      float o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float mu = ssch[16 * (T - ta) + 4 * kk + q].mu;
-        const float w0f = (1.0f - mu) * acc0[q];
-        const float w1f = mu * acc1[q];
-        o[q] = w0f + w1f;
-      }
       float *dst = a.out + (size_t)cb * a.out_stride + 16 * T + 4 * kk;
       if (16 * T + 4 * kk + 3 < ns) {
-        *reinterpret_cast<float4 *>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4 *>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (16 * T + 4 * kk + q < ns) dst[q] = o[q];
+          if (16 * T + 4 * kk + q < ns) dst[q] = acc[q];
       }
     }
   };
@@ -3206,13 +3204,14 @@ __global__ __launch_bounds__(64) void k_rs(RsArgs a) {
 }
 
 int launch_rs(const RsArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  static_assert(sizeof(RsLds) <= 16 * 1024, "k_rs LDS");
+  hipLaunchKernelGGL(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), sizeof(RsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_rds(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
   // k_rds workgroups fit beside them
-  static_assert(sizeof(RdsLds) <= 12 * 1024, "k_rds LDS");
+  static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
   hipLaunchKernelGGL(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }

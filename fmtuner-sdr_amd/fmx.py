@@ -17,8 +17,8 @@ FMX_BLEND_SOFT, FMX_BLEND_NORMAL, FMX_BLEND_AGGRESSIVE = 0, 1, 2
 FMX_DEEMPH_50US, FMX_DEEMPH_75US, FMX_DEEMPH_OFF = 0, 1, 2
 PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
              force_mono=6, force_stereo=7, bandwidth_mode=8, deemph_us=9, deviation_hz=10)
-K_FRONTEND, K_STEREO, K_AUDIO, K_RDS = 0, 1, 2, 3
-KERNEL_NAMES = ["frontend", "stereo", "audio", "rds"]
+K_FRONTEND, K_STEREO, K_AUDIO, K_RDS, K_RS = 0, 1, 2, 3, 4
+KERNEL_NAMES = ["frontend", "stereo", "audio", "rds", "rs"]
 
 
 class Config(C.Structure):
@@ -229,10 +229,11 @@ class Handle:
         self._ck(self.L.fmx_timing_enable(self.h, max(1, int(every)) if on else 0), "fmx_timing_enable")
 
     def kernel_times(self):
-        ms = (C.c_double * 4)()
-        cnt = (C.c_int * 4)()
-        self._ck(self.L.fmx_kernel_times(self.h, ms, cnt, 4), "fmx_kernel_times")
-        return {KERNEL_NAMES[k]: (ms[k], cnt[k]) for k in range(4)}
+        nk = len(KERNEL_NAMES)
+        ms = (C.c_double * nk)()
+        cnt = (C.c_int * nk)()
+        self._ck(self.L.fmx_kernel_times(self.h, ms, cnt, nk), "fmx_kernel_times")
+        return {KERNEL_NAMES[k]: (ms[k], cnt[k]) for k in range(nk)}
 
 
 def synth_rds_bits(scfg, ch0, n_ch):

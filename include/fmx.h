@@ -38,7 +38,11 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 4
+/* ABI history: 5 (round 4) adds FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+ * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
+ * which changed that struct's size: callers must be rebuilt against this
+ * header. */
+#define FMX_ABI_VERSION 5
 
 enum {
   FMX_OK = 0,
@@ -208,9 +212,10 @@ enum {
                          when process_block does not run it as its own kernel, k_rs)            */
   FMX_K_STEREO = 1,   /* pilot PLL + blend + L-R matrix (one lane per channel)                 */
   FMX_K_AUDIO = 2,    /* L/R 15 kHz FIRs + 32 kHz resampler + de-emphasis + DC + clamp         */
-  FMX_K_RDS = 3,      /* (k_rs: 240k -> 171k resample +) 57 kHz BPSK demod + symsync + biphase +
-                         block sync: the RDS stream's kernels                                   */
-  FMX_K_COUNT = 4
+  FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync + biphase + block sync                     */
+  FMX_K_RS = 4,       /* the 240k -> 171k RDS resampler when process_block runs it as its own
+                         kernel (k_rs, on the RDS stream ahead of k_rds)                        */
+  FMX_K_COUNT = 5
 };
 /* enable: 0 off, 1 every step's launches, N > 1 the launches of every N-th
  * step only (a sample: fewer event packets on the streams in the timed region) */

@@ -250,19 +250,22 @@ def test_resets_and_runtime_setters(fmx, oracle, torch_cuda, bw):
               pilot_tol=PILOT_UNLOCKED_TOL if narrow else 0, narrow=narrow)
 
 
-def test_rds_resampler_mixed_timing_groups(fmx, oracle, torch_cuda):
-    """k_rs (the 240k -> 171k RDS resampler of process_block) when the 16
-    channels of one MFMA workgroup sit in different timing groups: channels
-    3, 17 and 18 reset at different blocks put both workgroups of 20 channels
-    in two or three groups (per-channel path), while the other channels keep
-    their schedule; every channel against the oracle, RDS groups bit-exact."""
+def test_rds_after_staggered_resets(fmx, oracle, torch_cuda):
+    """Channels 3, 17 and 18 of 20 reset at different blocks (Runtime::reset,
+    main.cpp:686-691).  The reset clears their RDS decoders (NCO, symsync,
+    block sync) but not the 240k -> 171k resampler's timing
+    (SubcarrierSet::reset leaves it alone, subcarrier.cpp:108), so all
+    channels keep one RDS schedule and k_rs's MFMA tiles (16 channels on one
+    schedule) keep running for both workgroups; every channel against the
+    oracle, RDS groups bit-exact.  (Audio resampler timing does split per
+    channel: k_audio reads each channel's group.)"""
     C, nblk = 20, 20
     iq, _ = make_iq(fmx, 2, C, nblk, ch0=200)
     resets = {5: 3, 8: 17, 11: 18}
     g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk, resets=resets)
     ngroups = 0
     for c in range(C):
-        ngroups += len(check(g, outs[c], c, nblk, "rs_mixed")["groups_oracle"])
+        ngroups += len(check(g, outs[c], c, nblk, "rds_staggered_resets")["groups_oracle"])
     assert ngroups >= C
 
 

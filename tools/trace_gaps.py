@@ -39,12 +39,17 @@ if len(fe) > 3:
 
 # per step (k-th launch of each kernel = step k): start / end of every kernel
 # relative to its front end's start, us -- which stream waits for which
-seq = {key: [e for e in ev if key in e[2]] for key in ("k_fe8", "k_pll", "k_rds", "k_audio")}
-nst = min(len(v) for v in seq.values())
+KEYS = ("k_fe8", "k_pll", "k_rs", "k_rds", "k_audio")
+seq = {key: [e for e in ev if key in e[2]] for key in KEYS}
+# the first block runs k_frontend (cold decimator history), later ones k_fe8:
+# the i-th front end of any kind is step i
+seq["k_fe8"] = [e for e in ev if "k_fe8" in e[2] or "k_frontend" in e[2]]
+KEYS = tuple(k for k in KEYS if seq[k])
+nst = min(len(seq[k]) for k in KEYS)
 if nst > 6:
-    print("step  fe[s,e]        pll[s,e]        rds[s,e]        audio[s,e]   (us from fe start)")
+    print("step  " + "".join("%-16s" % (k[2:] + "[s,e]") for k in KEYS) + "(us from fe start)")
     for k in range(nst - 8, nst):
         t0 = seq["k_fe8"][k][0]
         row = " ".join("%6.0f,%6.0f " % ((seq[key][k][0] - t0) / 1e3, (seq[key][k][1] - t0) / 1e3)
-                       for key in ("k_fe8", "k_pll", "k_rds", "k_audio"))
+                       for key in KEYS)
         print("%4d  %s" % (k, row))
