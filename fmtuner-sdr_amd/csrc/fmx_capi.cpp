@@ -1684,6 +1684,14 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
       }
       break;
     }
+    case 12: // k_audio MFMA L/R FIR taps back from the f16 hi/lo fragments (row 0 lanes), as case 3
+      for (int k = 0; k < FMX_LR_LEN; ++k) {
+        const int dd = FMX_LR_LEN - 1 - k; // = 32 ks + 8 g + j with row 0
+        const int ks = dd / 32, gg = (dd % 32) / 8, j = dd % 8, l = 16 * gg;
+        const double q = f16_value(d->lr_frag[ks][0][l][j]) + f16_value(d->lr_frag[ks][1][l][j]);
+        v.push_back(static_cast<float>(q / 4096.0));
+      }
+      break;
     case 11: { // k_fe8 MFMA IQ FIR taps back from the f16 hi/lo fragments (row 0 lanes), as case 1
       const int sel = bandwidth_select(cfg->bandwidth_hz, std::clamp(cfg->w0_bandwidth_hz, 0, 400000));
       const int idx = (sel == 0) ? FMX_IQ_CTOR : sel;

@@ -410,6 +410,22 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
     d->pilot_pair[k][1] = d->pilot_pad[k + 1];
   }
   for (int k = 0; k < FMX_LR_LEN; ++k) d->lr_pad[k + 5] = d->lr_taps[k];
+  {
+    // MFMA L/R FIR fragments (k_audio): taps * 2^12, hi/lo split; P = 121 is
+    // already 8k + 1, so the window starts 120 samples before the output
+    constexpr int P = FMX_LR_LEN, P8 = P;
+    static_assert((P8 + 15 + 31) / 32 == FMX_LR_KS, "L/R FIR K steps");
+    for (int ks = 0; ks < FMX_LR_KS; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int dd = 32 * ks + 8 * (l >> 4) + j - (l & 15);
+          const int k = P8 - 1 - dd;
+          const float q = (k >= 0 && k < P) ? d->lr_taps[k] * 4096.0f : 0.0f;
+          const uint16_t hi = f32_to_f16_bits(q);
+          d->lr_frag[ks][0][l][j] = hi;
+          d->lr_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+        }
+  }
   for (int k = 0; k + 1 < FMX_LR_LEN + FMX_PAD; ++k) {
     d->lr_pair[k][0] = d->lr_pad[k];
     d->lr_pair[k][1] = d->lr_pad[k + 1];

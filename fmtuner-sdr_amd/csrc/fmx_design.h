@@ -16,6 +16,7 @@
 #define FMX_IQ_MAXLEN 121
 #define FMX_PILOT_MAX 511    // stereo_decoder.cpp:98 clamp
 #define FMX_LR_LEN 121       // stereo_decoder.cpp:110-111
+#define FMX_LR_KS 5          // K steps of k_audio's MFMA L/R FIR: (121 + 15 + 31) / 32
 #define FMX_NPFB 32          // resamp_rrrf / symsync filter-bank size
 #define FMX_AF_SUB 24        // 2*m, m = 12 (liquid_primitives.h:145)
 #define FMX_RDS_RS_SUB 26    // 2*m, m = 13 (subcarrier.cpp:45)
@@ -82,6 +83,9 @@ typedef struct {
   uint16_t pilot_frag[FMX_PILOT_KS_MAX][2][64][8] __attribute__((aligned(16)));
   float lr_scale;
   float lr_taps[FMX_LR_LEN];
+  // k_audio's MFMA L/R FIR fragments, as pilot_frag: taps * 2^12 as f16 hi +
+  // lo, lr_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - (l & 15)]
+  uint16_t lr_frag[FMX_LR_KS][2][64][8] __attribute__((aligned(16)));
   float lr_pad[FMX_LR_LEN + FMX_PAD];
   float lr_pair[FMX_LR_LEN + FMX_PAD][2] __attribute__((aligned(8)));
   float nominal, pll_min, pll_max, pll_alpha, pll_beta;

@@ -1071,6 +1071,13 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
  *   clamp (main.cpp:1305-1308), stores.
  * Modes: 0 stereo (FIR + AF), 1 AF only, 2 mono FMDemod::downsampleAudio,
  * 3 mono pipeline (x0.5, L = R), 4 FIR only (fmx_stereo). */
+// L/R FIRs on v_mfma_f32_16x16x32_f16 (FMX_AU_MFMA 1): the pilot BPF's
+// Toeplitz tiles (k_fe8) on f16 hi / lo images of the chunk's L and R
+// (x 2^10) and the design's tap fragments (FmxDesign::lr_frag, x 2^12), three
+// MFMAs per K step; 0 keeps the packed-FMA FIR
+#ifndef FMX_AU_MFMA
+#define FMX_AU_MFMA 1
+#endif
 #define AU2_T 2048
 #define AU2_PT 8                        // FIR outputs per thread (AU2_T / 256)
 #define AU2_MAXOUT (AU2_T / 3 + 16)     // resampler outputs per chunk (ratio >= 3)
@@ -1078,17 +1085,23 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
 // conflict-free ds_read_b64)
 __device__ __forceinline__ int au_xi(int i) { return i + (i >> 3); }
 #define AU_XN ((AU_HALO + AU2_T + 8) * 9 / 8 + 8)
+#define AU_IMG (AU_HALO + AU2_T + 24) // f16 image: 120 history + the chunk + the last K step's reach
+static_assert(4 * AU_IMG * 2 <= AU_XN * 8, "the four f16 images fit the FIR image region");
 struct AuShared {
   // one region, two lives per chunk: the raw (L, R) FIR image x (au_xi
   // order, 120 of history first) until the FIR has read it, then the
   // resampler input f (32 of history first, natural order).  Sharing it
   // takes the workgroup from 45.6 to 29 KB of LDS: four workgroups per CU
   // instead of three (isolated 0.206 ms at three, 0.263 at two).
-  float2 xf[AU_XN > AU_RHALO + AU2_T ? AU_XN : AU_RHALO + AU2_T];
+  float2 xf[AU_XN > AU_RHALO + AU2_T ? AU_XN : AU_RHALO + AU2_T] __attribute__((aligned(16)));
   float2 fh[AU_RHALO];                         // f's history between chunks
   float2 o[AU2_MAXOUT];                        // resampler outputs of the chunk
   float hT[FMX_AF_SUB][FMX_NPFB];              // resampler bank transposed: hT[n][b] = h_b[n]
+#if FMX_AU_MFMA
+  float2 hf[AU_HALO];                          // the chunk's last 120 (L, R) inputs: the next chunk's FIR history
+#else
   float lt[136] __attribute__((aligned(16)));  // L/R FIR taps, lt[k + 7] = h[k], zeros around
+#endif
   float ws[3][4][2];                           // scan scratch (A, BL, BR per wave)
   float iir[4];                                // de_L, de_R, dc_L, dc_R
   int eb, ee, count;
@@ -1164,8 +1177,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
   float2 *const X = S.xf; // FIR image (au_xi order)
   float2 *const F = S.xf; // resampler input, after the FIR
+#if FMX_AU_MFMA
+  // this thread's pair of the FIR history (threads < 120), across chunks
+  float2 cx = make_float2(0.0f, 0.0f);
+  if (lrfir && tid < AU_HALO) cx = make_float2(lrh[tid], lrh[(FMX_LR_LEN - 1) + tid]);
+  (void)X;
+#else
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) X[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
+#endif
   if (af)
     for (int h = tid; h < AU_RHALO; h += 256) S.fh[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
@@ -1194,8 +1214,10 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     S.eb = 0;
     S.count = 0;
   }
+#if !FMX_AU_MFMA
   if (lrfir)
     for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
+#endif
   // tiled input (raw L/R from k_pll): sample j of this channel at tin + ti(j)
   const bool tiled = a.in_tiled != 0;
   const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
@@ -1232,16 +1254,115 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         vl[k] = (j < cnt) ? inl[ti(n0 + j)] : 0.0f;
         vr[k] = (j < cnt && !mono) ? inr[ti(n0 + j)] : 0.0f;
       }
+#if FMX_AU_MFMA
+      if (lrfir) {
+        // f16 hi / lo images [L hi | L lo | R hi | R lo], index = chunk sample + 120
+        _Float16 *im = reinterpret_cast<_Float16 *>(S.xf);
+        auto put = [&](int i, float l, float r) __attribute__((always_inline)) {
+          l *= 1024.0f;
+          r *= 1024.0f;
+          const _Float16 lh = (_Float16)l, rh = (_Float16)r;
+          im[i] = lh;
+          im[AU_IMG + i] = (_Float16)(l - (float)lh);
+          im[2 * AU_IMG + i] = rh;
+          im[3 * AU_IMG + i] = (_Float16)(r - (float)rh);
+        };
+        if (tid < AU_HALO) put(tid, cx.x, cx.y);
+#pragma unroll
+        for (int k = 0; k < AU2_PT; ++k) put(AU_HALO + tid + 256 * k, vl[k], vr[k]);
+        if (tid < AU_IMG - AU_HALO - AU2_T) put(AU_HALO + AU2_T + tid, 0.0f, 0.0f); // zero taps' reach: finite
+        // the next chunk's history, exact: inputs cnt - 120 .. cnt - 1 (the
+        // older ones, for cnt < 120, from the current history)
+#pragma unroll
+        for (int k = 0; k < AU2_PT; ++k) {
+          const int j = tid + 256 * k;
+          if (j >= cnt - AU_HALO && j < cnt) S.hf[j - (cnt - AU_HALO)] = make_float2(vl[k], vr[k]);
+        }
+        if (tid < AU_HALO && tid >= cnt) S.hf[tid - cnt] = cx;
+      } else {
+#pragma unroll
+        for (int k = 0; k < AU2_PT; ++k) {
+          const int j = tid + 256 * k;
+          if (j < cnt) F[AU_RHALO + j] = make_float2(vl[k], vr[k]);
+        }
+      }
+#else
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {
         const int j = tid + 256 * k;
         if (lrfir) X[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
         else if (j < cnt) F[AU_RHALO + j] = make_float2(vl[k], vr[k]);
       }
+#endif
       if (!lrfir && af && tid < AU_RHALO) F[tid] = S.fh[tid];
     }
     if (tid == 0) S.ee = S.eb;
     __syncthreads();
+#if FMX_AU_MFMA
+    // ---- L/R FIR on MFMA: 16 outputs (rows, A = taps) x 16 blocks of 16
+    // outputs (columns, B = inputs), K = the block's 136 inputs from 120
+    // before it; each wave two tiles of L and of R (512 outputs each) ----
+    if (lrfir) {
+      typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+      typedef float f32x4_t __attribute__((ext_vector_type(4)));
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const int lane = tid & 63, wave = tid >> 6, col = lane & 15, g = lane >> 4;
+      const _Float16 *im = reinterpret_cast<const _Float16 *>(S.xf);
+      const int xb = 16 * (32 * wave + col) + 8 * g; // image index of block (2 wave) 16 + col's K start, 8-aligned
+      const f16x8_t *bLh = reinterpret_cast<const f16x8_t *>(im + xb);
+      const f16x8_t *bLl = reinterpret_cast<const f16x8_t *>(im + AU_IMG + xb);
+      const f16x8_t *bRh = reinterpret_cast<const f16x8_t *>(im + 2 * AU_IMG + xb);
+      const f16x8_t *bRl = reinterpret_cast<const f16x8_t *>(im + 3 * AU_IMG + xb);
+      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->lr_frag[0][0][0][0]) + lane;
+      f32x4_t aL[2], aR[2];
+      aL[0] = aL[1] = aR[0] = aR[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      u32x4 ah = fa[0], al = fa[64];
+#pragma unroll
+      for (int ks = 0; ks < FMX_LR_KS; ++ks) {
+        const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
+        if (ks + 1 < FMX_LR_KS) {
+          ah = fa[128 * (ks + 1)];
+          al = fa[128 * (ks + 1) + 64];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f16x8_t lh = bLh[32 * u + 4 * ks], ll = bLl[32 * u + 4 * ks]; // + 256 u + 32 ks samples
+          const f16x8_t rh = bRh[32 * u + 4 * ks], rl = bRl[32 * u + 4 * ks];
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, lh, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rh, aR[u], 0, 0, 0);
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ll, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rl, aR[u], 0, 0, 0);
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, lh, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, rh, aR[u], 0, 0, 0);
+        }
+      }
+      if (tid < AU_HALO) cx = S.hf[tid];
+      __syncthreads(); // the images are read: F takes their place
+      if (af && tid < AU_RHALO) F[tid] = S.fh[tid];
+      const float osc = sc * (1.0f / 4194304.0f); // taps x 2^12, inputs x 2^10
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
+        const int j = 256 * (2 * wave + u) + 16 * col + 4 * g;
+        float2 y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = make_float2(aL[u][i] * osc, aR[u][i] * osc);
+        if (af) {
+          float4 *fw = reinterpret_cast<float4 *>(F + AU_RHALO + j); // 16-B aligned: AU_RHALO and j even
+          fw[0] = make_float4(y[0].x, y[0].y, y[1].x, y[1].y);
+          fw[1] = make_float4(y[2].x, y[2].y, y[3].x, y[3].y);
+        }
+        if (a.lr_out_l) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (j + i < cnt) {
+              a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j + i] = y[i].x;
+              a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j + i] = y[i].y;
+            }
+        }
+      }
+    }
+#else
     // ---- L/R FIR: outputs j0 .. j0+7, inputs j0-120 .. j0+7 ----
     float2 cx = make_float2(0.0f, 0.0f); // the next chunk's FIR history (X is overwritten by F)
     if (lrfir) {
@@ -1293,6 +1414,7 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         }
       }
     }
+#endif
     __syncthreads();
     if (af) {
       // ---- resampler: one schedule entry per thread ----
@@ -1417,17 +1539,26 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       float2 cf = make_float2(0.0f, 0.0f);
       if (af && tid < AU_RHALO) cf = F[tid + cnt];
       __syncthreads(); // F is dead: X takes its place again
+#if !FMX_AU_MFMA
       if (lrfir && tid < AU_HALO) X[au_xi(tid)] = cx;
+#endif
       if (af && tid < AU_RHALO) S.fh[tid] = cf;
       __syncthreads();
     }
   }
+#if FMX_AU_MFMA
+  if (lrfir && tid < AU_HALO) {
+    lrh[tid] = cx.x;
+    lrh[(FMX_LR_LEN - 1) + tid] = cx.y;
+  }
+#else
   if (lrfir)
     for (int h = tid; h < AU_HALO; h += 256) {
       const float2 v = X[au_xi(h)];
       lrh[h] = v.x;
       lrh[(FMX_LR_LEN - 1) + h] = v.y;
     }
+#endif
   if (af) {
     for (int h = tid; h < AU_RHALO; h += 256) {
       const float2 v = S.fh[h];

@@ -255,8 +255,9 @@ int fmx_synth_device(void *handle, const fmx_synth_config *cfg, uint32_t ch0, in
 /* Filter taps the handle would use: which = 0 decimator, 1 IQ FIR,
  * 2 pilot BPF, 3 L/R LPF, 4 audio resampler prototype, 5 RDS resampler
  * prototype, 6 RDS 2.4 kHz LPF, 7 symsync RRC, 8 symsync derivative;
- * the k_fe8 MFMA tables read back as float taps: 9 decimator (both copies),
- * 10 pilot BPF fragments, 11 IQ FIR fragments, 13 decimator A fragments.
+ * the MFMA tables read back as float taps:
+ * 10 pilot BPF fragments, 11 IQ FIR fragments, 12 L/R LPF fragments (k_audio),
+ * 13 decimator A fragments (row 0), 9 the same fragments' rows 0..15.
  * Returns the tap count (negative on error). */
 int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap);
 /* liquid resamp_rrrf output schedule for rate 1/del over n_in inputs from

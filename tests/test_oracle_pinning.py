@@ -279,6 +279,19 @@ def test_mfma_pilot_tap_fragments(fmx, rates):
 
 
 @pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_lr_fir_tap_fragments(fmx, rates):
+    """k_audio's MFMA L/R FIR takes the 121 L/R LPF taps as f16 hi + lo
+    fragments (x 2^12, FmxDesign::lr_frag): they give the float taps back to
+    22 bits."""
+    cfg = fmx.make_config(**rates)
+    h = fmx.design_taps(cfg, 3).astype(np.float64)
+    q = fmx.design_taps(cfg, 12).astype(np.float64)
+    assert q.size == h.size == 121
+    err = np.abs(q - h)
+    assert err.max() <= np.abs(h).max() * 2.0 ** -21, err.max() / np.abs(h).max()
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
 @pytest.mark.parametrize("bw", [-1, 0, 56000, 110000, 311000])
 def test_mfma_iq_fir_tap_fragments(fmx, rates, bw):
     """k_fe8's MFMA IQ FIR takes the selected IQ filter's taps as f16 hi + lo
