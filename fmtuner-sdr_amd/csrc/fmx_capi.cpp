@@ -139,6 +139,7 @@ struct Handle {
   struct Pending {
     int k;
     hipEvent_t a, b;
+    bool b_pool; // b from the pool (KTimer), else a stream's completion event (KBind)
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
@@ -197,7 +198,60 @@ struct KTimer {
   ~KTimer() {
     if (on) {
       hipEventRecord(b, s);
-      h->pending.push_back({k, a, b});
+      h->pending.push_back({k, a, b, true});
+    }
+  }
+};
+
+static void timing_take(Handle *h, const Handle::Pending &p, bool wait) {
+  float ms = 0.0f;
+  if (wait) hipEventSynchronize(p.b);
+  hipEventElapsedTime(&ms, p.a, p.b);
+  h->kms[p.k] += ms;
+  h->klaunch[p.k]++;
+  h->pool.push_back(p.a);
+  if (p.b_pool) h->pool.push_back(p.b);
+}
+
+// The pending timings up to the last one ending on `e`, waited for: `e` is
+// about to be bound to a new launch.
+static void timing_release(Handle *h, hipEvent_t e) {
+  size_t last = 0;
+  for (size_t k = 0; k < h->pending.size(); ++k)
+    if (h->pending[k].b == e) last = k + 1;
+  for (size_t k = 0; k < last; ++k) timing_take(h, h->pending[k], true);
+  h->pending.erase(h->pending.begin(), h->pending.begin() + static_cast<std::ptrdiff_t>(last));
+}
+
+// process_block's launches: the stream's completion event `done` (evA / evR /
+// evC / evB / evD) is bound to the kernel itself through hipExtLaunchKernel
+// (set_launch_events), and with timing on a pool event takes its start: no
+// marker packets between the kernels of a stream (each marker was a packet
+// the next kernel and every cross-stream waiter queued behind).  A kernel
+// left out (diagnostics) or a failed launch records `done` as a marker.
+struct KBind {
+  Handle *h;
+  int k;
+  hipStream_t s;
+  hipEvent_t a = nullptr, done;
+  bool on, bound = false;
+  KBind(Handle *hh, int kk, hipStream_t ss, hipEvent_t d)
+      : h(hh), k(kk), s(ss), done(d), on(hh->timing && hh->step % static_cast<uint64_t>(hh->timing_every) == 0) {
+    if (on) {
+      timing_release(h, done);
+      a = ev_get(h);
+    }
+    set_launch_events(a, done);
+  }
+  // after a successful launch call
+  void launched() { bound = true; }
+  ~KBind() {
+    set_launch_events(nullptr, nullptr);
+    if (bound) {
+      if (on) h->pending.push_back({k, a, done, false});
+    } else {
+      if (on) h->pool.push_back(a);
+      hipEventRecord(done, s);
     }
   }
 };
@@ -212,26 +266,13 @@ static void harvest_timing(Handle *h) {
   for (; k < h->pending.size(); ++k) {
     auto &p = h->pending[k];
     if (hipEventQuery(p.b) != hipSuccess) break;
-    float ms = 0.0f;
-    hipEventElapsedTime(&ms, p.a, p.b);
-    h->kms[p.k] += ms;
-    h->klaunch[p.k]++;
-    h->pool.push_back(p.a);
-    h->pool.push_back(p.b);
+    timing_take(h, p, false);
   }
   h->pending.erase(h->pending.begin(), h->pending.begin() + static_cast<std::ptrdiff_t>(k));
 }
 
 static void collect_timing(Handle *h) {
-  for (auto &p : h->pending) {
-    float ms = 0.0f;
-    hipEventSynchronize(p.b);
-    hipEventElapsedTime(&ms, p.a, p.b);
-    h->kms[p.k] += ms;
-    h->klaunch[p.k]++;
-    h->pool.push_back(p.a);
-    h->pool.push_back(p.b);
-  }
+  for (auto &p : h->pending) timing_take(h, p, true);
   h->pending.clear();
 }
 
@@ -577,7 +618,7 @@ static void destroy(Handle *h) {
   if (h->sD) hipStreamSynchronize(h->sD);
   for (auto &p : h->pending) {
     hipEventDestroy(p.a);
-    hipEventDestroy(p.b);
+    if (p.b_pool) hipEventDestroy(p.b);
   }
   for (auto e : h->pool) hipEventDestroy(e);
   for (TimingSet *t : {&h->t_af, &h->t_mono, &h->t_rds}) {
@@ -658,10 +699,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
-    HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(false)));
-    HIP_TRY(hipEventCreateWithFlags(&h->evB[b], ev_flags(false)));
-    HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(false)));
-    HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(false)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(true)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evB[b], ev_flags(true)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(true)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(true)));
   }
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, ev_flags(false)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, ev_flags(false)));
@@ -743,7 +784,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_win[b], C * 32)) != FMX_OK) return rc;
-    HIP_TRY(hipEventCreateWithFlags(&h->evR[b], ev_flags(false)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evR[b], ev_flags(true)));
   }
   // construct every object (RS_CREATE) then apply main.cpp's configuration
   std::fill(h->hmask.begin(), h->hmask.end(), static_cast<int>(RS_CREATE));
@@ -951,18 +992,18 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.next_sched_dst = h->t_rds.d_slot[nbuf];
       a.next_sched_n16 = spec16;
     }
-    KTimer t(h, FMX_K_FRONTEND, h->sA);
+    KBind t(h, FMX_K_FRONTEND, h->sA, h->evA[buf]);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
       return rc;
     }
+    t.launched();
     dec_advance(h, n);
   }
   if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later
     HIP_TRY(hipEventRecord(h->t_rds.ev_h[h->t_rds.spec_img], h->sA));
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
-  HIP_TRY(hipEventRecord(h->evA[buf], h->sA));
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
   if (rds) {
@@ -986,23 +1027,30 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       r.out_stride = h->rds_stride;
       // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
       r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
-      KTimer t(h, FMX_K_RS, h->sC);
-      if (!FMX_SKIP(rds) && (rc = launch_rs(r, h->sC)) != FMX_OK) {
-        h->err = "rds resampler launch failed";
-        return rc;
+      {
+        KBind t(h, FMX_K_RS, h->sC, h->evR[buf]);
+        if (!FMX_SKIP(rds)) {
+          if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
+            h->err = "rds resampler launch failed";
+            return rc;
+          }
+          t.launched();
+        }
       }
-      HIP_TRY(hipEventRecord(h->evR[buf], h->sC));
       h->evR_set[buf] = true;
     }
-    KTimer t(h, FMX_K_RDS, h->sC);
-    if (!FMX_SKIP(rds) && (rc = launch_rds(a, h->sC)) != FMX_OK) {
-      h->err = "rds launch failed";
-      return rc;
+    KBind t(h, FMX_K_RDS, h->sC, h->evC[buf]);
+    if (!FMX_SKIP(rds)) {
+      if ((rc = launch_rds(a, h->sC)) != FMX_OK) {
+        h->err = "rds launch failed";
+        return rc;
+      }
+      t.launched();
     }
-  } else if (o->d_group_count) {
-    HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
+  } else {
+    if (o->d_group_count) HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
+    HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
   }
-  HIP_TRY(hipEventRecord(h->evC[buf], h->sC));
   h->evC_set[buf] = true;
   // ---- stereo PLL (sB) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
@@ -1011,17 +1059,20 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.stereo_out = o->d_stereo;
     a.pilot_tenths_out = o->d_pilot_tenths;
     a.indicator_out = o->d_stereo_indicator;
-    KTimer t(h, FMX_K_STEREO, h->sB);
-    if (!FMX_SKIP(pll) && (rc = launch_pll(a, h->sB)) != FMX_OK) {
-      h->err = "pll launch failed";
-      return rc;
+    KBind t(h, FMX_K_STEREO, h->sB, h->evB[buf]);
+    if (!FMX_SKIP(pll)) {
+      if ((rc = launch_pll(a, h->sB)) != FMX_OK) {
+        h->err = "pll launch failed";
+        return rc;
+      }
+      t.launched();
     }
   } else {
     if (o->d_stereo) HIP_TRY(hipMemsetAsync(o->d_stereo, 0, sizeof(int) * h->C, h->sB));
     if (o->d_pilot_tenths) HIP_TRY(hipMemsetAsync(o->d_pilot_tenths, 0, sizeof(int) * h->C, h->sB));
     if (o->d_stereo_indicator) HIP_TRY(hipMemsetAsync(o->d_stereo_indicator, 0, sizeof(int) * h->C, h->sB));
+    HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
   }
-  HIP_TRY(hipEventRecord(h->evB[buf], h->sB));
   h->evB_set[buf] = true;
   // ---- audio (sD): after the PLL (stereo) / the front end (mono), and
   // after k_rds, so that evD closes the step ----
@@ -1051,13 +1102,15 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.mute = h->mute;
     a.mute_fade = h->cfg.out_rate / 200;
     audio_signal_level(h, a, o, buf, n);
-    KTimer t(h, FMX_K_AUDIO, h->sD);
-    if (!FMX_SKIP(audio) && (rc = launch_audio(a, h->sD)) != FMX_OK) {
-      h->err = "audio launch failed";
-      return rc;
+    KBind t(h, FMX_K_AUDIO, h->sD, h->evD[buf]);
+    if (!FMX_SKIP(audio)) {
+      if ((rc = launch_audio(a, h->sD)) != FMX_OK) {
+        h->err = "audio launch failed";
+        return rc;
+      }
+      t.launched();
     }
   }
-  HIP_TRY(hipEventRecord(h->evD[buf], h->sD));
   h->evD_set[buf] = true;
   h->block_index++;
   step_done(h, stereo);

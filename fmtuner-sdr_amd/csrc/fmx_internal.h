@@ -173,6 +173,11 @@ struct RsArgs {
 // launchers (fmx_kernels.hip); stream is a hipStream_t
 // vec: the caller guarantees every channel's decimator history is full
 // (dec_valid == L-1); 16-B row alignment is checked here.
+// Events bound to the NEXT main-kernel launch of this thread (k_fe8 /
+// k_frontend, k_pll, k_audio, k_rs, k_rds) through hipExtLaunchKernel: `stop`
+// completes with the kernel and `start` (timing) takes its start time -- no
+// marker packets between two kernels of a stream.  Consumed by that launch.
+void set_launch_events(void *start, void *stop);
 int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec = false);
 // whether launch_frontend_m would run k_fe8 for these arguments
 bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec);

@@ -24,6 +24,7 @@
 // Build with -ffp-contract=off: wherever the reference's arithmetic order is
 // reproduced (IIRs, PLL, resamplers, RDS FIR) products and sums must round
 // separately.  The large FIRs use explicit fmaf.
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
@@ -1858,7 +1859,10 @@ __device__ __forceinline__ float rds_sum8(float x) {
 }
 
 __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
-  __builtin_amdgcn_s_setprio(2); // beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
+#ifndef FMX_RDS_PRIO
+#define FMX_RDS_PRIO 2
+#endif
+  __builtin_amdgcn_s_setprio(FMX_RDS_PRIO); // beside the front end's waves (round 1: 1.39 -> 1.375 ms/step)
   // dynamic LDS (sizeof(RdsLds) at launch): with a static size the backend
   // sees an LDS-limited occupancy and pads every wave's register allocation
   // up to it
@@ -2463,9 +2467,13 @@ __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
 #define FE8_MINB 1
 #endif
 template <int M, int TPP, bool RS>
+#ifndef FMX_FE_PRIO
+#define FMX_FE_PRIO 0 // k_fe8's wave priority (s_setprio) beside the other streams' waves
+#endif
 __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP, RS>;
+  if (FMX_FE_PRIO > 0) __builtin_amdgcn_s_setprio(FMX_FE_PRIO);
   constexpr int L = LY::L;
   uint8_t *raw = reinterpret_cast<uint8_t *>(smem);
   float2 *yb = reinterpret_cast<float2 *>(smem + LY::YB);
@@ -3090,6 +3098,21 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
   fe_next_sched_copy(a);
 }
 
+// the events of set_launch_events, consumed by the next fmx_launch
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+void set_launch_events(void *start, void *stop) {
+  t_ev_start = static_cast<hipEvent_t>(start);
+  t_ev_stop = static_cast<hipEvent_t>(stop);
+}
+template <typename K, typename... Args>
+static int fmx_launch(K kernel, dim3 grid, dim3 block, size_t smem, hipStream_t st, Args... args) {
+  hipEvent_t e0 = t_ev_start, e1 = t_ev_stop;
+  t_ev_start = t_ev_stop = nullptr;
+  if (e0 || e1) hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)smem, st, e0, e1, 0u, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, smem, st, args...);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+
 template <int M, int TPP, bool RS> static int fe8_launch_rs(const FeArgs &a, hipStream_t st) {
   // 160 KB per CU: two k_fe8 workgroups (512-B allocation granules) beside one
   // k_pll or k_rds workgroup (36 KB each, 36 864 B allocated)
@@ -3103,8 +3126,7 @@ template <int M, int TPP, bool RS> static int fe8_launch_rs(const FeArgs &a, hip
       return FMX_E_HIP;
     configured = true;
   }
-  hipLaunchKernelGGL((k_fe8<M, TPP, RS>), dim3(a.C), dim3(256), smem, st, a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_fe8<M, TPP, RS>, dim3(a.C), dim3(256), smem, st, a);
 }
 // the resampler in the kernel, or (rds_win_out set) left to k_rs
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
@@ -3123,8 +3145,7 @@ template <int M, int TPP, bool VEC> static int fe_launch(const FeArgs &a, hipStr
       return FMX_E_HIP;
     configured = true;
   }
-  hipLaunchKernelGGL((k_frontend<M, TPP, VEC>), dim3(a.C), dim3(256), smem, st, a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_frontend<M, TPP, VEC>, dim3(a.C), dim3(256), smem, st, a);
 }
 
 } // namespace fmx
@@ -3165,12 +3186,10 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
 }
 int launch_audio(const AudioArgs &a, void *stream) {
-  hipLaunchKernelGGL(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
 }
 /* ================================================================== */
 /* k_rs: the RDS resampler 240k -> 171k (subcarrier.cpp:117-147) on MFMA */
@@ -3336,15 +3355,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 
 int launch_rs(const RsArgs &a, void *stream) {
   static_assert(sizeof(RsLds) <= 16 * 1024, "k_rs LDS");
-  hipLaunchKernelGGL(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), sizeof(RsLds), static_cast<hipStream_t>(stream), a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), sizeof(RsLds), static_cast<hipStream_t>(stream), a);
 }
 int launch_rds(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
   // k_rds workgroups fit beside them
   static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
-  hipLaunchKernelGGL(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
-  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+  return fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
 }
 // 16-B words src -> dst (the schedule upload from mapped pinned memory)
 __global__ void k_copy16(const uint4 *src, uint4 *dst, size_t n16) {
