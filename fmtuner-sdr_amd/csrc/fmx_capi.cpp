@@ -43,6 +43,10 @@ namespace fmx {
 // schedules one step early on sB: the front end then waited, through the
 // upload's event, for the previous step's k_pll -- 35-50 us per step.)
 #define FMX_HSLOTS 8 // pinned schedule images per timing set
+// device schedule slots per timing set: one more than the intermediates'
+// slots, so that the RDS slot the front end of step k fills for step k+1 was
+// last read at step k-3 -- covered by the front end's one wait (evD(k-3))
+#define FMX_SSLOTS (FMX_NBUF + 1)
 struct TimingSet {
   float del = 1.0f;
   std::vector<ResampTiming> groups;
@@ -51,7 +55,7 @@ struct TimingSet {
   int G = 0;   // groups in the last simulated step
   int cur = 0; // slot holding the schedules of the step being launched
   size_t slot_bytes = 0;
-  unsigned char *d_slot[FMX_NBUF] = {};
+  unsigned char *d_slot[FMX_SSLOTS] = {};
   // pinned staging images, a ring deeper than the device slots: the image
   // reused at step k was copied at step k - FMX_HSLOTS, long complete, so the
   // host never blocks on it (with one image per device slot the host waited
@@ -59,11 +63,12 @@ struct TimingSet {
   unsigned char *h_slot[FMX_HSLOTS] = {};
   const void *h_dev[FMX_HSLOTS] = {}; // the images' device-side addresses (mapped pinned memory)
   int hnext = 0, hcur = 0; // next image to fill, image of the last simulation
-  hipEvent_t ev_h[FMX_HSLOTS] = {}; // after the last copy out of h_slot[i]
+  hipEvent_t ev_h[FMX_HSLOTS] = {}; // recorded after a copy kernel's read of h_slot[i]
+  hipEvent_t ev_use[FMX_HSLOTS] = {}; // the event marking the last read of h_slot[i]: ev_h[i], or the front end's evA
   bool ev_h_set[FMX_HSLOTS] = {};
-  FmxSched *d_sched[FMX_NBUF] = {};
-  int *d_count[FMX_NBUF] = {};
-  int *d_group[FMX_NBUF] = {};
+  FmxSched *d_sched[FMX_SSLOTS] = {};
+  int *d_count[FMX_SSLOTS] = {};
+  int *d_group[FMX_SSLOTS] = {};
   hipStream_t up_stream = nullptr; // stream of the last copy into the slots (the set's reader)
   // one step of speculation (the RDS set of process_block): the next step's
   // schedules for the same n, simulated into pinned image spec_img and copied
@@ -122,8 +127,6 @@ struct Handle {
   float *mpx[FMX_NBUF] = {}, *pilot[FMX_NBUF] = {}, *rds_in[FMX_NBUF] = {};
   int *rds_count[FMX_NBUF] = {};
   float *rds_win[FMX_NBUF] = {};  // [C][32] the previous call's last MPX samples, k_fe8 -> k_rs
-  hipEvent_t evR[FMX_NBUF] = {};  // after k_rs of the slot's step (it reads the RDS schedule slot)
-  bool evR_set[FMX_NBUF] = {};
   float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
   uint32_t block_index = 0;
@@ -135,6 +138,7 @@ struct Handle {
   // diagnostics build only (make variant V=diag KDEFS=-DFMX_DIAG=1): kernels
   // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
   bool skip_rds = false, skip_pll = false, skip_audio = false;
+  bool nowait_a = false; // FMX_DIAG_NOWAIT=1: the front end skips its cross-stream waits (outputs invalid)
 #endif
   struct Pending {
     int k;
@@ -223,23 +227,28 @@ static void timing_release(Handle *h, hipEvent_t e) {
   h->pending.erase(h->pending.begin(), h->pending.begin() + static_cast<std::ptrdiff_t>(last));
 }
 
-// process_block's launches: the stream's completion event `done` (evA / evR /
-// evC / evB / evD) is bound to the kernel itself through hipExtLaunchKernel
-// (set_launch_events), and with timing on a pool event takes its start: no
-// marker packets between the kernels of a stream (each marker was a packet
-// the next kernel and every cross-stream waiter queued behind).  A kernel
-// left out (diagnostics) or a failed launch records `done` as a marker.
+// process_block's launches: the stream's completion event `done` (evA / evC /
+// evB / evD, or none) is bound to the kernel itself through hipExtLaunchKernel
+// (set_launch_events), and with timing on a pool event takes its start (and
+// its end when there is no `done`): no marker packets between the kernels of
+// a stream (each marker was a packet the next kernel and every cross-stream
+// waiter queued behind).  A kernel left out (diagnostics) or a failed launch
+// records `done` as a marker.
 struct KBind {
   Handle *h;
   int k;
   hipStream_t s;
   hipEvent_t a = nullptr, done;
-  bool on, bound = false;
+  bool on, bound = false, own = false; // own: `done` from the pool (timing only)
   KBind(Handle *hh, int kk, hipStream_t ss, hipEvent_t d)
       : h(hh), k(kk), s(ss), done(d), on(hh->timing && hh->step % static_cast<uint64_t>(hh->timing_every) == 0) {
     if (on) {
-      timing_release(h, done);
+      if (done) timing_release(h, done);
       a = ev_get(h);
+      if (!done) {
+        done = ev_get(h);
+        own = true;
+      }
     }
     set_launch_events(a, done);
   }
@@ -248,10 +257,11 @@ struct KBind {
   ~KBind() {
     set_launch_events(nullptr, nullptr);
     if (bound) {
-      if (on) h->pending.push_back({k, a, done, false});
+      if (on) h->pending.push_back({k, a, done, own});
     } else {
       if (on) h->pool.push_back(a);
-      hipEventRecord(done, s);
+      if (own) h->pool.push_back(done);
+      else if (done) hipEventRecord(done, s);
     }
   }
 };
@@ -285,7 +295,7 @@ static FmxSched *tset_hsched(const Handle *h, TimingSet &t, int b) {
   return reinterpret_cast<FmxSched *>(t.h_slot[b] + tset_sched_off(h, t)); // b: host image
 }
 static void tset_free_slots(Handle *h, TimingSet &t) {
-  for (int b = 0; b < FMX_NBUF; ++b) {
+  for (int b = 0; b < FMX_SSLOTS; ++b) {
     if (t.d_slot[b]) {
       h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), static_cast<void *>(t.d_slot[b])),
                       h->allocs.end());
@@ -302,7 +312,7 @@ static int tset_alloc_slots(Handle *h, TimingSet &t) {
   const size_t off = tset_sched_off(h, t);
   t.slot_bytes = (off + sizeof(FmxSched) * static_cast<size_t>(t.stride) * t.cap_groups + 15) & ~static_cast<size_t>(15);
   int rc;
-  for (int b = 0; b < FMX_NBUF; ++b) {
+  for (int b = 0; b < FMX_SSLOTS; ++b) {
     if ((rc = dalloc(h, &t.d_slot[b], t.slot_bytes)) != FMX_OK) return rc;
 
     t.d_group[b] = reinterpret_cast<int *>(t.d_slot[b]);
@@ -393,7 +403,7 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
   const int hb = t.hnext;
   t.hnext = (hb + 1) % FMX_HSLOTS;
   t.hcur = hb;
-  if (t.ev_h_set[hb]) HIP_TRY(hipEventSynchronize(t.ev_h[hb]));
+  if (t.ev_h_set[hb]) HIP_TRY(hipEventSynchronize(t.ev_use[hb]));
   FmxSched *hs = tset_hsched(h, t, hb);
   int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
   int mx = 0;
@@ -422,6 +432,7 @@ static int tset_upload(Handle *h, TimingSet &t, int buf, hipStream_t s) {
   }
   if (launch_copy16(t.h_dev[t.hcur], t.d_slot[buf], (bytes + 15) / 16, s) != FMX_OK) return FMX_E_HIP;
   HIP_TRY(hipEventRecord(t.ev_h[t.hcur], s));
+  t.ev_use[t.hcur] = t.ev_h[t.hcur];
   t.ev_h_set[t.hcur] = true;
   t.up_stream = s;
   return FMX_OK;
@@ -463,7 +474,7 @@ static unsigned tset_speculate(Handle *h, TimingSet &t, int n, int slot, size_t 
   const size_t n16 = (bytes + 15) / 16;
   if (G > t.cap_groups || n16 > threads) return 0;
   const int hb = t.hnext;
-  if (t.ev_h_set[hb] && hipEventSynchronize(t.ev_h[hb]) != hipSuccess) return 0;
+  if (t.ev_h_set[hb] && hipEventSynchronize(t.ev_use[hb]) != hipSuccess) return 0;
   t.spec_groups = t.groups;
   FmxSched *hs = tset_hsched(h, t, hb);
   int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
@@ -628,7 +639,7 @@ static void destroy(Handle *h) {
   }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
-    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evR[b]})
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
@@ -690,6 +701,13 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     h->skip_audio = v.find("audio") != std::string::npos;
   }
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') serial = true;
+  if (const char *e = std::getenv("FMX_DIAG_NOWAIT"); e && e[0] == '1') h->nowait_a = true;
+  if (const char *e = std::getenv("FMX_DIAG_SAPRIO"); e && e[0] == '1') {
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(hipStreamDestroy(h->sA));
+    HIP_TRY(hipStreamCreateWithPriority(&h->sA, hipStreamNonBlocking, hi));
+  }
 #endif
   if (serial) {
     h->sB = h->sC = h->sD = h->sA;
@@ -784,7 +802,6 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_win[b], C * 32)) != FMX_OK) return rc;
-    HIP_TRY(hipEventCreateWithFlags(&h->evR[b], ev_flags(true)));
   }
   // construct every object (RS_CREATE) then apply main.cpp's configuration
   std::fill(h->hmask.begin(), h->hmask.end(), static_cast<int>(RS_CREATE));
@@ -948,16 +965,22 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   const int prev = (buf + FMX_NBUF - 1) % FMX_NBUF;
   // slot buf was last read by step k-FMX_NBUF; a caller-owned MPX buffer by
   // step k-1's readers
-  if (o->d_mpx && h->evD_set[prev]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[prev], 0));
+#if FMX_DIAG
+  const bool wait_a = !h->nowait_a;
+#else
+  constexpr bool wait_a = true;
+#endif
+  if (!wait_a) {
+  } else if (o->d_mpx && h->evD_set[prev]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[prev], 0));
   else if (h->evD_set[buf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evD[buf], 0));
-  // RDS resampler schedule of this step (read by the front end only): the
-  // slot the previous front end filled when the speculation holds, else a
-  // copy kernel on sA; then the next step's, copied by this front end
-  if (rds && (rc = tset_take_or_advance(h, h->t_rds, n, buf, h->sA)) != FMX_OK) return rc;
-  const int nbuf = (buf + 1) % FMX_NBUF;
-  const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nbuf, static_cast<size_t>(h->C) * 256) : 0u;
-  // slot nbuf was last read by k_rs two steps ago (sC): the front end's copy waits for it
-  if (spec16 && h->evR_set[nbuf]) HIP_TRY(hipStreamWaitEvent(h->sA, h->evR[nbuf], 0));
+  // RDS resampler schedule of this step (read by k_rs, or by the front end):
+  // the slot the previous front end filled when the speculation holds, else a
+  // copy kernel on sA; then the next step's, copied by this front end into
+  // slot k+1 of FMX_SSLOTS, last read by step k-3's k_rs (sC) -- before
+  // evD(k-3), which the front end waits for: no second wait
+  const int rslot = static_cast<int>(h->step % FMX_SSLOTS), nrslot = static_cast<int>((h->step + 1) % FMX_SSLOTS);
+  if (rds && (rc = tset_take_or_advance(h, h->t_rds, n, rslot, h->sA)) != FMX_OK) return rc;
+  const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nrslot, static_cast<size_t>(h->C) * 256) : 0u;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
   bool use_rs = false;
@@ -989,7 +1012,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.sig_sums = o->d_signal ? h->sig_sums[buf] : nullptr;
     if (spec16) {
       a.next_sched_src = h->t_rds.h_dev[h->t_rds.spec_img];
-      a.next_sched_dst = h->t_rds.d_slot[nbuf];
+      a.next_sched_dst = h->t_rds.d_slot[nrslot];
       a.next_sched_n16 = spec16;
     }
     KBind t(h, FMX_K_FRONTEND, h->sA, h->evA[buf]);
@@ -1000,8 +1023,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     t.launched();
     dec_advance(h, n);
   }
-  if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later
-    HIP_TRY(hipEventRecord(h->t_rds.ev_h[h->t_rds.spec_img], h->sA));
+  if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later: its read ends with the front end
+    h->t_rds.ev_use[h->t_rds.spec_img] = h->evA[buf];
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
@@ -1027,17 +1050,14 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       r.out_stride = h->rds_stride;
       // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
       r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
-      {
-        KBind t(h, FMX_K_RS, h->sC, h->evR[buf]);
-        if (!FMX_SKIP(rds)) {
-          if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
-            h->err = "rds resampler launch failed";
-            return rc;
-          }
-          t.launched();
+      KBind t(h, FMX_K_RS, h->sC, nullptr);
+      if (!FMX_SKIP(rds)) {
+        if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
+          h->err = "rds resampler launch failed";
+          return rc;
         }
+        t.launched();
       }
-      h->evR_set[buf] = true;
     }
     KBind t(h, FMX_K_RDS, h->sC, h->evC[buf]);
     if (!FMX_SKIP(rds)) {
@@ -1506,7 +1526,7 @@ int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_gro
     return FMX_OK;
   }
   const int buf = static_cast<int>(h->step % FMX_NBUF);
-  if ((rc = tset_advance(h, h->t_rds, n, buf, h->sA, nullptr)) != FMX_OK) return rc;
+  if ((rc = tset_advance(h, h->t_rds, n, static_cast<int>(h->step % FMX_SSLOTS), h->sA, nullptr)) != FMX_OK) return rc;
   {
     FeArgs a = fe_args(h, n, FE_IN_MPX, buf);
     a.in_f = d_mpx;

@@ -1061,10 +1061,11 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
 /* ================================================================== */
 /* k_audio: one workgroup (256 threads) per channel, the call in chunks of
  * AU2_T DSP samples, L and R carried together as packed (L, R) pairs:
- *   L/R 121-tap FIR          8 consecutive outputs per thread, every input
- *                            pair read once per thread and fed to 8 packed
- *                            FMAs (per output the same FMA chain, oldest
- *                            sample first, as before)           stereo_decoder.cpp:281-282
+ *   L/R 121-tap FIRs         v_mfma_f32_16x16x32_f16: the pilot BPF's
+ *                            Toeplitz tiles (k_fe8) on f16 hi / lo images
+ *                            of the chunk's L and R (x 2^10) and the
+ *                            design's tap fragments (FmxDesign::lr_frag,
+ *                            x 2^12), three MFMAs per K step   stereo_decoder.cpp:281-282
  *   resampler Fs -> 32 kHz   one output per thread and entry of the host
  *                            timing schedule (branch-transposed bank)   af_post_processor.cpp:56-64
  *   de-emphasis, DC block    block affine scans, 3 outputs per thread,
@@ -1072,37 +1073,20 @@ __device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) 
  *   clamp (main.cpp:1305-1308), stores.
  * Modes: 0 stereo (FIR + AF), 1 AF only, 2 mono FMDemod::downsampleAudio,
  * 3 mono pipeline (x0.5, L = R), 4 FIR only (fmx_stereo). */
-// L/R FIRs on v_mfma_f32_16x16x32_f16 (FMX_AU_MFMA 1): the pilot BPF's
-// Toeplitz tiles (k_fe8) on f16 hi / lo images of the chunk's L and R
-// (x 2^10) and the design's tap fragments (FmxDesign::lr_frag, x 2^12), three
-// MFMAs per K step; 0 keeps the packed-FMA FIR
-#ifndef FMX_AU_MFMA
-#define FMX_AU_MFMA 1
-#endif
 #define AU2_T 2048
-#define AU2_PT 8                        // FIR outputs per thread (AU2_T / 256)
+#define AU2_PT 8                        // chunk inputs per thread (AU2_T / 256)
 #define AU2_MAXOUT (AU2_T / 3 + 16)     // resampler outputs per chunk (ratio >= 3)
-// FIR input image: pair i at i + i/8 (lanes 8 pairs apart land 9 apart:
-// conflict-free ds_read_b64)
-__device__ __forceinline__ int au_xi(int i) { return i + (i >> 3); }
-#define AU_XN ((AU_HALO + AU2_T + 8) * 9 / 8 + 8)
 #define AU_IMG (AU_HALO + AU2_T + 24) // f16 image: 120 history + the chunk + the last K step's reach
-static_assert(4 * AU_IMG * 2 <= AU_XN * 8, "the four f16 images fit the FIR image region");
+#define AU_FN (AU_RHALO + AU2_T)
 struct AuShared {
-  // one region, two lives per chunk: the raw (L, R) FIR image x (au_xi
-  // order, 120 of history first) until the FIR has read it, then the
-  // resampler input f (32 of history first, natural order).  Sharing it
-  // takes the workgroup from 45.6 to 29 KB of LDS: four workgroups per CU
-  // instead of three (isolated 0.206 ms at three, 0.263 at two).
-  float2 xf[AU_XN > AU_RHALO + AU2_T ? AU_XN : AU_RHALO + AU2_T] __attribute__((aligned(16)));
+  // one region, two lives per chunk: the f16 hi / lo images of L and R (120
+  // of history first) until the FIR has read them, then the resampler input
+  // f (32 of history first)
+  float2 xf[AU_IMG > AU_FN ? AU_IMG : AU_FN] __attribute__((aligned(16))); // (4 f16 images = AU_IMG pairs)
   float2 fh[AU_RHALO];                         // f's history between chunks
   float2 o[AU2_MAXOUT];                        // resampler outputs of the chunk
   float hT[FMX_AF_SUB][FMX_NPFB];              // resampler bank transposed: hT[n][b] = h_b[n]
-#if FMX_AU_MFMA
   float2 hf[AU_HALO];                          // the chunk's last 120 (L, R) inputs: the next chunk's FIR history
-#else
-  float lt[136] __attribute__((aligned(16)));  // L/R FIR taps, lt[k + 7] = h[k], zeros around
-#endif
   float ws[3][4][2];                           // scan scratch (A, BL, BR per wave)
   float iir[4];                                // de_L, de_R, dc_L, dc_R
   int eb, ee, count;
@@ -1176,17 +1160,10 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
   // ---- carried state ----
   float *lrh = a.lr_hist + (size_t)c * 2 * (FMX_LR_LEN - 1);
   float *win = mono ? a.mono_win + (size_t)c * 32 : a.af_win + (size_t)c * 2 * 32;
-  float2 *const X = S.xf; // FIR image (au_xi order)
   float2 *const F = S.xf; // resampler input, after the FIR
-#if FMX_AU_MFMA
   // this thread's pair of the FIR history (threads < 120), across chunks
   float2 cx = make_float2(0.0f, 0.0f);
   if (lrfir && tid < AU_HALO) cx = make_float2(lrh[tid], lrh[(FMX_LR_LEN - 1) + tid]);
-  (void)X;
-#else
-  if (lrfir)
-    for (int h = tid; h < AU_HALO; h += 256) X[au_xi(h)] = make_float2(lrh[h], lrh[(FMX_LR_LEN - 1) + h]);
-#endif
   if (af)
     for (int h = tid; h < AU_RHALO; h += 256) S.fh[h] = make_float2(win[h], mono ? 0.0f : win[32 + h]);
   float *iir = mono ? a.mono_iir + (size_t)c * 2 : a.af_iir + (size_t)c * 4;
@@ -1215,10 +1192,6 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     S.eb = 0;
     S.count = 0;
   }
-#if !FMX_AU_MFMA
-  if (lrfir)
-    for (int k = tid; k < 136; k += 256) S.lt[k] = (k >= 7 && k <= 7 + AU_HALO) ? D->lr_pad[k - 7 + 5] : 0.0f;
-#endif
   // tiled input (raw L/R from k_pll): sample j of this channel at tin + ti(j)
   const bool tiled = a.in_tiled != 0;
   const float *inl = a.in_l + (tiled ? lr_tile_idx(c, 0, a.in_stride) : (size_t)c * a.in_stride);
@@ -1255,7 +1228,6 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         vl[k] = (j < cnt) ? inl[ti(n0 + j)] : 0.0f;
         vr[k] = (j < cnt && !mono) ? inr[ti(n0 + j)] : 0.0f;
       }
-#if FMX_AU_MFMA
       if (lrfir) {
         // f16 hi / lo images [L hi | L lo | R hi | R lo], index = chunk sample + 120
         _Float16 *im = reinterpret_cast<_Float16 *>(S.xf);
@@ -1287,19 +1259,10 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
           if (j < cnt) F[AU_RHALO + j] = make_float2(vl[k], vr[k]);
         }
       }
-#else
-#pragma unroll
-      for (int k = 0; k < AU2_PT; ++k) {
-        const int j = tid + 256 * k;
-        if (lrfir) X[au_xi(AU_HALO + j)] = make_float2(vl[k], vr[k]);
-        else if (j < cnt) F[AU_RHALO + j] = make_float2(vl[k], vr[k]);
-      }
-#endif
       if (!lrfir && af && tid < AU_RHALO) F[tid] = S.fh[tid];
     }
     if (tid == 0) S.ee = S.eb;
     __syncthreads();
-#if FMX_AU_MFMA
     // ---- L/R FIR on MFMA: 16 outputs (rows, A = taps) x 16 blocks of 16
     // outputs (columns, B = inputs), K = the block's 136 inputs from 120
     // before it; each wave two tiles of L and of R (512 outputs each) ----
@@ -1329,12 +1292,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
         for (int u = 0; u < 2; ++u) {
           const f16x8_t lh = bLh[32 * u + 4 * ks], ll = bLl[32 * u + 4 * ks]; // + 256 u + 32 ks samples
           const f16x8_t rh = bRh[32 * u + 4 * ks], rl = bRl[32 * u + 4 * ks];
-          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, lh, aL[u], 0, 0, 0);
-          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rh, aR[u], 0, 0, 0);
-          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ll, aL[u], 0, 0, 0);
-          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, rl, aR[u], 0, 0, 0);
-          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, lh, aL[u], 0, 0, 0);
-          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, rh, aR[u], 0, 0, 0);
+          // transposed tiles (images as A, taps as B: the same lane
+          // registers) -- D[block][output]: a 16-lane group holds 16
+          // consecutive outputs
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lh, ahi, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(rh, ahi, aR[u], 0, 0, 0);
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ll, ahi, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(rl, ahi, aR[u], 0, 0, 0);
+          aL[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lh, alo, aL[u], 0, 0, 0);
+          aR[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(rh, alo, aR[u], 0, 0, 0);
         }
       }
       if (tid < AU_HALO) cx = S.hf[tid];
@@ -1343,79 +1309,22 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
       const float osc = sc * (1.0f / 4194304.0f); // taps x 2^12, inputs x 2^10
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
-        const int j = 256 * (2 * wave + u) + 16 * col + 4 * g;
-        float2 y[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = make_float2(aL[u][i] * osc, aR[u][i] * osc);
-        if (af) {
-          float4 *fw = reinterpret_cast<float4 *>(F + AU_RHALO + j); // 16-B aligned: AU_RHALO and j even
-          fw[0] = make_float4(y[0].x, y[0].y, y[1].x, y[1].y);
-          fw[1] = make_float4(y[2].x, y[2].y, y[3].x, y[3].y);
-        }
-        if (a.lr_out_l) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (j + i < cnt) {
-              a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j + i] = y[i].x;
-              a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j + i] = y[i].y;
-            }
-        }
-      }
-    }
-#else
-    // ---- L/R FIR: outputs j0 .. j0+7, inputs j0-120 .. j0+7 ----
-    float2 cx = make_float2(0.0f, 0.0f); // the next chunk's FIR history (X is overwritten by F)
-    if (lrfir) {
-      const int j0 = AU2_PT * tid;
-      f32x2 acc[AU2_PT];
-#pragma unroll
-      for (int r = 0; r < AU2_PT; ++r) acc[r] = f32x2{0.0f, 0.0f};
-#pragma unroll 1
-      for (int m0 = 0; m0 < AU_HALO + AU2_PT; m0 += 8) {
-        // taps k = 113-m0 .. 128-m0 (zero outside 0..120): sample m0+u feeds
-        // output r with tap index 7 + r - u of this window
-        const float4 *tw = reinterpret_cast<const float4 *>(&S.lt[AU_HALO - m0]);
-        const float4 t0 = tw[0], t1 = tw[1], t2 = tw[2], t3 = tw[3];
-        const float t[16] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w,
-                             t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w};
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float2 v = X[au_xi(j0 + m0 + u)]; // input j0 - 120 + m0 + u
-          const f32x2 vv = f32x2{v.x, v.y};
-#pragma unroll
-          for (int r = 0; r < AU2_PT; ++r) {
-            const float h = t[7 + r - u];
-            acc[r] = __builtin_elementwise_fma(f32x2{h, h}, vv, acc[r]);
-          }
-        }
-      }
-      if (tid < AU_HALO) cx = X[au_xi(tid + cnt)];
-      __syncthreads(); // X is read: F takes its place
-      if (af && tid < AU_RHALO) F[tid] = S.fh[tid];
-      // the 8 outputs as four 16-B writes (8-B writes 64 B apart across the
-      // lanes met 8-way bank conflicts); F[AU_RHALO + 8 tid] is 16-B aligned
-      static_assert(AU_RHALO % 2 == 0 && AU2_PT == 8, "k_audio FIR output writes");
-      if (af && j0 + AU2_PT <= cnt) {
-        float4 *fw = reinterpret_cast<float4 *>(F + AU_RHALO + j0);
-#pragma unroll
-        for (int r = 0; r < AU2_PT; r += 2)
-          fw[r / 2] = make_float4(acc[r].x * sc, acc[r].y * sc, acc[r + 1].x * sc, acc[r + 1].y * sc);
-      }
-#pragma unroll
-      for (int r = 0; r < AU2_PT; ++r) {
-        const int j = j0 + r;
-        if (j < cnt) {
-          const float2 y = make_float2(acc[r].x * sc, acc[r].y * sc);
-          if (af && j0 + AU2_PT > cnt) F[AU_RHALO + j] = y;
-          if (a.lr_out_l) {
+        for (int i = 0; i < 4; ++i) {
+          // lane: output 256 (2 wave + u) + 16 (4 g + i) + col -- a 16-lane
+          // group writes 16 consecutive pairs: conflict-free ds_write_b64
+          // (untransposed, 4 consecutive outputs per lane, 16-B writes 128 B
+          // apart across an 8-lane group: 8-way)
+          const int j = 256 * (2 * wave + u) + 16 * (4 * g + i) + col;
+          const float2 y = make_float2(aL[u][i] * osc, aR[u][i] * osc);
+          if (af) F[AU_RHALO + j] = y;
+          if (a.lr_out_l && j < cnt) {
             a.lr_out_l[(size_t)c * a.lr_out_stride + n0 + j] = y.x;
             a.lr_out_r[(size_t)c * a.lr_out_stride + n0 + j] = y.y;
           }
         }
       }
     }
-#endif
     __syncthreads();
     if (af) {
       // ---- resampler: one schedule entry per thread ----
@@ -1430,22 +1339,31 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
           const bool boundary = (en3[k].packed >> 24) & 1;
           const int b0 = boundary ? FMX_NPFB - 1 : b, b1 = boundary ? 0 : b + 1;
           const int i0 = boundary ? i - 1 : i;
-          f32x2 y0 = f32x2{0.0f, 0.0f}, y1 = f32x2{0.0f, 0.0f};
+          // scalar multiply-then-add per channel and branch (the reference's
+          // two roundings), as asm: the vectoriser's packed-FP32 form put LDS
+          // loads right over the sources of a just-issued v_pk_* op (the
+          // pattern tests/test_isa_scan.py keeps out of the shipped kernels)
+          float y0l = 0.0f, y0r = 0.0f, y1l = 0.0f, y1r = 0.0f;
+          auto mac = [](float &y, float h, float x) __attribute__((always_inline)) {
+            float t;
+            asm("v_mul_f32 %0, %2, %3\n\tv_add_f32 %1, %1, %0" : "=&v"(t), "+v"(y) : "v"(h), "v"(x));
+          };
 #pragma unroll
           for (int m = 0; m < FMX_AF_SUB; ++m) {
             const float2 v0 = F[AU_RHALO + i0 - (FMX_AF_SUB - 1) + m];
             const float2 v1 = F[AU_RHALO + i - (FMX_AF_SUB - 1) + m];
             const float h0 = S.hT[FMX_AF_SUB - 1 - m][b0], h1 = S.hT[FMX_AF_SUB - 1 - m][b1];
-            const f32x2 p0 = f32x2{h0, h0} * f32x2{v0.x, v0.y};
-            const f32x2 p1 = f32x2{h1, h1} * f32x2{v1.x, v1.y};
-            y0 = y0 + p0;
-            y1 = y1 + p1;
+            mac(y0l, h0, v0.x);
+            mac(y0r, h0, v0.y);
+            mac(y1l, h1, v1.x);
+            mac(y1r, h1, v1.y);
           }
           const float mu = en3[k].mu, omu = 1.0f - mu;
-          const f32x2 w0 = f32x2{omu, omu} * y0;
-          const f32x2 w1 = f32x2{mu, mu} * y1;
-          const f32x2 y = w0 + w1;
-          S.o[e - eb] = make_float2(y.x, y.y);
+          float yl, yr;
+          asm("v_mul_f32 %0, %2, %3\n\tv_mul_f32 %1, %2, %4" : "=&v"(yl), "=&v"(yr) : "v"(omu), "v"(y0l), "v"(y0r));
+          mac(yl, mu, y1l);
+          mac(yr, mu, y1r);
+          S.o[e - eb] = make_float2(yl, yr);
           last = e;
         }
       }
@@ -1539,27 +1457,15 @@ __global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
     {
       float2 cf = make_float2(0.0f, 0.0f);
       if (af && tid < AU_RHALO) cf = F[tid + cnt];
-      __syncthreads(); // F is dead: X takes its place again
-#if !FMX_AU_MFMA
-      if (lrfir && tid < AU_HALO) X[au_xi(tid)] = cx;
-#endif
+      __syncthreads(); // F is dead: the next chunk's images take its place
       if (af && tid < AU_RHALO) S.fh[tid] = cf;
       __syncthreads();
     }
   }
-#if FMX_AU_MFMA
   if (lrfir && tid < AU_HALO) {
     lrh[tid] = cx.x;
     lrh[(FMX_LR_LEN - 1) + tid] = cx.y;
   }
-#else
-  if (lrfir)
-    for (int h = tid; h < AU_HALO; h += 256) {
-      const float2 v = X[au_xi(h)];
-      lrh[h] = v.x;
-      lrh[(FMX_LR_LEN - 1) + h] = v.y;
-    }
-#endif
   if (af) {
     for (int h = tid; h < AU_RHALO; h += 256) {
       const float2 v = S.fh[h];
@@ -2398,6 +2304,13 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
 #define FMX_DEC_UNROLL 1
 #endif
 __host__ __device__ constexpr int fe8_i(int i) { return i + (i >> 3); }
+// Decimator staging (k_fe8): output o as float2 at o + 2 (o / 32), i.e. one
+// 16-B pad per 16 float4 pairs.  The transposed MFMA tiles write 16
+// consecutive outputs per 16-lane ds_write_b64 group (conflict-free either
+// way); each thread then reads its 8 consecutive outputs as four b128 pairs,
+// 64 B apart across the lanes -- 4-way on the 256-B bank row unpadded,
+// conflict-free padded (tools/lds_banks.py, the guide's lane groups).
+__device__ __forceinline__ int fe8_stg(int o) { return o + 2 * (o >> 5); }
 typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
 
@@ -2444,9 +2357,10 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   static constexpr int BYTES = SH + (int)sizeof(FeShared);
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
-  // (16-B aligned, above the complex image, inside the dead raw region)
-  static constexpr int STG = (YB + 15) & ~15;
-  static_assert(STG + FE8_T * 8 <= R0, "decimator staging inside the raw region");
+  // (fe8_stg order), in the raw region once every wave has read it; read
+  // back before the barrier after which the IQ images take the region
+  static constexpr int STG = 0;
+  static_assert(STG + (FE8_T + 2 * (FE8_T / 32)) * 8 <= R0, "decimator staging (padded, fe8_stg) inside the raw region");
   // LDS-DMA targets (determinism): the early pieces of
   // the next chunk land below uc while the RDS resampler reads uc; the late
   // pieces cover uc only after the barrier that ends its reads, and no piece
@@ -2463,14 +2377,14 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
 // rounded up to 8k + 1 (up to 7 zero taps at the oldest end, same sums), so
 // every K step starts on an 8-sample boundary.
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
-#ifndef FE8_MINB
-#define FE8_MINB 1
-#endif
+// register budget: two workgroups (8 waves) per CU beside a k_pll / k_rds /
+// k_rs wave -- <= 168 VGPRs (3 waves per SIMD); M = 8 (the reference's
+// 2.048 MS/s rate) keeps its longer decimator window at 2
 template <int M, int TPP, bool RS>
 #ifndef FMX_FE_PRIO
 #define FMX_FE_PRIO 0 // k_fe8's wave priority (s_setprio) beside the other streams' waves
 #endif
-__global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 : 3))) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP, RS>;
   if (FMX_FE_PRIO > 0) __builtin_amdgcn_s_setprio(FMX_FE_PRIO);
@@ -2701,34 +2615,33 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
           const f16x2_t q2 = cvt(w.z, 0x04030401u), q3 = cvt(w.w, 0x04030401u);
           const f16x8_t bi = {i0.x, i0.y, i1.x, i1.y, i2.x, i2.y, i3.x, i3.y};
           const f16x8_t bq = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bi, acc[u][0], 0, 0, 0);
-          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bq, acc[u][1], 0, 0, 0);
-          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bi, acc[u][0], 0, 0, 0);
-          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bq, acc[u][1], 0, 0, 0);
+          // transposed tile (bytes as A, taps as B: the same lane
+          // registers): D[block][output], so the 16 lanes of a group hold 16
+          // consecutive outputs
+          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bi, ahi, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq, ahi, acc[u][1], 0, 0, 0);
+          acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bi, alo, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq, alo, acc[u][1], 0, 0, 0);
         }
       }
       FE_STAMP_D(2)
       __syncthreads(); // every wave is past raw: its outputs go to the (aliased) staging area
-      float4 *stg = reinterpret_cast<float4 *>(smem + LY::STG);
+      float2 *stg = reinterpret_cast<float2 *>(smem + LY::STG);
       const float dc = D->dec_dc16, sc = D->dec_scale16;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
-        const int o = 256 * (2 * wave + u) + 16 * col + 4 * g;
-        float yr[4], yi[4];
+        // lane: outputs 256 (2 wave + u) + 16 (4 g + i) + col, i = 0..3
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          yr[i] = (acc[u][0][i] - dc) * sc;
-          yi[i] = (acc[u][1][i] - dc) * sc;
+          const int o = 256 * (2 * wave + u) + 16 * (4 * g + i) + col;
+          stg[fe8_stg(o)] = make_float2((acc[u][0][i] - dc) * sc, (acc[u][1][i] - dc) * sc);
         }
-        stg[o / 2] = make_float4(yr[0], yi[0], yr[1], yi[1]);
-        stg[o / 2 + 1] = make_float4(yr[2], yi[2], yr[3], yi[3]);
       }
       __syncthreads();
       int myclip = 0;
 #pragma unroll
       for (int r = 0; r < 8; r += 2) {
-        const float4 v = stg[(j0 + r) / 2];
+        const float4 v = *reinterpret_cast<const float4 *>(stg + fe8_stg(j0 + r)); // 16-B aligned: j0 + r even
         xv[r] = make_float2(v.x, v.y);
         xv[r + 1] = make_float2(v.z, v.w);
       }
@@ -2785,8 +2698,12 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
       __syncthreads();
       float vI = sh->carry_i, vQ = sh->carry_q;
       for (int w = 0; w < wave; ++w) {
-        vI = sh->wave_a[w] * vI + sh->wave_bi[w];
-        vQ = sh->wave_a[w] * vQ + sh->wave_bq[w];
+        // scalar asm: the vectoriser's packed form of this pair put LDS loads
+        // over the sources of a just-issued v_pk_* op (tests/test_isa_scan.py)
+        const float wa = sh->wave_a[w], wi = sh->wave_bi[w], wq = sh->wave_bq[w];
+        asm("v_mul_f32 %0, %2, %0\n\tv_add_f32 %0, %0, %3\n\tv_mul_f32 %1, %2, %1\n\tv_add_f32 %1, %1, %4"
+            : "+v"(vI), "+v"(vQ)
+            : "v"(wa), "v"(wi), "v"(wq));
       }
       vI = eA * vI + eI;
       vQ = eA * vQ + eQ;
@@ -2848,22 +2765,25 @@ __global__ __launch_bounds__(256, FE8_MINB) void k_fe8(FeArgs a) {
         for (int u = 0; u < 2; ++u) {
           const f16x8_t ihi = bih[32 * u + 4 * ks], ilo = bil[32 * u + 4 * ks]; // + 256 u + 32 ks samples
           const f16x8_t qhi = bqh[32 * u + 4 * ks], qlo = bql[32 * u + 4 * ks];
-          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ihi, ai[u], 0, 0, 0);
-          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, qhi, aq[u], 0, 0, 0);
-          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, ilo, ai[u], 0, 0, 0);
-          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, qlo, aq[u], 0, 0, 0);
-          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, ihi, ai[u], 0, 0, 0);
-          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, qhi, aq[u], 0, 0, 0);
+          // transposed tiles (images as A, taps as B), as the decimator's
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ihi, ahi, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qhi, ahi, aq[u], 0, 0, 0);
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ilo, ahi, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qlo, ahi, aq[u], 0, 0, 0);
+          ai[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ihi, alo, ai[u], 0, 0, 0);
+          aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qhi, alo, aq[u], 0, 0, 0);
         }
       }
       const float osc = iqscale * (1.0f / (4096.0f * kIqIn)); // exact: a power-of-two rescale
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
-        // (yb + 1 + even: 8-B aligned only, so float2 stores)
-        float2 *yo = yb + 1 + 256 * (2 * wave + u) + 16 * col + 4 * g;
+        // lane: outputs 256 (2 wave + u) + 16 (4 g + i) + col -- 16 lanes,
+        // 16 consecutive float2: conflict-free ds_write_b64 (untransposed,
+        // 4 outputs per lane 128 B apart across the lanes, it was 16-way)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) yo[i] = make_float2(ai[u][i] * osc, aq[u][i] * osc);
+        for (int i = 0; i < 4; ++i)
+          yb[1 + 256 * (2 * wave + u) + 16 * (4 * g + i) + col] = make_float2(ai[u][i] * osc, aq[u][i] * osc);
       }
       if (tid == 0) yb[0] = make_float2(sh->fd_re, sh->fd_im);
     }
@@ -3210,14 +3130,22 @@ int launch_audio(const AudioArgs &a, void *stream) {
  * 0.847 ms per pipelined step (profiles/r03h_ab_lds_history_nors.txt). */
 #define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
 #define RS_TMAX FMX_RS_TMAX // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
-#define RS_XP 68   // padded window row: 16 channel rows 68 floats apart read conflict-free
+// the tile's window, sample s of a channel at [c][RS_XS (s mod 4) + s / 4]:
+// a lane's 16 samples of one K column are one 64-B run (4 ds_read_b128
+// instead of 16 ds_read_b32 -- those were 2-way on the 32-bank rows), and the
+// loader's 4 x 4 register transpose stores 16-B runs; rows 80 floats apart,
+// columns 20: 1 extra cycle per read group, stores conflict-free
+// (tools/lds_banks.py)
+#define RS_XP 80
+#define RS_XS 20
 // <= 96 VGPRs (five waves per SIMD): a k_rs wave beside two k_fe8 waves (168
 // each) and a k_pll wave (80)
 struct RsLds {
   float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
   FmxSched ssch[RS_TMAX * 16];
-  // the tile's MPX window [buffer][channel][sample - k0]: 15.3 KB in all, so
-  // a k_rs workgroup fits beside two k_fe8 and one k_pll workgroup on a CU
+  // the tile's MPX window [buffer][channel][column-major samples - k0]:
+  // 16.5 KB in all, so a k_rs workgroup fits beside two k_fe8 (52.4 KB each)
+  // and one k_pll workgroup (31.2 KB) on a CU
   float xs[2][16][RS_XP] __attribute__((aligned(16)));
 };
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_rs(RsArgs a) {
@@ -3282,12 +3210,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   };
   auto store_w = [&](int T, int buf, const float4 (&v)[4]) __attribute__((always_inline)) {
     const int k0 = tile_k0(T);
+    float4 w[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool ok = lcv && k0 + 16 * lq + 4 * j < a.n;
-      *reinterpret_cast<float4 *>(&xs[buf][lc][16 * lq + 4 * j]) =
-          ok ? v[j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      w[j] = ok ? v[j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
+    // samples 16 lq + 4 j + e: column e, rows 4 lq + j
+    *reinterpret_cast<float4 *>(&xs[buf][lc][4 * lq]) = make_float4(w[0].x, w[1].x, w[2].x, w[3].x);
+    *reinterpret_cast<float4 *>(&xs[buf][lc][RS_XS + 4 * lq]) = make_float4(w[0].y, w[1].y, w[2].y, w[3].y);
+    *reinterpret_cast<float4 *>(&xs[buf][lc][2 * RS_XS + 4 * lq]) = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
+    *reinterpret_cast<float4 *>(&xs[buf][lc][3 * RS_XS + 4 * lq]) = make_float4(w[0].w, w[1].w, w[2].w, w[3].w);
   };
   auto tile = [&](int T, int buf) __attribute__((always_inline)) {
     const FmxSched en = ssch[16 * (T - ta) + r];
@@ -3311,12 +3244,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const float mu = en.mu, mu1 = 1.0f - mu;
     float hv[RS_KS], xv[RS_KS];
 #pragma unroll
+    for (int q = 0; q < RS_KS / 4; ++q) { // samples 4 st + kk, st = 4 q .. 4 q + 3
+      const float4 x4 = *reinterpret_cast<const float4 *>(&xs[buf][r][RS_XS * kk + 4 * q]);
+      xv[4 * q] = x4.x;
+      xv[4 * q + 1] = x4.y;
+      xv[4 * q + 2] = x4.z;
+      xv[4 * q + 3] = x4.w;
+    }
+#pragma unroll
     for (int st = 0; st < RS_KS; ++st) {
       const int m = m0 + 4 * st;
       const int mc = min(max(m, 0), FMX_RDS_RS_SUB);
       const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
       hv[st] = in ? mu1 * tab[row0][mc] + mu * tab[row1][mc] : 0.0f;
-      xv[st] = xs[buf][r][4 * st + kk];
     }
     f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -3354,7 +3294,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 }
 
 int launch_rs(const RsArgs &a, void *stream) {
-  static_assert(sizeof(RsLds) <= 16 * 1024, "k_rs LDS");
+  static_assert(sizeof(RsLds) <= 17 * 1024, "k_rs LDS");
+  static_assert(RS_XS >= RS_KS && RS_XP >= 4 * RS_XS && RS_XS % 4 == 0, "k_rs window layout");
   return fmx_launch(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), sizeof(RsLds), static_cast<hipStream_t>(stream), a);
 }
 int launch_rds(const RdsArgs &a, void *stream) {

@@ -1,0 +1,43 @@
+"""Weak-carrier parity of the f16 hi / lo MFMA FIRs.
+
+k_fe8's decimator, IQ FIR and pilot BPF and k_audio's L/R FIRs run on
+v_mfma_f32_16x16x32_f16 with every operand split into an f16 hi and lo half
+(data x 2^10, taps x 2^12).  A weak carrier makes the IQ small, and a lo half
+below 2^-14 would lose bits as an f16 subnormal.  Here the carrier sits at
+-40 and -60 dBFS (synth amplitude 10^(dB/20) of full scale), with the DSP AGC
+(fast) off and on, against the oracle on the same bytes.
+
+What the bytes allow: the IQ reaches the FIRs as u8 - 127.5 (the reference's
+ComplexDecimator / processSplit input), so any nonzero input is >= 0.5 in
+byte units, i.e. >= 4 after the x 2^10 / 127.5 image scaling, and its lo half
+is >= 2^-9: far from f16 subnormals (2^-14).  At -60 dBFS the carrier is 0.13
+LSB and the bytes quantise it to a sign pattern; the discriminator then sees a
+few-LSB IQ vector, where (as for the narrow W0 filters in
+test_gpu_parity.py) single MPX samples are sensitive to 1e-7 relative
+differences, so -60 dBFS holds MPX to MPX_MAX_TOL_NARROW and a free-running
+pilot to PILOT_UNLOCKED_TOL; PCM, flags, counts and RDS groups keep the full
+bars.  Every achieved error goes to gpurun_out/parity_errors.jsonl."""
+import pytest
+
+from test_gpu_parity import PILOT_UNLOCKED_TOL, check, run_both  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("level_db", [-40, -60])
+@pytest.mark.parametrize("agc", [0, 1])
+def test_weak_carrier(fmx, oracle, torch_cuda, level_db, agc):
+    C, nblk, M, B = 4, 16, 10, 4096
+    amp = 10.0 ** (level_db / 20.0)
+    scfg = fmx.make_synth(kind=2, amplitude=amp, n_bits=8192)
+    bits, _ = fmx.synth_rds_bits(scfg, 0, C)
+    iq = fmx.synth_host(scfg, 0, C, 0, B * M * nblk, bits)
+    # the bytes really are a weak carrier: peak deviation from 127.5 in LSB
+    dev = abs(iq.astype(float) - 127.5).max()
+    assert dev <= 127.5 * amp + 1.0, dev
+    kw = dict(dsp_agc=1, blend=0) if agc else {}
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
+    weak = level_db <= -60
+    for c in range(C):
+        check(g, outs[c], c, nblk, f"weak_carrier{level_db}dB_agc{agc}",
+              pilot_tol=PILOT_UNLOCKED_TOL if weak else 0, narrow=weak)
