@@ -11,15 +11,17 @@ What the bytes allow: the IQ reaches the FIRs as u8 - 127.5 (the reference's
 ComplexDecimator / processSplit input), so any nonzero input is >= 0.5 in
 byte units, i.e. >= 4 after the x 2^10 / 127.5 image scaling, and its lo half
 is >= 2^-9: far from f16 subnormals (2^-14).  At -60 dBFS the carrier is 0.13
-LSB and the bytes quantise it to a sign pattern; the discriminator then sees a
-few-LSB IQ vector, where (as for the narrow W0 filters in
-test_gpu_parity.py) single MPX samples are sensitive to 1e-7 relative
-differences, so -60 dBFS holds MPX to MPX_MAX_TOL_NARROW and a free-running
-pilot to PILOT_UNLOCKED_TOL; PCM, flags, counts and RDS groups keep the full
-bars.  Every achieved error goes to gpurun_out/parity_errors.jsonl."""
+LSB and the bytes quantise it to a sign pattern (the discriminator still sees
+FM: the phase survives the quantisation).  Every bar is the full one of
+tests/test_gpu_parity.py.  Achieved (round 4, 16 channels x 16 blocks over the
+four cases, profiles/r04r_parity_errors.jsonl): MPX max 1.3e-5, MPX RMS
+4.2e-7, PCM RMS 8.1e-7, PCM max 1.2e-5, pilot level exact, RDS groups
+bit-exact -- the same as at full carrier, so the f16 hi / lo FIRs need no
+exact-f32 fallback.  Every achieved error goes to
+gpurun_out/parity_errors.jsonl."""
 import pytest
 
-from test_gpu_parity import PILOT_UNLOCKED_TOL, check, run_both  # noqa: F401
+from test_gpu_parity import check, run_both
 
 pytestmark = pytest.mark.gpu
 
@@ -37,7 +39,5 @@ def test_weak_carrier(fmx, oracle, torch_cuda, level_db, agc):
     assert dev <= 127.5 * amp + 1.0, dev
     kw = dict(dsp_agc=1, blend=0) if agc else {}
     g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
-    weak = level_db <= -60
     for c in range(C):
-        check(g, outs[c], c, nblk, f"weak_carrier{level_db}dB_agc{agc}",
-              pilot_tol=PILOT_UNLOCKED_TOL if weak else 0, narrow=weak)
+        check(g, outs[c], c, nblk, f"weak_carrier{level_db}dB_agc{agc}")
