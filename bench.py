@@ -374,7 +374,11 @@ def main():
 
     # ---- roofline: the kernel with the longest live launch (HIP events on
     # its own stream over the timed region), against SURVEY 8(d)'s 2.107 B/IQ ----
-    units = C * n_iq  # IQ samples one launch of each kernel processes on this rank
+    units_step = C * n_iq  # IQ samples one step processes on this rank
+    # launches per timed step of each kernel (the front end may run as two
+    # channel halves): a launch processes units_step / that many IQ samples
+    timed = max(1, -(-args.steps // max(1, args.kernel_timing_every)))
+    lps = {k: max(1, round(v[1] / timed)) for k, v in ktimes.items() if v[1] > 0}
     avg = {k: v[0] / max(v[1], 1) * 1e-3 for k, v in ktimes.items() if v[1] > 0}
     if not avg:  # --no-kernel-timing (diagnostic): no per-kernel figures
         avg = {k: float("nan") for k in ktimes}
@@ -390,13 +394,14 @@ def main():
                 pmc = pm.get("kernels", {})
         except (OSError, ValueError):
             pmc = None
+    units = units_step // lps.get(dom, 1)  # IQ samples of one launch of the dominant kernel
     alg_bytes = ALG_BYTES_PER_IQ * units
     achieved = alg_bytes / dom_s / 1e9
     traffic = pmc_bytes(pmc, dom)
     step_traffic = None
     if all(pmc_bytes(pmc, k) is not None for k in avg):
-        step_traffic = sum(pmc_bytes(pmc, k) for k in avg)
-    path_tflops = ALG_FLOP_PER_IQ * units / (ms_per_step * 1e-3) / 1e12
+        step_traffic = sum(pmc_bytes(pmc, k) * lps.get(k, 1) for k in avg)
+    path_tflops = ALG_FLOP_PER_IQ * units_step / (ms_per_step * 1e-3) / 1e12
     roof = {"bound": "hbm", "kernel": KNAME[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": os.path.relpath(pmc_path, ROOT) if pmc else None,
@@ -405,7 +410,7 @@ def main():
             # the whole step's counted HBM bytes (all four kernels) over the
             # path's algorithmic bytes: intermediates round-tripping HBM
             "step_traffic": step_traffic,
-            "step_traffic_over_algorithmic": round(step_traffic / alg_bytes, 3) if step_traffic else None,
+            "step_traffic_over_algorithmic": round(step_traffic / (ALG_BYTES_PER_IQ * units_step), 3) if step_traffic else None,
             # the roof that binds this path (no MFMA: FIR/IIR/PLL work is FP32 VALU)
             "valu_path": {"achieved": round(path_tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(path_tflops / FP32_PEAK_TFLOPS, 4), "flop_per_iq": ALG_FLOP_PER_IQ,
@@ -416,7 +421,9 @@ def main():
             continue
         avg_s = avg[k]
         bpi, fpi = PER_IQ[k]
+        units = units_step // lps[k]
         ent = {"kernel": KNAME[k], "ms_total": round(v[0], 3), "launches": v[1], "avg_ms": round(avg_s * 1e3, 4),
+               "launches_per_step": lps[k],
                # live in the pipelined timed region (co-running kernels included)
                "design_bytes_per_launch": bpi * units,
                "design_hbm_gbs": round(bpi * units / avg_s / 1e9, 1),
