@@ -1018,6 +1018,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     KBind t(h, FMX_K_FRONTEND, h->sA, h->evA[buf]);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
+      h->t_rds.spec = false; // the next step's schedule was not copied
       return rc;
     }
     t.launched();

@@ -316,42 +316,6 @@ __device__ __forceinline__ float resamp_out_pair(const float2 (*hp)[FMX_NPFB], i
   return w0 + w1;
 }
 
-// Block-wide (256 threads) exclusive scan of affine maps v -> A v + B with
-// two B lanes (left/right sharing A), applied to the carries (cl, cr):
-// returns v_{k-1} for element k = tid.  `ws` is 3*4 floats of LDS.
-__device__ __forceinline__ void block_affine_prev(float A, float BL, float BR, float cl, float cr, float *ws,
-                                                  float &pl, float &pr) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const float pA = __shfl_up(A, d), pL = __shfl_up(BL, d), pR = __shfl_up(BR, d);
-    if (lane >= d) {
-      BL = A * pL + BL;
-      BR = A * pR + BR;
-      A = A * pA;
-    }
-  }
-  if (lane == 63) {
-    ws[wave] = A;
-    ws[4 + wave] = BL;
-    ws[8 + wave] = BR;
-  }
-  float eA = __shfl_up(A, 1), eL = __shfl_up(BL, 1), eR = __shfl_up(BR, 1);
-  if (lane == 0) {
-    eA = 1.0f;
-    eL = 0.0f;
-    eR = 0.0f;
-  }
-  __syncthreads();
-  float vl = cl, vr = cr;
-  for (int w = 0; w < wave; ++w) {
-    vl = ws[w] * vl + ws[4 + w];
-    vr = ws[w] * vr + ws[8 + w];
-  }
-  pl = eA * vl + eL;
-  pr = eA * vr + eR;
-  __syncthreads();  // ws reusable
-}
 
 __device__ __forceinline__ int sched_lower_bound(const FmxSched *s, int n, int i) {
   int lo = 0, hi = n;
@@ -1092,32 +1056,54 @@ struct AuShared {
   int eb, ee, count;
 };
 
+// DPP move of x (CTRL, rows ROWS); lanes that receive nothing get id
+template <int CTRL, int ROWS> __device__ __forceinline__ float dpp_or(float x, float id) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, id), __builtin_bit_cast(int, x), CTRL,
+                                                               ROWS, 0xF, false));
+}
+// Inclusive wave64 scan of affine maps v -> A v + (B1, B2), earlier lanes
+// applied first, by DPP (no LDS round trip: ds_bpermute per step before
+// round 4): row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast:15
+// into rows 1 and 3 and row_bcast:31 into rows 2 and 3.  Lanes that receive
+// nothing combine with the identity (1, 0, 0): exact.
+#define WAVE_AFF_STEP(CTRL, ROWS)                                                       \
+  {                                                                                   \
+    const float pA_ = dpp_or<CTRL, ROWS>(A, 1.0f), p1_ = dpp_or<CTRL, ROWS>(B1, 0.0f); \
+    const float p2_ = dpp_or<CTRL, ROWS>(B2, 0.0f);                                     \
+    B1 = A * p1_ + B1;                                                                \
+    B2 = A * p2_ + B2;                                                                \
+    A = A * pA_;                                                                      \
+  }
+__device__ __forceinline__ void wave_affine_scan(float &A, float &B1, float &B2) {
+  WAVE_AFF_STEP(0x111, 0xF)
+  WAVE_AFF_STEP(0x112, 0xF)
+  WAVE_AFF_STEP(0x114, 0xF)
+  WAVE_AFF_STEP(0x118, 0xF)
+  WAVE_AFF_STEP(0x142, 0xA)
+  WAVE_AFF_STEP(0x143, 0xC)
+}
+#undef WAVE_AFF_STEP
+// the previous lane's map (wave_shr:1; lane 0: the identity)
+__device__ __forceinline__ void wave_affine_prev(float A, float B1, float B2, float &eA, float &e1, float &e2) {
+  eA = dpp_or<0x138, 0xF>(A, 1.0f);
+  e1 = dpp_or<0x138, 0xF>(B1, 0.0f);
+  e2 = dpp_or<0x138, 0xF>(B2, 0.0f);
+}
+
 // exclusive block scan (256 threads) of per-thread affine maps v -> A v + B
 // (B for L and R), applied to the carries: the state before this thread's
 // first element.
 __device__ __forceinline__ void au_scan_prev(float A, float BL, float BR, float cl, float cr, float (*ws)[4][2],
                                              float &pl, float &pr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const float pA = __shfl_up(A, d), pL = __shfl_up(BL, d), pR = __shfl_up(BR, d);
-    if (lane >= d) {
-      BL = A * pL + BL;
-      BR = A * pR + BR;
-      A = A * pA;
-    }
-  }
+  wave_affine_scan(A, BL, BR);
   if (lane == 63) {
     ws[0][wave][0] = A;
     ws[1][wave][0] = BL;
     ws[2][wave][0] = BR;
   }
-  float eA = __shfl_up(A, 1), eL = __shfl_up(BL, 1), eR = __shfl_up(BR, 1);
-  if (lane == 0) {
-    eA = 1.0f;
-    eL = 0.0f;
-    eR = 0.0f;
-  }
+  float eA, eL, eR;
+  wave_affine_prev(A, BL, BR, eA, eL, eR);
   __syncthreads();
   float vl = cl, vr = cr;
   for (int w = 0; w < wave; ++w) {
@@ -2675,26 +2661,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
         BQ = xv[r].y + dc_c * BQ;
         A = dc_c * A;
       }
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const float pA = __shfl_up(A, d), pI = __shfl_up(BI, d), pQ = __shfl_up(BQ, d);
-        if (lane >= d) {
-          BI = A * pI + BI;
-          BQ = A * pQ + BQ;
-          A = A * pA;
-        }
-      }
+      wave_affine_scan(A, BI, BQ);
       if (lane == 63) {
         sh->wave_a[wave] = A;
         sh->wave_bi[wave] = BI;
         sh->wave_bq[wave] = BQ;
       }
-      float eA = __shfl_up(A, 1), eI = __shfl_up(BI, 1), eQ = __shfl_up(BQ, 1);
-      if (lane == 0) {
-        eA = 1.0f;
-        eI = 0.0f;
-        eQ = 0.0f;
-      }
+      float eA, eI, eQ;
+      wave_affine_prev(A, BI, BQ, eA, eI, eQ);
       __syncthreads();
       float vI = sh->carry_i, vQ = sh->carry_q;
       for (int w = 0; w < wave; ++w) {
