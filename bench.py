@@ -53,13 +53,14 @@ ALG_FLOP_PER_IQ = 290.0
 # The 240k -> 171k RDS resampler (k_rs: MPX in, RDS-rate samples out) runs on
 # the RDS stream ahead of k_rds, which reads the RDS-rate samples.
 PER_IQ = {
-    "frontend": (2.0 + 0.4 + 0.4, 112.0 + 32.4 + 61.0),
+    "frontend": (2.0 + 0.4, 112.0 + 32.4),
     "stereo": (0.4 + 0.8 + 0.8, 20.0),
     "audio": (0.8 + 0.107, 48.0 + 3.0),
     "rds": (4.0 * 0.7125 / 10.0, 15.0),
     "rs": (0.4 + 4.0 * 0.7125 / 10.0, 7.4),
+    "pilot": (0.4 + 0.4, 61.0),
 }
-KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs"}
+KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs", "pilot": "k_pilot"}
 
 
 def pmc_bytes(pmc, k):

@@ -91,6 +91,7 @@ struct Handle {
   // audio of step k overlaps the PLL of step k+1 (raw L/R double-buffered).
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
+  hipEvent_t evP[FMX_NBUF] = {}; // k_pilot (sA, after k_fe8): k_pll's input
   hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr, evTmpU = nullptr;
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   uint64_t step = 0;
@@ -639,7 +640,7 @@ static void destroy(Handle *h) {
   }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
-    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b]})
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evP[b]})
       if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
@@ -719,6 +720,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   for (int b = 0; b < FMX_NBUF; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evB[b], ev_flags(true)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evP[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(true)));
   }
@@ -983,7 +985,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nrslot, static_cast<size_t>(h->C) * 256) : 0u;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
-  bool use_rs = false;
+  bool use_rs = false, pil_k = false;
   // ---- front end (sA) ----
   {
     FeArgs a = fe_args(h, n, h->M > 1 ? FE_IN_U8_DECIM : FE_IN_U8_DIRECT, buf);
@@ -1005,8 +1007,15 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     // (16 outputs' windows span <= 15 del + 31 samples: inside k_rs's 64 for del <= 2.1)
     // k_rs takes one resampler schedule for all channels: the RDS timing set
     // is never reset per channel (SubcarrierSet::reset, subcarrier.cpp:108)
-    use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 &&
-             frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
+    const bool fe8 = frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
+    use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 && fe8;
+    // the pilot BPF of a k_fe8 step runs as k_pilot (after it, on sA): k_fe8
+    // writes the MPX and the stereo history rows k_pilot starts from
+    pil_k = FMX_PILOT_K && stereo && fe8;
+    if (pil_k) {
+      a.pilot_out = nullptr;
+      a.st_hist_out = 1;
+    }
     if (use_rs) a.rds_win_out = h->rds_win[buf];
     a.clip_out = o->d_clip_ratio ? o->d_clip_ratio : h->clip;
     a.sig_sums = o->d_signal ? h->sig_sums[buf] : nullptr;
@@ -1027,6 +1036,27 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later: its read ends with the front end
     h->t_rds.ev_use[h->t_rds.spec_img] = h->evA[buf];
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
+  }
+  // ---- pilot BPF (sA, after the front end; read by k_pll) ----
+  if (pil_k) {
+    PilotArgs p{};
+    p.des = h->ddes;
+    p.des_pilot_len = h->hdes->pilot_len;
+    p.C = h->C;
+    p.n = n;
+    p.mpx = mpx;
+    p.mpx_stride = mpx_stride;
+    p.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
+    p.out = h->pilot[buf];
+    p.out_stride = h->cfg.block;
+    KBind t(h, FMX_K_PILOT, h->sA, h->evP[buf]);
+    if (!FMX_SKIP(pll)) {
+      if ((rc = launch_pilot(p, h->sA)) != FMX_OK) {
+        h->err = "pilot launch failed";
+        return rc;
+      }
+      t.launched();
+    }
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
   HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
@@ -1074,7 +1104,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   h->evC_set[buf] = true;
   // ---- stereo PLL (sB) ----
-  HIP_TRY(hipStreamWaitEvent(h->sB, h->evA[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : h->evA[buf], 0));
   if (stereo) {
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;

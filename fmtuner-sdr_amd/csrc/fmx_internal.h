@@ -35,6 +35,12 @@ bool timing_equal(const ResampTiming &a, const ResampTiming &b);
 // ---- kernel argument blocks (fmx_kernels.hip) ----
 enum FeInMode { FE_IN_U8_DECIM = 0, FE_IN_CF = 1, FE_IN_U8_DIRECT = 2, FE_IN_MPX = 3 };
 
+// process_block: the 19 kHz pilot BPF of a k_fe8 step as its own kernel
+// (k_pilot, after k_fe8 on the front-end stream) instead of inside k_fe8,
+// which then writes only the MPX and its history rows (FeArgs::st_hist_out)
+#ifndef FMX_PILOT_K
+#define FMX_PILOT_K 1
+#endif
 struct FeArgs {
   const FmxDesign *des;
   int des_fs;        // DSP rate (host copy of des->fs, for the launcher)
@@ -52,6 +58,7 @@ struct FeArgs {
   int mpx_stride;
   float *pilot_out;  // null = no pilot BPF
   int pilot_stride;
+  int st_hist_out;   // write the stereo history rows (st_hist_wr) even without the pilot BPF
   float *rds_out;    // null = no RDS resampling
   int rds_stride;
   int *rds_count;    // [C]
@@ -155,6 +162,18 @@ struct RdsArgs {
 
 // k_rs: the 240k -> 171k RDS resampler of a process_block step (liquid
 // resamp_rrrf, host timing schedule), 16 channels per workgroup on FP32 MFMA
+struct PilotArgs {
+  const FmxDesign *des;
+  int des_pilot_len;        // host copy of des->pilot_len (launcher check)
+  int C, n;
+  const float *mpx;         // this step's MPX rows (the front end's output)
+  int mpx_stride;
+  const float *st_hist_rd;  // [C][FMX_HIST] the previous call's last MPX samples
+  float *out;               // pilot rows (k_pll's input)
+  int out_stride;
+  int vec;                  // set by the launcher: 16-B rows
+};
+
 struct RsArgs {
   const FmxDesign *des;
   int C, n;
@@ -182,6 +201,7 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec = 
 // whether launch_frontend_m would run k_fe8 for these arguments
 bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec);
 int launch_pll(const PllArgs &a, void *stream);
+int launch_pilot(const PilotArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);
 #ifndef FMX_RS_TMAX

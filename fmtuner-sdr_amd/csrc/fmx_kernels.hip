@@ -519,6 +519,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
   const float iqscale = D->iq_scale[par.iqsel];
   const bool demod = a.do_demod != 0;
   const bool pilot = a.pilot_out != nullptr;
+  const bool hist_out = pilot || a.st_hist_out != 0; // the stereo history rows
   const bool rds = a.rds_out != nullptr;
   const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
   const float dc_c = -dc_a1;
@@ -540,9 +541,9 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       sh->fd_im = a.fd_prev[2 * c + 1];
     }
   }
-  if (pilot || rds || demod) {
+  if (hist_out || rds || demod) {
     const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
-    for (int h = tid; h < FMX_HIST; h += 256) mx[h] = pilot ? hist[h] : 0.0f;
+    for (int h = tid; h < FMX_HIST; h += 256) mx[h] = hist_out ? hist[h] : 0.0f;
   }
   if (tid == 0) sh->clip = 0;
   float agc_g = 1.0f, agc_y2p = 1.0f;
@@ -935,7 +936,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
       }
     }
   }
-  if (pilot) {
+  if (hist_out) {
     float *hist = a.st_hist_wr + (size_t)c * FMX_HIST;
     for (int h = tid; h < FMX_HIST; h += 256) hist[h] = mx[h];
   }
@@ -2452,6 +2453,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
   const int iqL = D->iq_len[par.iqsel];
   const float iqscale = D->iq_scale[par.iqsel];
   const bool pilot = a.pilot_out != nullptr;
+  const bool hist_out = pilot || a.st_hist_out != 0; // the stereo history rows
   const bool rds = a.rds_out != nullptr;
   // rs: the resampler runs here (else k_rs does it, from the MPX and the
   // previous call's window this kernel hands over in rds_win_out)
@@ -2791,9 +2793,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
         const float m = fmx_atan2f(im, re) * ref; // select-free (fmx_math.h)
         mv[k] = m;
         // f16 hi / lo split for the MFMA pilot BPF (m = hi + lo to 22 bits)
-        const _Float16 hv = (_Float16)m;
-        xh[FMX_HIST + j] = hv;
-        xl[FMX_HIST + j] = (_Float16)(m - (float)hv);
+        if (pilot) {
+          const _Float16 hv = (_Float16)m;
+          xh[FMX_HIST + j] = hv;
+          xl[FMX_HIST + j] = (_Float16)(m - (float)hv);
+        }
         if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
       if (tid == 0) {
@@ -2814,7 +2818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     }
     if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
     const bool last_chunk = n0 + FE8_T >= n;
-    if (rds || pilot) { // unpadded f32 copy: the RDS resampler's input (its own window history first), the history rows
+    if (rds || hist_out) { // unpadded f32 copy: the RDS resampler's input (its own window history first), the history rows
 #pragma unroll
       for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
     }
@@ -2875,7 +2879,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     // 32 the next chunk's window history (every read of tl32 for this chunk
     // was before the "uc complete" barrier)
     if (last_chunk) {
-      if (pilot) {
+      if (hist_out) {
         static_assert(FMX_HIST == 512, "two history words per thread");
         const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.st_hist_wr + (size_t)c * FMX_HIST, FMX_HIST * 4);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + FE8_T - FMX_HIST + tid]), rh,
@@ -3084,6 +3088,132 @@ int launch_pll(const PllArgs &a, void *stream) {
 }
 int launch_audio(const AudioArgs &a, void *stream) {
   return fmx_launch(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
+}
+/* ================================================================== */
+/* k_pilot: the 19 kHz pilot band-pass (stereo_decoder.cpp:229-230)    */
+/* ================================================================== */
+/* k_fe8's pilot stage as its own kernel on the front-end stream, after
+ * k_fe8 (which then writes only the MPX and the stereo history rows).  In
+ * k_fe8 the stage waited on one tap-fragment load per K step with two
+ * workgroups (8 waves) per CU to hide it; here a workgroup is 6.3 KB of LDS
+ * and 4 small waves, so many are resident and the loads overlap.  The sums
+ * are k_fe8's: the same f16 hi / lo images of the same samples, the same
+ * 8-aligned windows, the same three MFMAs per K step in the same order
+ * (a tile of 256 outputs starts on a 256-sample boundary in both).
+ * Workgroup = 4096 outputs of one channel (4 waves x 4 tiles of 16 x 16:
+ * the fragments, 22 KB per K sweep from L2, are loaded once per 4 tiles); the
+ * block -> (channel, segment) map keeps a channel's segments on one XCD, so
+ * the window halo a neighbour loaded is an L2 hit. */
+#define PIL_TPW 4                  // 256-output tiles per wave: one tap-fragment load feeds PIL_TPW MFMA chains
+#define PIL_SEG (4 * 256 * PIL_TPW) // outputs per workgroup
+struct PilLds {
+  // sample s0 - FMX_HIST + i at [i]: the history (previous call's MPX rows
+  // for s < 0), the segment, 32 zero-slack samples (read by K steps past the
+  // filter, against zero taps)
+  _Float16 xh[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
+  _Float16 xl[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
+};
+__global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
+  __shared__ PilLds L;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+  typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  const FmxDesign *__restrict__ D = a.des;
+  const int nseg = (a.n + PIL_SEG - 1) / PIL_SEG;
+  const int units = a.C * nseg;
+  const int per = (units + 7) / 8; // units per XCD (workgroups go round-robin over the 8 XCDs)
+  const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (u >= units) return;
+  const int c = u / nseg, s0 = (u % nseg) * PIL_SEG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int P8 = fir8_len(D->pilot_len);
+  const int KSP = D->pilot_ks;
+  const float *mrow = a.mpx + (size_t)c * a.mpx_stride;
+  const float *hrow = a.st_hist_rd + (size_t)c * FMX_HIST + FMX_HIST; // hrow[s], s < 0
+  // the images from the window's first sample (8-aligned: P8 = 8k + 1), 4
+  // samples per thread and pass
+  const int i0 = FMX_HIST - (P8 - 1);
+  // (every pass's loads issued before the first conversion)
+  constexpr int NPASS = (FMX_HIST + PIL_SEG + 32 + 1023) / 1024;
+  float4 v[NPASS];
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    const int i = i0 + 4 * tid + 1024 * q, s = s0 - FMX_HIST + i;
+    if (i >= FMX_HIST + PIL_SEG + 32) continue;
+    if (a.vec && s >= 0 && s + 4 <= a.n) {
+      v[q] = *reinterpret_cast<const float4 *>(mrow + s);
+    } else {
+      float w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = (s + k < 0) ? hrow[s + k] : (s + k < a.n ? mrow[s + k] : 0.0f);
+      v[q] = make_float4(w[0], w[1], w[2], w[3]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    const int i = i0 + 4 * tid + 1024 * q;
+    if (i >= FMX_HIST + PIL_SEG + 32) continue;
+    const float w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+    f16x4_t hv, lv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hv[k] = (_Float16)w[k];
+      lv[k] = (_Float16)(w[k] - (float)hv[k]);
+    }
+    *reinterpret_cast<f16x4_t *>(&L.xh[i]) = hv;
+    *reinterpret_cast<f16x4_t *>(&L.xl[i]) = lv;
+  }
+  __syncthreads();
+  // tiles PIL_TPW w + u: 16 outputs (rows, A = taps, FmxDesign::pilot_frag)
+  // of 16 blocks of 16 outputs (columns, B = MPX), K = P8 + 15 inputs
+  const int col = lane & 15, g = lane >> 4;
+  const int xb = FMX_HIST + 256 * PIL_TPW * wave + 16 * col - (P8 - 1) + 8 * g;
+  const f16x8_t *bh = reinterpret_cast<const f16x8_t *>(&L.xh[xb]);
+  const f16x8_t *bl = reinterpret_cast<const f16x8_t *>(&L.xl[xb]);
+  const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->pilot_frag[0][0][0][0]) + lane;
+  f32x4_t acc[PIL_TPW];
+#pragma unroll
+  for (int u = 0; u < PIL_TPW; ++u) acc[u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+  u32x4 ah = fa[0], al = fa[64];
+  for (int ks = 0; ks < KSP; ++ks) {
+    const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
+    if (ks + 1 < KSP) {
+      ah = fa[128 * (ks + 1)];
+      al = fa[128 * (ks + 1) + 64];
+    }
+#pragma unroll
+    for (int u = 0; u < PIL_TPW; ++u) {
+      const f16x8_t xhi = bh[32 * u + 4 * ks], xlo = bl[32 * u + 4 * ks]; // + 256 u + 32 ks samples
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, xhi, acc[u], 0, 0, 0);
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, xlo, acc[u], 0, 0, 0);
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, xhi, acc[u], 0, 0, 0);
+    }
+  }
+  // lane: outputs 16 col + 4 g + i of a tile's 256 (1 KB per store, contiguous)
+  constexpr float kInv = 1.0f / 4096.0f;
+#pragma unroll
+  for (int u = 0; u < PIL_TPW; ++u) {
+    const int o = s0 + 256 * (PIL_TPW * wave + u) + 16 * col + 4 * g;
+    float *po = a.out + (size_t)c * a.out_stride + o;
+    if (a.vec && o + 4 <= a.n) {
+      *reinterpret_cast<float4 *>(po) =
+          make_float4(acc[u][0] * kInv, acc[u][1] * kInv, acc[u][2] * kInv, acc[u][3] * kInv);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (o + k < a.n) po[k] = acc[u][k] * kInv;
+    }
+  }
+}
+int launch_pilot(const PilotArgs &a0, void *stream) {
+  PilotArgs a = a0;
+  if (a.C <= 0 || a.n <= 0) return FMX_OK;
+  if (((a.des_pilot_len + 6) & ~7) > FMX_HIST) return FMX_E_INVALID; // the images' history holds the reach (fir8_len - 1)
+  a.vec = ((((uintptr_t)a.mpx) | ((uintptr_t)a.mpx_stride * 4) | ((uintptr_t)a.out) | ((uintptr_t)a.out_stride * 4)) &
+           15) == 0;
+  const long units = (long)a.C * ((a.n + PIL_SEG - 1) / PIL_SEG);
+  return fmx_launch(k_pilot, dim3((unsigned)(8 * ((units + 7) / 8))), dim3(256), 0, static_cast<hipStream_t>(stream), a);
 }
 /* ================================================================== */
 /* k_rs: the RDS resampler 240k -> 171k (subcarrier.cpp:117-147) on MFMA */

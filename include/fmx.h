@@ -38,11 +38,11 @@
 extern "C" {
 #endif
 
-/* ABI history: 5 (round 4) adds FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+/* ABI history: 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
  * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
  * which changed that struct's size: callers must be rebuilt against this
  * header. */
-#define FMX_ABI_VERSION 5
+#define FMX_ABI_VERSION 6
 
 enum {
   FMX_OK = 0,
@@ -208,14 +208,16 @@ int fmx_memset(void *handle, void *d_ptr, int value, size_t bytes);
  * stream it runs on; fmx_kernel_times returns the summed milliseconds and
  * launch counts per kernel id since the last reset. */
 enum {
-  FMX_K_FRONTEND = 0, /* decimate + DC + IQ FIR + AGC + discriminator + pilot BPF (+ RDS resample
-                         when process_block does not run it as its own kernel, k_rs)            */
+  FMX_K_FRONTEND = 0, /* decimate + DC + IQ FIR + AGC + discriminator (+ pilot BPF, + RDS
+                         resample when process_block does not run them as kernels of their own) */
   FMX_K_STEREO = 1,   /* pilot PLL + blend + L-R matrix (one lane per channel)                 */
   FMX_K_AUDIO = 2,    /* L/R 15 kHz FIRs + 32 kHz resampler + de-emphasis + DC + clamp         */
   FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync + biphase + block sync                     */
   FMX_K_RS = 4,       /* the 240k -> 171k RDS resampler when process_block runs it as its own
                          kernel (k_rs, on the RDS stream ahead of k_rds)                        */
-  FMX_K_COUNT = 5
+  FMX_K_PILOT = 5,    /* the 19 kHz pilot BPF when process_block runs it as its own kernel
+                         (k_pilot, on the front-end stream after k_fe8)                         */
+  FMX_K_COUNT = 6
 };
 /* enable: 0 off, 1 every step's launches, N > 1 the launches of every N-th
  * step only (a sample: fewer event packets on the streams in the timed region) */

@@ -74,6 +74,19 @@ def test_pll_register_and_lds_budget(tmp_path):
         assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
 
 
+def test_pilot_kernel_budget(tmp_path):
+    """k_pilot (the pilot BPF after k_fe8, round 4): 18.1 KB of f16 images, so
+    it fits a CU beside two k_fe8 (53.7 KB each) and a k_pll (31.2 KB), and
+    four accumulator chains without spills."""
+    ks = _kernels(tmp_path)
+    hits = _find(ks, r"7k_pilotENS_9PilotArgs")
+    assert len(hits) == 1
+    for name, f in hits.items():
+        assert f.get("group_segment_fixed_size", 0) <= 160 * 1024 - 2 * 54272 - 32 * 1024, (name, f)
+        assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 64, (name, f)
+        assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
+
+
 def test_rds_fits_beside_two_front_ends(tmp_path):
     ks = _kernels(tmp_path)
     for name, f in _find(ks, r"5k_rdsE").items():
