@@ -2329,7 +2329,9 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   // zero slack, natural order), the chunk's last FMX_HIST samples in f32
   // (stereo history write-back) and the previous chunk's last 32 in f32
   // (the RDS resampler's window)
-  static constexpr int XW = FMX_HIST + FE8_T + 32;
+  // (RS = false, process_block's variant, runs no pilot BPF -- k_pilot does
+  // -- and has no images: 10.4 KB less)
+  static constexpr int XW = RS ? FMX_HIST + FE8_T + 32 : 0;
   static constexpr int MX = HX + FE_HALO_IQ * 8;                     // XH: f16 hi [XW]
   static constexpr int XLO = MX + XW * 2;                            // XL: f16 lo [XW]
   // (round 3: no f32 copy of the chunk's last FMX_HIST samples -- the call's
@@ -2452,7 +2454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
   using PAll = std::integral_constant<int, LY::NPC>;
   const int iqL = D->iq_len[par.iqsel];
   const float iqscale = D->iq_scale[par.iqsel];
-  const bool pilot = a.pilot_out != nullptr;
+  const bool pilot = RS && a.pilot_out != nullptr; // (the launcher never passes a pilot row to RS = false)
   const bool hist_out = pilot || a.st_hist_out != 0; // the stereo history rows
   const bool rds = a.rds_out != nullptr;
   // rs: the resampler runs here (else k_rs does it, from the MPX and the
@@ -2466,7 +2468,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     reinterpret_cast<uint32_t *>(xh)[h] = 0u;
     reinterpret_cast<uint32_t *>(xl)[h] = 0u;
   }
-  __syncthreads();
+  if (RS) __syncthreads();
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
     const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
     hx[h] = make_float2(v.x, v.y);
@@ -2478,7 +2480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     sh->fd_im = a.fd_prev[2 * c + 1];
     sh->clip = 0;
   }
-  {
+  if (RS) {
     const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
     for (int h = tid; h < FMX_HIST; h += 256) {
       const float v = pilot ? hist[h] : 0.0f;
@@ -2939,7 +2941,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     }
     FE_STAMP(4)
     // ================= carry halos to the next chunk =================
-    {
+    // (RS = false has no images; nothing after the "uc is dead" barrier reads
+    // LDS there, so the next chunk needs no barrier here)
+    if (RS) {
       // the chunk's last FMX_HIST samples become the f16 images' history
       static_assert(FMX_HIST == 2 * 256, "one f16 pair per thread");
       const uint32_t ch = reinterpret_cast<const uint32_t *>(xh)[FE8_T / 2 + tid];
@@ -3027,8 +3031,10 @@ template <int M, int TPP, bool RS> static int fe8_launch_rs(const FeArgs &a, hip
   return fmx_launch(k_fe8<M, TPP, RS>, dim3(a.C), dim3(256), smem, st, a);
 }
 // the resampler in the kernel, or (rds_win_out set) left to k_rs
+// (process_block's variant, RS = false, has no pilot BPF: k_pilot runs it)
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
-  return (a.rds_out && a.rds_win_out) ? fe8_launch_rs<M, TPP, false>(a, st) : fe8_launch_rs<M, TPP, true>(a, st);
+  if (a.rds_out && a.rds_win_out) return a.pilot_out ? FMX_E_INVALID : fe8_launch_rs<M, TPP, false>(a, st);
+  return fe8_launch_rs<M, TPP, true>(a, st);
 }
 
 /* ================================================================== */
