@@ -33,6 +33,7 @@ import glob
 import json
 import math
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -141,8 +142,14 @@ def plan_channels(args, world, rank):
     return rank * c, c, c * world, "weak"
 
 
+def tag_key(path):
+    """Order of the profile tags r<round><letters>: r04z < r04aa < r04al."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
 def newest_pmc():
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")), key=tag_key)
     return files[-1] if files else None
 
 

@@ -30,7 +30,7 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("k_fe8", "k_frontend", "k_pll", "k_audio", "k_rds", "k_rs", "k_reset", "k_synth"):
+    for k in ("k_fe8", "k_frontend", "k_pll", "k_pilot", "k_audio", "k_rds", "k_rs", "k_reset", "k_synth"):
         if k in name:
             return k
     return None
