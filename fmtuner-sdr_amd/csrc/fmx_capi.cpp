@@ -1011,7 +1011,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 && fe8;
     // the pilot BPF of a k_fe8 step runs as k_pilot (after it, on sA): k_fe8
     // writes the MPX and the stereo history rows k_pilot starts from
-    pil_k = FMX_PILOT_K && stereo && fe8;
+    pil_k = stereo && fe8;
     if (pil_k) {
       a.pilot_out = nullptr;
       a.st_hist_out = 1;

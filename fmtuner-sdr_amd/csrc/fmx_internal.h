@@ -35,12 +35,9 @@ bool timing_equal(const ResampTiming &a, const ResampTiming &b);
 // ---- kernel argument blocks (fmx_kernels.hip) ----
 enum FeInMode { FE_IN_U8_DECIM = 0, FE_IN_CF = 1, FE_IN_U8_DIRECT = 2, FE_IN_MPX = 3 };
 
-// process_block: the 19 kHz pilot BPF of a k_fe8 step as its own kernel
-// (k_pilot, after k_fe8 on the front-end stream) instead of inside k_fe8,
-// which then writes only the MPX and its history rows (FeArgs::st_hist_out)
-#ifndef FMX_PILOT_K
-#define FMX_PILOT_K 1
-#endif
+// process_block runs the 19 kHz pilot BPF of a k_fe8 step as its own kernel
+// (k_pilot, after k_fe8 on the front-end stream); k_fe8 then writes only the
+// MPX and its history rows (FeArgs::st_hist_out)
 struct FeArgs {
   const FmxDesign *des;
   int des_fs;        // DSP rate (host copy of des->fs, for the launcher)
@@ -160,8 +157,7 @@ struct RdsArgs {
   unsigned long long *dbg; // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
 };
 
-// k_rs: the 240k -> 171k RDS resampler of a process_block step (liquid
-// resamp_rrrf, host timing schedule), 16 channels per workgroup on FP32 MFMA
+// k_pilot: the 19 kHz pilot BPF of a process_block step (after k_fe8)
 struct PilotArgs {
   const FmxDesign *des;
   int des_pilot_len;        // host copy of des->pilot_len (launcher check)
@@ -174,6 +170,8 @@ struct PilotArgs {
   int vec;                  // set by the launcher: 16-B rows
 };
 
+// k_rs: the 240k -> 171k RDS resampler of a process_block step (liquid
+// resamp_rrrf, host timing schedule), 16 channels per workgroup on FP32 MFMA
 struct RsArgs {
   const FmxDesign *des;
   int C, n;
