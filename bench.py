@@ -337,6 +337,7 @@ def main():
         dist.barrier()
     h.sync()
     torch.cuda.synchronize()
+    h.host_stats()  # reset the counters: the timed region's waits only
     t0 = time.perf_counter()
     host_call = []  # host time per process_block call (submission only): stalls show here
     for b in range(args.warmup, nblk):
@@ -350,6 +351,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     ktimes = h.kernel_times()
+    hstats = h.host_stats()
     ngroups = int(gcnt.sum().item())
     stereo_frac = float(st.float().mean().item())
     chans_all = float(C)
@@ -479,6 +481,9 @@ def main():
         "scan": scan,
         "host_submit_ms": {"mean": round(1e3 * sum(host_call) / len(host_call), 4),
                            "max": round(1e3 * max(host_call), 4)},
+        # waits of process_block on the pinned schedule images' last readers
+        # (the host's only throttle): how many blocked, and for how long
+        "host_image_waits": hstats,
         "check": {"rds_groups_last_step": ngroups, "rds_groups_warmup": groups_warm,
                   "stereo_fraction": stereo_frac},
         # the library this run loaded (fmx.LIB_PATH; FMX_LIB selects A/B builds)

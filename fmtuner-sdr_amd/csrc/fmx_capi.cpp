@@ -43,6 +43,13 @@ namespace fmx {
 // schedules one step early on sB: the front end then waited, through the
 // upload's event, for the previous step's k_pll -- 35-50 us per step.)
 #define FMX_HSLOTS 8 // pinned schedule images per timing set
+// front-end completion events, a ring deeper than the image ring: a pinned
+// image the front end of step s read (the speculated RDS schedule) is reused
+// at the earliest FMX_HSLOTS / 2 steps later (at most two simulations per
+// step), while evF[s % FMX_FRING] still marks that launch (round 4 bound the
+// image to evA[s % FMX_NBUF], which the front end of step s + 3 re-binds: the
+// host then waited for a later front end than the image's reader)
+#define FMX_FRING (2 * FMX_HSLOTS)
 // device schedule slots per timing set: one more than the intermediates'
 // slots, so that the RDS slot the front end of step k fills for step k+1 was
 // last read at step k-3 -- covered by the front end's one wait (evD(k-3))
@@ -64,7 +71,7 @@ struct TimingSet {
   const void *h_dev[FMX_HSLOTS] = {}; // the images' device-side addresses (mapped pinned memory)
   int hnext = 0, hcur = 0; // next image to fill, image of the last simulation
   hipEvent_t ev_h[FMX_HSLOTS] = {}; // recorded after a copy kernel's read of h_slot[i]
-  hipEvent_t ev_use[FMX_HSLOTS] = {}; // the event marking the last read of h_slot[i]: ev_h[i], or the front end's evA
+  hipEvent_t ev_use[FMX_HSLOTS] = {}; // the event marking the last read of h_slot[i]: ev_h[i], or the front end's evF
   bool ev_h_set[FMX_HSLOTS] = {};
   FmxSched *d_sched[FMX_SSLOTS] = {};
   int *d_count[FMX_SSLOTS] = {};
@@ -92,6 +99,11 @@ struct Handle {
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
   hipEvent_t evP[FMX_NBUF] = {}; // k_pilot (sA, after k_fe8): k_pll's input
+  hipEvent_t evF[FMX_FRING] = {}; // process_block's front end of step k: evF[k % FMX_FRING]
+  // host waits on pinned-image reuse (fmx_host_stats): waits, waits that
+  // found the event pending (the host blocked), milliseconds blocked
+  long host_waits = 0, host_stalls = 0;
+  double host_stall_ms = 0.0;
   hipEvent_t evTmpB = nullptr, evTmpC = nullptr, evTmpD = nullptr, evTmpU = nullptr;
   bool evB_set[FMX_NBUF] = {}, evC_set[FMX_NBUF] = {}, evD_set[FMX_NBUF] = {};
   uint64_t step = 0;
@@ -228,7 +240,7 @@ static void timing_release(Handle *h, hipEvent_t e) {
   h->pending.erase(h->pending.begin(), h->pending.begin() + static_cast<std::ptrdiff_t>(last));
 }
 
-// process_block's launches: the stream's completion event `done` (evA / evC /
+// process_block's launches: the stream's completion event `done` (evF / evC /
 // evB / evD, or none) is bound to the kernel itself through hipExtLaunchKernel
 // (set_launch_events), and with timing on a pool event takes its start (and
 // its end when there is no `done`): no marker packets between the kernels of
@@ -387,6 +399,21 @@ static void tset_compact(TimingSet &t) {
   t.groups = ng;
 }
 
+// Wait until the last reader of pinned image i is done (counted: a wait that
+// finds the event pending blocks the host).
+static hipError_t image_wait(Handle *h, TimingSet &t, int i) {
+  if (!t.ev_h_set[i]) return hipSuccess;
+  h->host_waits++;
+  hipError_t q = hipEventQuery(t.ev_use[i]);
+  if (q == hipSuccess) return hipSuccess;
+  if (q != hipErrorNotReady) return q;
+  h->host_stalls++;
+  const auto t0 = std::chrono::steady_clock::now();
+  q = hipEventSynchronize(t.ev_use[i]);
+  h->host_stall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return q;
+}
+
 // Simulate n inputs for every group into the pinned image of slot `buf`
 // (the caller uploads it); returns the largest output count in *max_count.
 static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count) {
@@ -404,7 +431,7 @@ static int tset_simulate(Handle *h, TimingSet &t, int n, int buf, int *max_count
   const int hb = t.hnext;
   t.hnext = (hb + 1) % FMX_HSLOTS;
   t.hcur = hb;
-  if (t.ev_h_set[hb]) HIP_TRY(hipEventSynchronize(t.ev_use[hb]));
+  HIP_TRY(image_wait(h, t, hb));
   FmxSched *hs = tset_hsched(h, t, hb);
   int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
   int mx = 0;
@@ -475,7 +502,7 @@ static unsigned tset_speculate(Handle *h, TimingSet &t, int n, int slot, size_t 
   const size_t n16 = (bytes + 15) / 16;
   if (G > t.cap_groups || n16 > threads) return 0;
   const int hb = t.hnext;
-  if (t.ev_h_set[hb] && hipEventSynchronize(t.ev_use[hb]) != hipSuccess) return 0;
+  if (image_wait(h, t, hb) != hipSuccess) return 0;
   t.spec_groups = t.groups;
   FmxSched *hs = tset_hsched(h, t, hb);
   int *hc = reinterpret_cast<int *>(t.h_slot[hb]) + h->C;
@@ -642,6 +669,8 @@ static void destroy(Handle *h) {
   for (int b = 0; b < FMX_NBUF; ++b)
     for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evP[b]})
       if (e) hipEventDestroy(e);
+  for (hipEvent_t e : h->evF)
+    if (e) hipEventDestroy(e);
   if (h->evTmpB) hipEventDestroy(h->evTmpB);
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
   if (h->evTmpD) hipEventDestroy(h->evTmpD);
@@ -724,6 +753,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(true)));
   }
+  for (hipEvent_t &e : h->evF) HIP_TRY(hipEventCreateWithFlags(&e, ev_flags(true)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpB, ev_flags(false)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpC, ev_flags(false)));
   HIP_TRY(hipEventCreateWithFlags(&h->evTmpD, ev_flags(false)));
@@ -938,13 +968,13 @@ static void step_done(Handle *h, bool stereo_hist_written) {
 // One reference block for every channel (main.cpp:1239-1308), on four
 // streams: sA front end, sC RDS, sB stereo PLL, sD audio.  Per step k (slot
 // buf = k mod FMX_NBUF of the intermediates):
-//   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evA(k)
-//   sC: [wait evA(k)] k_rs, k_rds -> evC(k)
-//   sB: [wait evA(k)] k_pll -> evB(k)
+//   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evF(k), k_pilot -> evP(k)
+//   sC: [wait evF(k)] k_rs, k_rds -> evC(k)
+//   sB: [wait evP(k)] k_pll -> evB(k)
 //   sD: [wait evB(k), evC(k)] [audio schedule copy] k_audio -> evD(k)
 // evD(k) therefore marks every reader of slot buf done (k_audio waits for
 // k_rds as well as k_pll), so the front end of step k+3 -- the next writer of
-// the slot, and through evA of the raw L/R slot k_pll writes -- needs ONE
+// the slot, and through evP of the raw L/R slot k_pll writes -- needs ONE
 // cross-stream wait.  The resampler schedules go on the stream of their only
 // reader, right before it.  Front end k+1 runs while k_pll / k_rs / k_rds /
 // k_audio of step k (and k-1) still run.  (Measured and rejected in round 4:
@@ -985,6 +1015,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nrslot, static_cast<size_t>(h->C) * 256) : 0u;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
   const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
+  hipEvent_t evFE = h->evF[h->step % FMX_FRING];
   bool use_rs = false, pil_k = false;
   // ---- front end (sA) ----
   {
@@ -1024,7 +1055,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.next_sched_dst = h->t_rds.d_slot[nrslot];
       a.next_sched_n16 = spec16;
     }
-    KBind t(h, FMX_K_FRONTEND, h->sA, h->evA[buf]);
+    KBind t(h, FMX_K_FRONTEND, h->sA, evFE);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
       h->t_rds.spec = false; // the next step's schedule was not copied
@@ -1034,7 +1065,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     dec_advance(h, n);
   }
   if (spec16) { // the pinned image is reused FMX_HSLOTS simulations later: its read ends with the front end
-    h->t_rds.ev_use[h->t_rds.spec_img] = h->evA[buf];
+    h->t_rds.ev_use[h->t_rds.spec_img] = evFE;
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
   // ---- pilot BPF (sA, after the front end; read by k_pll) ----
@@ -1059,7 +1090,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
-  HIP_TRY(hipStreamWaitEvent(h->sC, h->evA[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sC, evFE, 0));
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
@@ -1104,7 +1135,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   h->evC_set[buf] = true;
   // ---- stereo PLL (sB) ----
-  HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : h->evA[buf], 0));
+  HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : evFE, 0));
   if (stereo) {
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;
@@ -1227,6 +1258,16 @@ int fmx_sync(void *handle) {
 }
 
 int fmx_num_channels(void *handle) { return handle ? H(handle)->C : 0; }
+
+int fmx_host_stats(void *handle, double *out, int n) {
+  Handle *h = H(handle);
+  if (!h || !out || n < 0) return FMX_E_INVALID;
+  const double v[3] = {static_cast<double>(h->host_waits), static_cast<double>(h->host_stalls), h->host_stall_ms};
+  for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  h->host_waits = h->host_stalls = 0;
+  h->host_stall_ms = 0.0;
+  return FMX_OK;
+}
 
 static int reset_channels(Handle *h, int channel, int extra) {
   if (channel < -1 || channel >= h->C) {

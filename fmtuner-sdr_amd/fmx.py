@@ -100,6 +100,7 @@ def lib():
         "fmx_memset": (i, [vp, vp, i, sz]),
         "fmx_timing_enable": (i, [vp, i]),
         "fmx_kernel_times": (i, [vp, C.POINTER(C.c_double), C.POINTER(i), i]),
+        "fmx_host_stats": (i, [vp, C.POINTER(C.c_double), i]),
         "fmx_synth_rds_bits": (i, [C.POINTER(SynthConfig), C.c_uint32, i, vp, vp]),
         "fmx_synth_host": (i, [C.POINTER(SynthConfig), C.c_uint32, i, C.c_int64, i, vp, vp, sz, i]),
         "fmx_synth_device": (i, [vp, C.POINTER(SynthConfig), C.c_uint32, i, C.c_int64, i, vp, vp, sz]),
@@ -234,6 +235,13 @@ class Handle:
         cnt = (C.c_int * nk)()
         self._ck(self.L.fmx_kernel_times(self.h, ms, cnt, nk), "fmx_kernel_times")
         return {KERNEL_NAMES[k]: (ms[k], cnt[k]) for k in range(nk)}
+
+    def host_stats(self):
+        """Host waits on pinned schedule images since the last call: (waits,
+        waits that blocked, milliseconds blocked)."""
+        v = (C.c_double * 3)()
+        self._ck(self.L.fmx_host_stats(self.h, v, 3), "fmx_host_stats")
+        return {"image_waits": int(v[0]), "blocked": int(v[1]), "blocked_ms": round(v[2], 4)}
 
 
 def synth_rds_bits(scfg, ch0, n_ch):

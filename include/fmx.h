@@ -38,11 +38,11 @@
 extern "C" {
 #endif
 
-/* ABI history: 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+/* ABI history: 7 (round 5) adds fmx_host_stats; 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
  * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
  * which changed that struct's size: callers must be rebuilt against this
  * header. */
-#define FMX_ABI_VERSION 6
+#define FMX_ABI_VERSION 7
 
 enum {
   FMX_OK = 0,
@@ -227,6 +227,11 @@ int fmx_timing_enable(void *handle, int enable);
  * FMX_E_INVALID otherwise -- the product libfmx.so reads no environment) */
 int fmx_debug_stamps(void *handle, unsigned long long *out, int n);
 int fmx_kernel_times(void *handle, double *ms, int *launches, int n);
+/* host-side waits of fmx_process_block since the last call (then reset):
+ * out[0] waits on a pinned schedule image's last reader, out[1] those that
+ * found it still pending (the host blocked), out[2] milliseconds blocked.
+ * Fills at most n (<= 3) entries. */
+int fmx_host_stats(void *handle, double *out, int n);
 
 /* ---- synthetic IQ (bench / tests input; see fmx_synth.h) ---- */
 typedef struct {

@@ -13,6 +13,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_LIB = os.path.join(_HERE, "libfmx_oracle.so")
 REF_LIB = os.path.join(_HERE, "_ref", "libfmx_ref.so")
+XDR_REF_LIB = os.path.join(_HERE, "_ref", "libfmx_xdrref.so")
 
 
 class OracleCfg(C.Structure):
@@ -36,6 +37,7 @@ class BlockInfo(C.Structure):
 
 _lib = None
 _ref = None
+_xref = None
 
 
 def lib():
@@ -95,6 +97,10 @@ def ref_available():
     return os.path.exists(REF_LIB)
 
 
+def xdr_ref_available():
+    return os.path.exists(XDR_REF_LIB)
+
+
 def ref():
     """The reference's own block_sync/group/util + signal_level, compiled by
     oracle/Makefile from /root/reference (travels as a built .so)."""
@@ -113,12 +119,22 @@ def ref():
                                        C.c_double, C.POINTER(C.c_double)]
         L.ref_smooth_signal_level.restype = C.c_float
         L.ref_smooth_signal_level.argtypes = [C.c_float, C.POINTER(i), C.POINTER(C.c_float)]
+        _ref = L
+    return _ref
+
+
+def xref():
+    """The reference's XDRServer (src/xdr_server.cpp) behind refdrv/xdr_driver.cpp."""
+    global _xref
+    if _xref is None:
+        L = C.CDLL(XDR_REF_LIB)
+        vp, i = C.c_void_p, C.c_int
         L.ref_xdr_pi_state.restype = i
         L.ref_xdr_pi_state.argtypes = [vp, vp, i, C.c_uint16]
         L.ref_xdr_session.restype = i
         L.ref_xdr_session.argtypes = [vp, vp, i, C.c_char_p, i, i, C.c_char_p, i]
-        _ref = L
-    return _ref
+        _xref = L
+    return _xref
 
 
 def make_cfg(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=4096,
@@ -209,10 +225,10 @@ def ref_blocksync(bits):
 
 
 def ref_xdr_pi_state(buf64, err8, fill, value):
-    """The reference's evaluatePiState (xdr_server.cpp:189-213), oracle/_ref."""
+    """The reference's evaluatePiState (xdr_server.cpp:189-213), oracle/_ref/libfmx_xdrref.so."""
     b = np.ascontiguousarray(buf64, dtype=np.uint16)
     e = np.ascontiguousarray(err8, dtype=np.uint8)
-    return ref().ref_xdr_pi_state(b.ctypes.data, e.ctypes.data, int(fill), int(value))
+    return xref().ref_xdr_pi_state(b.ctypes.data, e.ctypes.data, int(fill), int(value))
 
 
 def ref_xdr_session(groups, scan_lines=(), port=None):
@@ -228,7 +244,7 @@ def ref_xdr_session(groups, scan_lines=(), port=None):
     out = C.create_string_buffer(cap)
     for attempt in range(8):  # a busy port: another one
         pt = port or random.randint(20000, 60000)
-        rc = ref().ref_xdr_session(g.ctypes.data, e.ctypes.data, len(groups), scan or None, len(scan_lines), pt,
+        rc = xref().ref_xdr_session(g.ctypes.data, e.ctypes.data, len(groups), scan or None, len(scan_lines), pt,
                                    out, cap)
         if rc != -1 or port:
             break

@@ -21,7 +21,9 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace refdrv {
@@ -118,16 +120,22 @@ int ref_xdr_session(const uint16_t *groups, const uint8_t *errors, int n, const 
     if (line == "I1000,0") break;
   }
   // batches of groups (the server queue keeps 256 lines), each closed by a
-  // sentinel scan line: the server sends queued RDS lines before queued scan
-  // lines, so the sentinel arrives after every line of its batch
+  // sentinel scan line.  The client loop (xdr_server.cpp:808-844) takes the
+  // RDS queue and the scan queue under two locks in one pass: a pass that
+  // reads the RDS queue while a batch is still being pushed can send the
+  // batch's sentinel before the batch's tail, which then arrives (in order)
+  // before the next batch's lines.  So after the last batch a second sentinel
+  // is pushed after a pause longer than a loop pass: every RDS line precedes it.
   auto drain_to = [&](const std::string &sentinel) -> bool {
     for (;;) {
       if (!refdrv::read_line(fd, buf, line)) return false;
       if (line == "U" + sentinel) return true;
       if (!line.empty() && line[0] == 'S') {
-        // a periodic signal line, after the periodic "P" line when the
-        // server has a debounced PI (xdr_server.cpp:848-878): drop both
-        if (!got.empty() && got.back()[0] == 'P') got.pop_back();
+        // a periodic signal line, right after the periodic "P%04X" line when
+        // the server has a debounced PI and RDS within 1.5 s
+        // (xdr_server.cpp:848-878; every RDS line here is recent): drop both.
+        // An updateRDS P line may carry a '?' suffix; the periodic one never
+        if (!got.empty() && got.back().size() == 5 && got.back()[0] == 'P') got.pop_back();
         continue;
       }
       got.push_back(line);
@@ -140,6 +148,11 @@ int ref_xdr_session(const uint16_t *groups, const uint8_t *errors, int n, const 
     const std::string s = "#fmx-batch-" + std::to_string(k);
     srv.pushScanLine(s);
     if (!drain_to(s)) return fail(-3);
+  }
+  if (n > 0) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    srv.pushScanLine("#fmx-rds-end");
+    if (!drain_to("#fmx-rds-end")) return fail(-3);
   }
   const char *sp = scan;
   for (int i = 0; i < nscan; ++i) {

@@ -135,7 +135,7 @@ def test_xdr_lines_from_gpu_groups(fmx, oracle, cfg3_pipelined):
     assert got == want
     # and the reference's own XDRServer (oracle/_ref, built in the build
     # container and shipped as a library) over the HIP groups
-    if oracle.ref_available():
+    if oracle.xdr_ref_available():
         hip_groups = [grp for j in (0, 1, 0) for b in range(NBLK) for grp in g[b]["groups"][j]]
         assert oracle.ref_xdr_session(hip_groups) == got
     # ~5 groups per station in 36 blocks (11.4 groups/s), three passes

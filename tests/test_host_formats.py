@@ -105,8 +105,8 @@ def test_xdr_rds_lines_match_reference_live(fmx, oracle):
     """The same against the reference server compiled here (oracle/_ref),
     on fresh seeded streams: random error masks, missing A / B blocks, PI
     changes, and a long run past the server's 64-entry PI history."""
-    if not oracle.ref_available():
-        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    if not oracle.xdr_ref_available():
+        pytest.skip("oracle/_ref/libfmx_xdrref.so not built (no /root/reference here)")
     rng = np.random.default_rng(99)
     for trial in range(3):
         groups = _random_groups(rng, 700, [0x1234, 0xC0DE, 0x9ABC, 0x0001][: trial + 2])
@@ -117,8 +117,8 @@ def test_xdr_rds_lines_match_reference_live(fmx, oracle):
 def test_xdr_pi_state_restatement_matches_reference(oracle):
     """evaluatePiState (xdr_server.cpp:189-213, the reference's own code in
     oracle/_ref) against the tests' restatement, on random histories."""
-    if not oracle.ref_available():
-        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    if not oracle.xdr_ref_available():
+        pytest.skip("oracle/_ref/libfmx_xdrref.so not built (no /root/reference here)")
     rng = np.random.default_rng(5)
     for _ in range(3000):
         x = PyXdr()

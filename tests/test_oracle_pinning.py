@@ -29,6 +29,18 @@ def bits_of(s):
     return np.frombuffer(s.encode(), dtype=np.uint8) - ord("0")
 
 
+def test_reference_libraries_built_where_the_reference_lies(oracle):
+    """Where /root/reference is present (the build container), both reference
+    libraries must have been built: the reference-pinned tests below skip when
+    they are absent, so a failed build must fail here instead of skipping
+    quietly (on the GPU box the reference is absent and the built files are
+    what travels)."""
+    if not os.path.isdir("/root/reference/src"):
+        pytest.skip("no /root/reference on this host")
+    assert oracle.ref_available(), oracle.REF_LIB
+    assert oracle.xdr_ref_available(), oracle.XDR_REF_LIB
+
+
 @pytest.mark.parametrize("stream", [s["name"] for s in load("blocksync.json")["streams"]])
 def test_blocksync_matches_reference_fixture(oracle, stream):
     fx = {s["name"]: s for s in load("blocksync.json")["streams"]}[stream]

@@ -109,8 +109,8 @@ def xdr_scan_lines():
 
 def main():
     os.makedirs(GOLD, exist_ok=True)
-    if not oracle.ref_available():
-        sys.exit("oracle/_ref/libfmx_ref.so missing: build it with `make -C oracle` in the build container")
+    if not (oracle.ref_available() and oracle.xdr_ref_available()):
+        sys.exit("oracle/_ref/libfmx_ref.so / libfmx_xdrref.so missing: build them with `make -C oracle` in the build container")
     fx = []
     for name, bits in streams().items():
         groups = oracle.ref_blocksync(bits)
