@@ -1011,13 +1011,8 @@ __device__ __forceinline__ void dma_dword_s(const float *base, uint32_t voff, ui
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p);
 }
-// sine and cosine of an NCO word (phase 2 pi theta / 2^32) by v_sin / v_cos,
-// which take turns: the word as a signed fraction of a turn, in [-0.5, 0.5)
-__device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) {
-  const float r = (float)(int32_t)theta * 2.3283064365386963e-10f;
-  *s = __builtin_amdgcn_sinf(r);
-  *c = __builtin_amdgcn_cosf(r);
-}
+// sine and cosine of an NCO word (fmx_word_sincos, fmx_math.h)
+__device__ __forceinline__ void word_sincos(uint32_t theta, float *s, float *c) { fmx_word_sincos(theta, s, c); }
 
 #include "fmx_pll.inc"
 

@@ -1,16 +1,8 @@
-// fmx_math.h -- small fp32 math kernels shared by the HIP kernels and the
-// host-side accuracy test (tests/cpp/math_test.cpp).
-//
-// fmx_sincos: sin and cos of one fp32 phase, |x| <= 8 (the NCO phases of the
-// stereo PLL, stereo_decoder.cpp:251-253 / 277-278, and the RDS mix-down,
-// subcarrier.cpp:158, are wrapped to [-pi, 2pi]).  Three-part Cody-Waite
-// reduction by pi/2 with FMA (exact for |q| <= 5) and the cephes sinf/cosf
-// minimax polynomials on [-pi/4, pi/4] with the reduced argument carried as
-// a float pair: one shared reduction and ~30 VALU
-// instead of the libm sincosf path with its large-argument branch.  Max error
-// against the correctly rounded result is checked by tests/test_math.py:
-// < 1 ulp, ~95 % correctly rounded over [-2pi, 2pi] (the oracle's glibc
-// sinf/cosf are the reference; parity bars on the PLL outputs are tolerances).
+// fmx_math.h -- small fp32 / integer math shared by the HIP kernels and the
+// host-side accuracy tests (tests/cpp/*_test.cpp, tests/hip/pllmath_sweep.hip).
+// Every helper here is called by a product kernel; each has an exhaustive or
+// swept check against the reference's own arithmetic (tests/test_math.py,
+// tests/test_gpu_pllmath.py).
 #ifndef FMX_MATH_H
 #define FMX_MATH_H
 
@@ -22,48 +14,6 @@
 #include <cmath>
 #define FMX_HD inline
 #endif
-
-// The quadrant-swapped polynomials of fmx_sincos_q before their signs:
-// sin x = (qi & 2) ? -*s0 : *s0, cos x = ((qi + 1) & 2) ? -*c0 : *c0.  A
-// recursion that multiplies by sin x can flip its other factor's sign bit
-// off the dependency chain instead (the k_pll feedback loop).
-FMX_HD void fmx_sincos_q_abs(float x, float q, int qi, float *s0, float *c0) {
-  // r = x - q pi/2 as rh + rl (pi/2 in three parts)
-  const float r1 = fmaf(-q, 1.57079637050628662109375f, x);
-  const float rh = fmaf(-q, -4.3711388286737929e-08f, r1);
-  float rl = fmaf(-q, -4.3711388286737929e-08f, r1 - rh);
-  rl = fmaf(-q, -1.7151245100058819e-15f, rl);
-  const float z = rh * rh;
-  // sin: rh + (rl + rh z P(z)),  degree-9 minimax
-  float ps = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
-  ps = fmaf(z, ps, 0.00833307858556509017944336f);
-  ps = fmaf(z, ps, -0.166666597127914428710938f);
-  const float sr = rh + fmaf(rh * z, ps, rl);
-  // cos: (1 - z/2) split exactly, + z^2 Q(z) - rh rl
-  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
-  pc = fmaf(z, pc, 4.166664568298827e-2f);
-  const float hz = 0.5f * z;
-  const float w = 1.0f - hz;
-  const float tail = (1.0f - w) - hz;
-  const float cr = w + (fmaf(z * z, pc, tail) - rh * rl);
-  const bool swap = (qi & 1) != 0;
-  *s0 = swap ? cr : sr;
-  *c0 = swap ? sr : cr;
-}
-
-// sin and cos of x given its quadrant count qi (x ~ qi pi/2, |x - qi pi/2|
-// <= pi/4 + a few ulp); q = (float)qi.
-FMX_HD void fmx_sincos_q(float x, float q, int qi, float *s, float *c) {
-  float s0, c0;
-  fmx_sincos_q_abs(x, q, qi, &s0, &c0);
-  *s = (qi & 2) ? -s0 : s0;
-  *c = ((qi + 1) & 2) ? -c0 : c0;
-}
-
-FMX_HD void fmx_sincos(float x, float *s, float *c) {
-  const float q = rintf(x * 0.636619772367581343f);
-  fmx_sincos_q(x, q, (int)q, s, c);
-}
 
 // x / c for a constant c with rc = RN(1/c): q = x rc, then one Markstein
 // correction with the exact FMA residual -- 3 dependent ops instead of the
@@ -123,31 +73,46 @@ FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
   return (s >= 4294967296.0f) ? 0u : fmx_cvt_u32(s);
 }
 
-// Quadrant count of an NCO phase word: round(theta / 2^30) in 0..4, the
-// quadrant of the exact phase 2 pi theta / 2^32.  The float phase the
-// reference computes from theta is within 0.5 ulp of it, so fmx_sincos_q of
-// that phase with this count stays inside the polynomial range; it is known
-// as soon as theta is, off the phase's dependency chain (the k_pll loop).
-FMX_HD int fmx_nco_quadrant(uint32_t theta) { return (int)((theta >> 30) + ((theta >> 29) & 1u)); }
-
-// sin(2 pi theta / 2^32) for the stereo PLL's feedback chain only (k_pll
-// W0, stereo_decoder.cpp:251-256): half-turn reduction on the phase word,
-// theta = m 2^31 + d (|d| <= 2^30, m's parity returned in bit 31 of *sg),
-// r = d pi / 2^31 (one rounding), and the degree-9 minimax sine on
-// [-pi/2, pi/2]; sin = (*sg ? -1 : 1) * the return value.  11 VALU instead
-// of the float phase (an f64 multiply) and both quadrant polynomials.  Its
-// error against sin of the reference's float phase is measured over all 2^32
-// words by tests/cpp/pllsin_test.cpp (tests/golden/pllsin_exhaustive.json).
-FMX_HD float pll_sin_word(uint32_t theta, uint32_t *sg) {
-  const uint32_t s = (theta + 0x40000000u) & 0x80000000u;
-  const float r = (float)(int32_t)(theta ^ s) * 1.4629180792671596e-09f;
-  const float z = r * r;
-  float u = fmaf(z, 2.6083159809786593541503e-06f, -0.0001981069071916863322258f);
-  u = fmaf(u, z, 0.00833307858556509017944336f);
-  u = fmaf(u, z, -0.166666597127914428710938f);
-  *sg = s;
-  return fmaf(z, u * r, r);
+#ifdef __HIPCC__
+// The stereo PLL's feedback chain (k_pll W0, stereo_decoder.cpp:178-192), one
+// sample: vcoQ = sin(phase) of the NCO word theta, then liquid's pll_step
+// (dtheta += constrain(e alpha), theta += constrain(e beta)) and step (theta
+// += dtheta), e = pilot vcoQ.  These two functions ARE the chain's
+// arithmetic: k_pll calls them, and the GPU test kernel
+// (tests/hip/pllmath_sweep.hip) sweeps them against the reference's float
+// phase / double-precision constrain (tests/test_gpu_pllmath.py,
+// tests/golden/pllmath_gpu.json).
+//
+// fmx_chain_sin: v_sin_f32 takes turns; the word's top 23 bits become the
+// mantissa of a float in [1, 2) with one v_alignbit_b32 ({0x7F, theta} >> 9 =
+// 0x3F800000 | theta >> 9), so sin(2 pi (1 + theta / 2^32)) = sin(2 pi theta /
+// 2^32) up to the truncated 9 bits (< 2^-23 turn) and v_sin's own error.  One
+// VALU op instead of a convert and a multiply on the serial chain.
+__device__ __forceinline__ float fmx_chain_sin(uint32_t theta) {
+  return __builtin_amdgcn_sinf(__builtin_bit_cast(float, __builtin_amdgcn_alignbit(0x7Fu, theta, 9u)));
 }
+// fmx_word_sincos: sine and cosine of an NCO word (phase 2 pi theta / 2^32)
+// by v_sin / v_cos, which take turns: the word as a signed fraction of a
+// turn in [-0.5, 0.5) (rounded to 24 bits: < 2^-25 turn).  k_pll's outputs
+// (vcoI / vcoQ of the pilot I/Q, cos 2 phase of the L-R mix,
+// stereo_decoder.cpp:178-180,194-195,218-220), swept with the chain.
+__device__ __forceinline__ void fmx_word_sincos(uint32_t theta, float *s, float *c) {
+  const float r = (float)(int32_t)theta * 2.3283064365386963e-10f;
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
+// fmx_chain_words: the two constrain words of pll_step from the pilot's
+// pre-products pa = pilot alpha/2pi 2^32, pb = pilot beta/2pi 2^32 (one packed
+// multiply by vcoQ, then truncating converts): for |e k| < 1/2 the word
+// constrain(e k) = frac(e k / 2 pi) 2^32 equals (uint32)(int32)(e k / 2 pi 2^32)
+// up to the float roundings, which the sweep bounds.
+__device__ __forceinline__ void fmx_chain_words(float pa, float pb, float vcoQ, uint32_t *ca, uint32_t *cb) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 x = f2{pa, pb} * f2{vcoQ, vcoQ};
+  *ca = (uint32_t)(int32_t)x.x;
+  *cb = (uint32_t)(int32_t)x.y;
+}
+#endif
 
 // RF-level clip pre-test on one 4-byte word of u8 I/Q (signal_level.cpp:
 // computeSignalLevel counts samples with a component <= 8 or >= 247): nonzero

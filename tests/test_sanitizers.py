@@ -118,9 +118,7 @@ def test_oracle_stages_and_blocksync_sanitized(fmx, san_exe):
 
 
 @pytest.mark.parametrize("name,args,extra", [
-    ("math_test", ["20000"], []),
     ("divconst_test", ["4099"], ["-fopenmp"]),
-    ("pllsin_test", ["4099"], ["-fopenmp"]),
     ("atan2_test", ["20000"], ["-fopenmp"]),
     ("ncoconstrain_test", ["4099"], ["-fopenmp"]),
 ])

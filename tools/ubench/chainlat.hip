@@ -43,73 +43,37 @@ __global__ void k_op(const float *in, unsigned long long *out, float *sink) {
 }
 
 // ---- the W0 PLL feedback iteration ----
-// V0: k_pll today (two exact constrains with the f64 product, the word sine)
-// V1: the constrains' f64 product as f32 hi/lo (bit-exact candidate), word sine
-// V2: the (theta + dtheta) add off the chain + the constrain sum reassociated
-// V3: V2 with the hardware sine (v_sin_f32 of theta / 2^32 turns)
-// V4: V3 with the constrain as fract (p = err*beta/2pi in f32, no f64)
-__device__ __forceinline__ uint32_t cons_v1(float x) {
-  // p = RN_f32(x * K), K = 0.159154943091895 (double) as Kh + Kl
-  const float Kh = 0.15915493667125702f, Kl = -4.0856918e-09f; // placeholder split (timing only)
-  const float ph = x * Kh;
-  const float e = fmaf(x, Kh, -ph);
-  const float p = ph + fmaf(x, Kl, e);
-  const float f = p - floorf(p);
-  const uint32_t uu = (uint32_t)(f * 4294967296.0f);
-  return (f == 1.0f) ? 0u : uu;
-}
-__device__ __forceinline__ uint32_t cons_fract(float p) {
-  const float f = __builtin_amdgcn_fractf(p);
-  return (uint32_t)(f * 4294967296.0f);
-}
+// R4: the round-4 k_pll chain: per sample two products pilot k 2^32 vcoQ,
+//     two truncating converts, add3, and v_sin of (float)(int32)theta 2^-32
+// R5: the round-5 chain (fmx_chain_words / fmx_chain_sin): one packed
+//     multiply, two converts, add3, v_alignbit_b32 and v_sin
 template <int V>
 __global__ void k_pll(const float *pilot, unsigned long long *out, float *sink) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
   uint32_t theta = threadIdx.x * 7919u, dtheta = 123456789u;
-  const float alpha = 1e-2f, beta = 0.1f;
-  const float ka = alpha * 0.159154943091895f, kb = beta * 0.159154943091895f;
+  const float ka = 1e-2f * 0.159154943091895f, kb = 0.1f * 0.159154943091895f;
+  const float kaw = ka * 4294967296.0f, kbw = kb * 4294967296.0f;
   float pv[8];
   for (int i = 0; i < 8; ++i) pv[i] = pilot[(threadIdx.x + i) & 63];
-  uint32_t sg = 0;
-  float s = pll_sin_word(theta, &sg);
+  float s = fmx_chain_sin(theta);
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < NREP; ++r) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      uint32_t ca, cb;
       if constexpr (V == 0) {
-        const float err = __uint_as_float(__float_as_uint(pv[i]) ^ sg) * s;
-        dtheta += fmx_nco_constrain(err * alpha);
-        theta += fmx_nco_constrain(err * beta);
-        theta += dtheta;
-        s = pll_sin_word(theta, &sg);
-      } else if constexpr (V == 1) {
-        const float err = __uint_as_float(__float_as_uint(pv[i]) ^ sg) * s;
-        dtheta += cons_v1(err * alpha);
-        theta += cons_v1(err * beta);
-        theta += dtheta;
-        s = pll_sin_word(theta, &sg);
-      } else if constexpr (V == 2) {
-        const float err = __uint_as_float(__float_as_uint(pv[i]) ^ sg) * s;
-        const uint32_t ca = fmx_nco_constrain(err * alpha);
-        const uint32_t T = theta + dtheta;  // off the chain
-        dtheta += ca;
-        theta = T + (ca + fmx_nco_constrain(err * beta));
-        s = pll_sin_word(theta, &sg);
-      } else if constexpr (V == 3) {
-        const float err = pv[i] * s;
-        const uint32_t ca = fmx_nco_constrain(err * alpha);
-        const uint32_t T = theta + dtheta;
-        dtheta += ca;
-        theta = T + (ca + fmx_nco_constrain(err * beta));
-        s = __builtin_amdgcn_sinf((float)(int32_t)theta * 2.3283064365386963e-10f);
+        ca = (uint32_t)(int32_t)(pv[i] * kaw * s);
+        cb = (uint32_t)(int32_t)(pv[i] * kbw * s);
       } else {
-        const float err = pv[i] * s;
-        const uint32_t ca = cons_fract(err * ka);
-        const uint32_t T = theta + dtheta;
-        dtheta += ca;
-        theta = T + (ca + cons_fract(err * kb));
-        s = __builtin_amdgcn_sinf((float)(int32_t)theta * 2.3283064365386963e-10f);
+        const f2 pab = f2{pv[i], pv[i]} * f2{kaw, kbw};
+        fmx_chain_words(pab.x, pab.y, s, &ca, &cb);
       }
+      const uint32_t T = theta + dtheta;
+      dtheta += ca;
+      theta = T + ca + cb;
+      if constexpr (V == 0) s = __builtin_amdgcn_sinf((float)(int32_t)theta * 2.3283064365386963e-10f);
+      else s = fmx_chain_sin(theta);
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -159,13 +123,9 @@ int main() {
   printf("%-34s %7.2f\n", ops[10], run(k_op<10>, in, out, sink, 8));
   printf("%-34s %7.2f\n", ops[11], run(k_op<11>, in, out, sink, 8));
   printf("%-34s %7.2f\n", ops[12], run(k_op<12>, in, out, sink, 8));
-  const char *vs[] = {"V0 k_pll today", "V1 f32 hi/lo constrain product", "V2 reassociated adds",
-                      "V3 V2 + v_sin_f32", "V4 V3 + fract constrain"};
+  const char *vs[] = {"R4 cvt+mul+sin word sine", "R5 pk_mul + alignbit + sin"};
   printf("PLL feedback iteration, ticks per sample\n");
   printf("%-34s %7.2f\n", vs[0], run(k_pll<0>, in, out, sink, 8));
   printf("%-34s %7.2f\n", vs[1], run(k_pll<1>, in, out, sink, 8));
-  printf("%-34s %7.2f\n", vs[2], run(k_pll<2>, in, out, sink, 8));
-  printf("%-34s %7.2f\n", vs[3], run(k_pll<3>, in, out, sink, 8));
-  printf("%-34s %7.2f\n", vs[4], run(k_pll<4>, in, out, sink, 8));
   return 0;
 }
