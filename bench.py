@@ -60,8 +60,10 @@ PER_IQ = {
     "rds": (4.0 * 0.7125 / 10.0, 15.0),
     "rs": (0.4 + 4.0 * 0.7125 / 10.0, 7.4),
     "pilot": (0.4 + 0.4, 61.0),
+    "frontend_generic": (2.0 + 0.4, 112.0 + 32.4),
 }
-KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs", "pilot": "k_pilot"}
+KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs", "pilot": "k_pilot",
+         "frontend_generic": "k_frontend"}
 
 
 def pmc_bytes(pmc, k):
@@ -71,7 +73,13 @@ def pmc_bytes(pmc, k):
         return None
     return sum(pmc[n]["hbm_bytes_per_launch"] for n in names)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
-FP32_PEAK_TFLOPS = 157.3   # dense FP32 VALU
+# per-unit peaks (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs at ~2.4 GHz; a SIMD
+# retires one wave64 VALU instruction per 2 cycles when several waves share it
+CLOCK_HZ = 2.4e9
+N_CU = 256
+VALU_ISSUE_PEAK = N_CU * 4 * CLOCK_HZ / 2.0   # wave-instructions / s
+MFMA_F16_PEAK = 2.5e15                        # dense FLOP / s
+MFMA_F32_PEAK = 157.3e12
 METRIC = "IQ MS/s demodulated per GPU (2.4 MS/s FM channels, stereo+RDS) at 1/2/4/8 MI355X"
 
 
@@ -87,6 +95,8 @@ def parse(argv=None):
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the all-core CPU sample")
+    ap.add_argument("--retune-per-step", action="store_true",
+                    help="diagnostic: fmx_retune one channel before every step (main.cpp:1028-1042)")
     ap.add_argument("--sync-steps", action="store_true",
                     help="diagnostic: synchronize after every step (no cross-step overlap; not the reported mode)")
     ap.add_argument("--pmc-json", default=None,
@@ -151,6 +161,34 @@ def tag_key(path):
 def newest_pmc():
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")), key=tag_key)
     return files[-1] if files else None
+
+
+def newest_units(channels, block):
+    """The newest profiles/r*_units*.json (tools/gpu_units.sh) of this shape."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_units*.json")), key=tag_key, reverse=True):
+        try:
+            with open(f) as fh:
+                u = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if int(u.get("channels", -1)) == channels and int(u.get("block", -1)) == block:
+            return f, u
+    return None, None
+
+
+def unit_fracs(u, t):
+    """Fractions of each unit's peak that the counted work of one launch
+    (units-file entry u) takes over t seconds."""
+    out = {}
+    if "valu_insts" in u:
+        out["valu"] = u["valu_insts"] / t / VALU_ISSUE_PEAK
+    if "mfma_flop_f16" in u or "mfma_flop_f32" in u:
+        out["mfma"] = (u.get("mfma_flop_f16", 0.0) / MFMA_F16_PEAK + u.get("mfma_flop_f32", 0.0) / MFMA_F32_PEAK) / t
+    if "lds_active_cycles" in u:
+        out["lds"] = u["lds_active_cycles"] / (N_CU * CLOCK_HZ * t)
+    if "hbm_bytes" in u:
+        out["hbm"] = u["hbm_bytes"] / t / (HBM_PEAK_GBS * 1e9)
+    return {k: round(v, 4) for k, v in out.items()}
 
 
 def cpu_info():
@@ -320,6 +358,8 @@ def main():
     torch.cuda.synchronize()
 
     def step(b):
+        if args.retune_per_step:  # diagnostic A/B: a live receiver retuning one channel per block
+            h.retune((b * 7919) % C, -1)
         h.process_block(d_iq.data_ptr() + b * 2 * n_iq, row, B, outs[b % 3])
         if args.sync_steps:
             h.sync()
@@ -394,9 +434,14 @@ def main():
         avg = {k: float("nan") for k in ktimes}
     dom = max(avg, key=avg.get)
     dom_s = avg[dom]
+    units_path, ucnt = newest_units(C, B)
     pmc_path = args.pmc_json or newest_pmc()
     pmc = None
-    if pmc_path and os.path.exists(pmc_path):
+    if ucnt and not args.pmc_json:
+        # the units passes carry FETCH / WRITE too: one source for both
+        pmc_path = units_path
+        pmc = {k: {"hbm_bytes_per_launch": e["hbm_bytes"]} for k, e in ucnt["kernels"].items() if "hbm_bytes" in e}
+    elif pmc_path and os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
@@ -411,9 +456,43 @@ def main():
     step_traffic = None
     if all(pmc_bytes(pmc, k) is not None for k in avg):
         step_traffic = sum(pmc_bytes(pmc, k) * lps.get(k, 1) for k in avg)
-    path_tflops = ALG_FLOP_PER_IQ * units_step / (ms_per_step * 1e-3) / 1e12
-    roof = {"bound": "hbm", "kernel": KNAME[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+    # measured per-unit utilisation (counters of tools/gpu_units.sh over the
+    # live launch times of this run): the dominant kernel's and the step's
+    unit_rec = None
+    if ucnt:
+        uk = ucnt["kernels"]
+        dom_u = unit_fracs(uk.get(KNAME[dom], {}), dom_s)
+        step_work = {}
+        for k in avg:
+            e = uk.get(KNAME[k])
+            if e is None:
+                continue
+            for name in ("valu_insts", "mfma_flop_f16", "mfma_flop_f32", "lds_active_cycles", "hbm_bytes"):
+                if name in e:
+                    step_work[name] = step_work.get(name, 0.0) + e[name] * lps.get(k, 1)
+        step_u = unit_fracs(step_work, ms_per_step * 1e-3)
+        unit_rec = {"source": os.path.relpath(units_path, ROOT),
+                    "source_library_sha256_16": ucnt.get("library_sha256_16"),
+                    "source_matches_loaded_library": ucnt.get("library_sha256_16") == _sha16(fmx.LIB_PATH),
+                    "peaks": {"valu": f"{VALU_ISSUE_PEAK:.4g} wave-instr/s (1024 SIMDs x 2.4 GHz / 2 cycles)",
+                              "mfma": "2.5 PFLOP/s f16, 157.3 TFLOP/s f32 (dense)",
+                              "lds": f"{N_CU} CUs x 2.4 GHz LDS-array cycles (SQ_LDS_IDX_ACTIVE)",
+                              "hbm": f"{HBM_PEAK_GBS:.0f} GB/s"},
+                    "dominant_kernel": {"kernel": KNAME[dom], "avg_launch_ms": round(dom_s * 1e3, 4), **dom_u},
+                    "dominant_binding_unit": max(dom_u, key=dom_u.get) if dom_u else None,
+                    "step": {"ms_per_step": round(ms_per_step, 4), **step_u},
+                    "step_binding_unit": max(step_u, key=step_u.get) if step_u else None}
+    # the contract's roof (hbm | mfma): whichever of the two the dominant
+    # kernel's counters put closer to its peak (hbm when there are none);
+    # achieved = the ALGORITHMIC bytes (or MFMA FLOP) of one launch over its
+    # live time.  The unit that binds among all four is units.*_binding_unit.
+    bound, r_ach, r_peak, r_unit = "hbm", round(achieved, 1), HBM_PEAK_GBS, "GB/s"
+    du = unit_rec["dominant_kernel"] if unit_rec else {}
+    if du.get("mfma", 0.0) > du.get("hbm", 0.0):
+        alg_flop = PER_IQ[dom][1] * units
+        bound, r_ach, r_peak, r_unit = "mfma", round(alg_flop / dom_s / 1e12, 2), MFMA_F16_PEAK / 1e12, "TFLOP/s"
+    roof = {"bound": bound, "kernel": KNAME[dom], "achieved": r_ach, "peak": r_peak,
+            "unit": r_unit, "frac": round(r_ach / r_peak, 4), "traffic": traffic,
             "traffic_source": os.path.relpath(pmc_path, ROOT) if pmc else None,
             "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_iq": ALG_BYTES_PER_IQ,
             "avg_launch_ms": round(dom_s * 1e3, 4),
@@ -421,10 +500,12 @@ def main():
             # path's algorithmic bytes: intermediates round-tripping HBM
             "step_traffic": step_traffic,
             "step_traffic_over_algorithmic": round(step_traffic / (ALG_BYTES_PER_IQ * units_step), 3) if step_traffic else None,
-            # the roof that binds this path (no MFMA: FIR/IIR/PLL work is FP32 VALU)
-            "valu_path": {"achieved": round(path_tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": round(path_tflops / FP32_PEAK_TFLOPS, 4), "flop_per_iq": ALG_FLOP_PER_IQ,
-                          "per": "ms_per_step"}}
+            # what the hardware units actually do: measured fractions of each
+            # unit's peak (VALU issue, MFMA, LDS, HBM) for the dominant kernel
+            # and the whole step; the FIRs run on f16 MFMA, the recursions on
+            # the VALU, and none of the four is near its roof -- the path is
+            # latency-bound
+            "units": unit_rec}
     kern = {}
     for k, v in ktimes.items():
         if v[1] == 0:
@@ -437,7 +518,11 @@ def main():
                # live in the pipelined timed region (co-running kernels included)
                "design_bytes_per_launch": bpi * units,
                "design_hbm_gbs": round(bpi * units / avg_s / 1e9, 1),
-               "fp32_tflops": round(fpi * units / avg_s / 1e12, 3)}
+               # the kernel's share of the path's 290 algorithmic FLOP/IQ (FIR MACs
+               # as 2 FLOP; most of it runs on f16 hi/lo MFMA passes)
+               "alg_tflops": round(fpi * units / avg_s / 1e12, 3)}
+        if ucnt and KNAME[k] in ucnt["kernels"]:
+            ent["units"] = unit_fracs(ucnt["kernels"][KNAME[k]], avg_s)
         pb = pmc_bytes(pmc, k)
         if pb is not None:
             ent["pmc_bytes_per_launch"] = pb
@@ -469,7 +554,8 @@ def main():
         "config": {"workload": wl + ", M=10 -> 240 kHz, dsp_block=4096, deemphasis 50 us",
                    "total_channels": int(chans_all), "channels_rank0": C, "block": B, "iq_rate": 2_400_000,
                    "parallelism": f"channels/{world}gpu", "backend": backend if world > 1 else None,
-                   "world_reported": world_reported},
+                   "world_reported": world_reported,
+                   **({"retune_per_step": True} if args.retune_per_step else {})},
         "per_gpu_ms_s": round(value / world, 1),
         "realtime_channels_per_gpu": round(value / world / 2.4, 1),
         "roofline": roof,

@@ -134,6 +134,10 @@ struct Handle {
   FmxRdsState *rds = nullptr;
   int *reset_mask = nullptr;
   std::vector<int> hmask;
+  // process_block's channel resets of this step, per stream part (round 5):
+  // the front-end part runs on sA at prepare time, the others on their
+  // streams right before their kernels (fmx_capi.cpp process_block)
+  std::vector<ResetList> rl_pending;
   int *mute = nullptr; // [C][2] retune fade/mute {remaining, total} (main.cpp:1310-1337)
   float *dec_scratch = nullptr; // [C][2 * block] complex, fmx_decimate_u8 (allocated on first use)
   // intermediates (double-buffered by step parity)
@@ -603,6 +607,56 @@ static int prepare(Handle *h) {
   return apply_resets(h);
 }
 
+// the pending lists' `part` on stream s (the part's owner)
+static int launch_reset_parts(Handle *h, int part, hipStream_t s) {
+  for (const ResetList &L : h->rl_pending) {
+    if (launch_reset_list(reset_args(h), L, part, h->st_idx, s) != FMX_OK) {
+      h->err = "reset kernel launch failed";
+      return FMX_E_HIP;
+    }
+  }
+  return FMX_OK;
+}
+
+// process_block's resets without draining the pipeline: up to
+// FMX_RESET_LISTS_MAX lists of FMX_RESET_LIST channels (kernel arguments, no
+// upload) whose parts run on the stream that owns each part's state, right
+// before that stream's kernel of this step -- after the previous step's
+// kernel of the same stream, before this step's.  A reset of a handle's
+// every channel, object creation, or more channels than the lists hold take
+// the joined path (prepare).  A retune per block at 4096 channels: 1.01 ->
+// see profiles/r05*_ab_retune* (round 4's join drained the pipeline).
+#define FMX_RESET_LISTS_MAX 4
+static int prepare_pipelined(Handle *h) {
+  int rc = sync_params(h);
+  if (rc != FMX_OK) return rc;
+  h->rl_pending.clear();
+  int cnt = 0;
+  bool create = false;
+  for (int v : h->hmask) {
+    cnt += (v != 0);
+    create |= (v & RS_CREATE) != 0;
+  }
+  if (cnt == 0) return FMX_OK;
+  if (create || cnt > FMX_RESET_LISTS_MAX * FMX_RESET_LIST) return apply_resets(h);
+  ResetList L{};
+  for (int c = 0; c < h->C; ++c) {
+    const int v = h->hmask[static_cast<size_t>(c)];
+    if (v == 0) continue;
+    if (v & RS_DECIM) h->dec_fill = 0;
+    L.ch[L.n] = c;
+    L.m[L.n] = v;
+    if (++L.n == FMX_RESET_LIST) {
+      h->rl_pending.push_back(L);
+      L = ResetList{};
+    }
+  }
+  if (L.n > 0) h->rl_pending.push_back(L);
+  std::fill(h->hmask.begin(), h->hmask.end(), 0);
+  return launch_reset_parts(h, RSP_FRONT, h->sA);
+}
+
+
 /* ---------------- reference setters (host mirrors) ---------------- */
 static void set_bandwidth(Handle *h, int c, int bw) { // fm_demod.cpp:168-204
   const int sel = bandwidth_select(bw, h->w0[static_cast<size_t>(c)]);
@@ -989,7 +1043,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     return FMX_E_INVALID;
   }
   if (n == 0) return FMX_OK;
-  if ((rc = prepare(h)) != FMX_OK) return rc;
+  if ((rc = prepare_pipelined(h)) != FMX_OK) return rc;
   if (h->timing) harvest_timing(h);
   const bool stereo = h->cfg.stereo != 0;
   const bool rds = h->cfg.rds != 0;
@@ -1038,7 +1092,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     // (16 outputs' windows span <= 15 del + 31 samples: inside k_rs's 64 for del <= 2.1)
     // k_rs takes one resampler schedule for all channels: the RDS timing set
     // is never reset per channel (SubcarrierSet::reset, subcarrier.cpp:108)
-    const bool fe8 = frontend_is_fe8(a, h->M, h->hdes->dec_tpp, dec_warm(h));
+    const bool fe8 = frontend_is_fe8(a, h->M, h->hdes->dec_tpp);
     use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 && fe8;
     // the pilot BPF of a k_fe8 step runs as k_pilot (after it, on sA): k_fe8
     // writes the MPX and the stereo history rows k_pilot starts from
@@ -1055,7 +1109,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.next_sched_dst = h->t_rds.d_slot[nrslot];
       a.next_sched_n16 = spec16;
     }
-    KBind t(h, FMX_K_FRONTEND, h->sA, evFE);
+    KBind t(h, fe8 ? FMX_K_FRONTEND : FMX_K_FRONTEND_GENERIC, h->sA, evFE);
     if ((rc = launch_frontend_m(a, h->M, h->hdes->dec_tpp, h->sA, dec_warm(h))) != FMX_OK) {
       h->err = "frontend launch failed";
       h->t_rds.spec = false; // the next step's schedule was not copied
@@ -1091,6 +1145,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
   HIP_TRY(hipStreamWaitEvent(h->sC, evFE, 0));
+  if ((rc = launch_reset_parts(h, RSP_RDS, h->sC)) != FMX_OK) return rc;
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
@@ -1136,6 +1191,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   h->evC_set[buf] = true;
   // ---- stereo PLL (sB) ----
   HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : evFE, 0));
+  if ((rc = launch_reset_parts(h, RSP_STEREO, h->sB)) != FMX_OK) return rc;
   if (stereo) {
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
     a.stereo_out = o->d_stereo;
@@ -1160,6 +1216,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   // after k_rds, so that evD closes the step ----
   HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0));
   HIP_TRY(hipStreamWaitEvent(h->sD, h->evC[buf], 0));
+  if ((rc = launch_reset_parts(h, RSP_AUDIO, h->sD)) != FMX_OK) return rc;
+  h->rl_pending.clear();
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
   if ((rc = tset_advance(h, *tau, n, buf, h->sD, nullptr)) != FMX_OK) return rc;
   {

@@ -189,7 +189,8 @@ struct RsArgs {
 
 // launchers (fmx_kernels.hip); stream is a hipStream_t
 // vec: the caller guarantees every channel's decimator history is full
-// (dec_valid == L-1); 16-B row alignment is checked here.
+// (dec_valid == L-1) -- only k_frontend's VEC form needs it; k_fe8 takes cold
+// and warm channels alike; 16-B row alignment is checked here.
 // Events bound to the NEXT main-kernel launch of this thread (k_fe8 /
 // k_frontend, k_pll, k_audio, k_rs, k_rds) through hipExtLaunchKernel: `stop`
 // completes with the kernel and `start` (timing) takes its start time -- no
@@ -197,7 +198,7 @@ struct RsArgs {
 void set_launch_events(void *start, void *stop);
 int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec = false);
 // whether launch_frontend_m would run k_fe8 for these arguments
-bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec);
+bool frontend_is_fe8(const FeArgs &a, int M, int tpp);
 int launch_pll(const PllArgs &a, void *stream);
 int launch_pilot(const PilotArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
@@ -245,7 +246,24 @@ enum ResetParts {
   RS_MUTE = 512,   // retune fade/mute start; mute length in bits 16..31 (main.cpp:1034-1035)
   RS_FREQDEM = 1024 // discriminator re-created (FMDemod::setDeviation)
 };
+// the stream-local parts of a channel reset (reset_channel, fmx_kernels.hip):
+// each part's state is read / written by the kernels of one process_block
+// stream only
+enum ResetStreamPart {
+  RSP_FRONT = 1,  // sA: decimator / IQ FIR / DC / AGC / discriminator state, stereo history rows
+  RSP_STEREO = 2, // sB: FmxStereoState (k_pll)
+  RSP_RDS = 4,    // sC: FmxRdsState, mix-down ring (k_rds)
+  RSP_AUDIO = 8,  // sD: L/R FIR history, AF / mono resampler + IIRs, retune mute (k_audio)
+  RSP_ALL = 15
+};
+#define FMX_RESET_LIST 64 // channels per k_reset_list launch (a kernel argument, no upload)
+struct ResetList {
+  int n;
+  int ch[FMX_RESET_LIST];
+  int m[FMX_RESET_LIST];
+};
 int launch_reset(const ResetArgs &a, void *stream);
+int launch_reset_list(const ResetArgs &a, const ResetList &L, int parts, int st_buf, void *stream);
 int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, size_t out_stride, void *stream);
 int launch_copy16(const void *src, void *dst, size_t n16, void *stream); // 16-B words, any memory the device maps
 

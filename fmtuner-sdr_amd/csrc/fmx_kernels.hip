@@ -114,6 +114,8 @@ __device__ __forceinline__ int au_channel(int b, int C, bool tiled) {
 /* ================================================================== */
 struct FeShared {
   float carry_i, carry_q; // DC blocker v of the last processed sample
+  float carry_n[2];       // k_fe8: the same after the chunk's last sample, by its owner thread
+  float2 cold_y[32];      // k_fe8: a cold channel's first outputs, computed in f32 from the bytes
   float fd_re, fd_im;     // discriminator r_prev (last IQ FIR / AGC output)
   float wave_a[4], wave_bi[4], wave_bq[4];
   int clip;
@@ -1809,21 +1811,44 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   // its first lane at entry)
   f32x2 acc[FMX_RDS_NACC];
   for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = lead ? f32x2{G.acc_re[i], G.acc_im[i]} : f32x2{0.0f, 0.0f};
-  if (act && lead && G.rebuild) {
+  {
     // decimation phase changed by a reset: rebuild the partial sums from the
-    // last mixed samples (the reference's FIR window survives the reset)
-    for (int i = 0; i < FMX_RDS_NACC; ++i) {
-      float ar = 0.0f, ai = 0.0f;
-      for (int kp = FMX_RDS_FIR - 1 - 24 * i; kp >= 1; --kp) {
-        const uint32_t idx = (G.ring_pos - (uint32_t)kp) & (FMX_RDS_RING - 1);
-        const float h = D->rds_fir[24 * i + kp];
-        const float pr = h * ring[2 * idx];
-        const float pi = h * ring[2 * idx + 1];
-        ar = ar + pr;
-        ai = ai + pi;
+    // last mixed samples (the reference's FIR window survives the reset).
+    // Round 5: the whole wave computes each such channel's 11 sums (terms
+    // strided over the 64 lanes, a shuffle tree) -- round 4's serial loop in
+    // the channel's first lane, ~2 800 dependent ring loads, held the wave's
+    // other seven channels ~80 us at every retune
+    // (the sums go through the input ring's LDS, free until the first
+    // moves below: a dynamically indexed acc[] would live in scratch)
+    static_assert(RDS_CPW * FMX_RDS_NACC * 2 <= RDS_NR * 3 * 64, "rebuild sums fit the input ring");
+    f32x2 *rb = reinterpret_cast<f32x2 *>(&L.xin[0][0][0]);
+    const bool mine = act && lead && G.rebuild;
+    uint64_t need = __ballot(mine);
+    while (need) {
+      const int src = __ffsll((unsigned long long)need) - 1;
+      need &= need - 1;
+      const uint32_t rp = (uint32_t)__shfl((int)G.ring_pos, src);
+      const float *rg = a.ring + (size_t)(c0 + src / RDS_LPC) * FMX_RDS_RING * 2;
+      for (int i = 0; i < FMX_RDS_NACC; ++i) {
+        float ar = 0.0f, ai = 0.0f;
+        for (int kp = FMX_RDS_FIR - 1 - 24 * i - lane; kp >= 1; kp -= 64) {
+          const uint32_t idx = (rp - (uint32_t)kp) & (FMX_RDS_RING - 1);
+          const float h = D->rds_fir[24 * i + kp];
+          const float pr = h * rg[2 * idx];
+          const float pi = h * rg[2 * idx + 1];
+          ar = ar + pr;
+          ai = ai + pi;
+        }
+        for (int d = 32; d >= 1; d >>= 1) { // scalar adds as asm: never packed beside the shuffles' LDS returns
+          const float tr = __shfl_xor(ar, d), ti = __shfl_xor(ai, d);
+          asm("v_add_f32 %0, %0, %2\n\tv_add_f32 %1, %1, %3" : "+v"(ar), "+v"(ai) : "v"(tr), "v"(ti));
+        }
+        if (lane == src) rb[(src / RDS_LPC) * FMX_RDS_NACC + i] = f32x2{ar, ai};
       }
-      acc[i] = f32x2{ar, ai};
     }
+    if (mine)
+#pragma unroll
+      for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = rb[g * FMX_RDS_NACC + i];
   }
   float agc_g = G.agc_g, agc_y2p = G.agc_y2p;
   float ss_rate = G.ss_rate, ss_del = G.ss_del, ss_tau = G.ss_tau, ss_q_hat = G.ss_q_hat, ss_v1 = G.ss_v1;
@@ -2107,68 +2132,51 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
 /* ================================================================== */
 /* state reset / construction                                          */
 /* ================================================================== */
-__global__ void k_reset(ResetArgs a) {
-  const int c = blockIdx.x;
+// One channel's reset, the parts selected by `parts` (ResetStreamPart): each
+// part touches only state that the kernels of ONE stream of process_block
+// read or write, so process_block runs it on that stream right before that
+// stream's kernel of the step (no cross-stream join, round 5); st_buf: the
+// stereo history buffer the step reads (-1: all of them, the joined path).
+__device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int st_buf) {
   const int tid = threadIdx.x;
-  const int m = a.mask[c];
-  if (m == 0) return;
   const FmxDesign *D = a.des;
   const bool create = m & RS_CREATE;
-  if (create || (m & RS_DECIM)) {
-    if (tid == 0) a.dec_valid[c] = 0;
-  }
-  if (create || (m & (RS_DEMOD | RS_IQFIR))) {
-    for (int h = tid; h < FMX_IQ_MAXLEN - 1; h += blockDim.x)
-      a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{0.0f, 0.0f};
-  }
-  if (m & RS_FREQDEM) { // freqdem re-created (setDeviation): r_prev = 0
-    if (tid == 0) {
+  if (parts & RSP_FRONT) { // sA: k_fe8 / k_frontend / k_pilot state
+    if (create || (m & RS_DECIM)) {
+      if (tid == 0) a.dec_valid[c] = 0;
+    }
+    if (create || (m & (RS_DEMOD | RS_IQFIR))) {
+      for (int h = tid; h < FMX_IQ_MAXLEN - 1; h += blockDim.x)
+        a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h] = float2_t{0.0f, 0.0f};
+    }
+    if (tid == 0 && (create || (m & (RS_FREQDEM | RS_DEMOD)))) { // freqdem re-created / reset: r_prev = 0
       a.fd_prev[2 * c] = 0.0f;
       a.fd_prev[2 * c + 1] = 0.0f;
     }
-  }
-  if (create || (m & RS_DEMOD)) {
-    if (tid == 0) {
+    if (tid == 0 && (create || (m & RS_DEMOD))) {
       a.dc_v[2 * c] = 0.0f;
       a.dc_v[2 * c + 1] = 0.0f;
-      a.fd_prev[2 * c] = 0.0f;
-      a.fd_prev[2 * c + 1] = 0.0f;
-      a.mono_iir[2 * c] = 0.0f;
-      a.mono_iir[2 * c + 1] = 0.0f;
     }
-    for (int h = tid; h < 32; h += blockDim.x) a.mono_win[(size_t)c * 32 + h] = 0.0f;
-  }
-  if (create || (m & RS_AGC)) {
-    if (tid == 0) {
+    if (tid == 0 && (create || (m & RS_AGC))) {
       a.agc[2 * c] = 1.0f;
       a.agc[2 * c + 1] = 1.0f;
     }
-  }
-  if (create || (m & RS_STEREO)) {
-    for (int h = tid; h < FMX_HIST; h += blockDim.x)
-      for (int k = 0; k < FMX_ST_BUFS; ++k) a.st_hist[((size_t)k * a.C + c) * FMX_HIST + h] = 0.0f;
-    for (int h = tid; h < 2 * (FMX_LR_LEN - 1); h += blockDim.x)
-      a.lr_hist[(size_t)c * 2 * (FMX_LR_LEN - 1) + h] = 0.0f;
-    if (tid == 0) {
-      FmxStereoState s{};
-      s.theta = 0;
-      s.dtheta = D->pll_dtheta0;
-      s.pll_freq = D->nominal;
-      a.st[c] = s;
+    if (create || (m & RS_STEREO)) { // the pilot BPF window / delay line (the previous call's MPX rows)
+      for (int h = tid; h < FMX_HIST; h += blockDim.x)
+        for (int k = 0; k < FMX_ST_BUFS; ++k)
+          if (st_buf < 0 || k == st_buf) a.st_hist[((size_t)k * a.C + c) * FMX_HIST + h] = 0.0f;
     }
+    if (create) // the RDS resampler's window (k_fe8 hands it on): a new object only, as the reference
+      for (int h = tid; h < 32; h += blockDim.x) a.rds_hist[(size_t)c * 32 + h] = 0.0f;
   }
-  if (create || (m & RS_AF)) {
-    for (int h = tid; h < 64; h += blockDim.x) a.af_win[(size_t)c * 64 + h] = 0.0f;
-    if (tid < 4) a.af_iir[(size_t)c * 4 + tid] = 0.0f;
+  if ((parts & RSP_STEREO) && tid == 0 && (create || (m & RS_STEREO))) { // sB: k_pll
+    FmxStereoState s{};
+    s.theta = 0;
+    s.dtheta = D->pll_dtheta0;
+    s.pll_freq = D->nominal;
+    a.st[c] = s;
   }
-  if (m & RS_DEEMPH) {
-    if (tid == 0) {
-      a.af_iir[(size_t)c * 4 + 0] = 0.0f;
-      a.af_iir[(size_t)c * 4 + 1] = 0.0f;
-      a.mono_iir[2 * c] = 0.0f;
-    }
-  }
-  if (create || (m & RS_RDS)) {
+  if ((parts & RSP_RDS) && (create || (m & RS_RDS))) { // sC: k_rds
     if (tid == 0) {
       FmxRdsState s;
       if (create) {
@@ -2217,17 +2225,47 @@ __global__ void k_reset(ResetArgs a) {
       s.bs_bits_since_lost = 0;
       a.rds[c] = s;
     }
-    if (create) {
+    if (create)
       for (int h = tid; h < 2 * FMX_RDS_RING; h += blockDim.x) a.ring[(size_t)c * 2 * FMX_RDS_RING + h] = 0.0f;
-      for (int h = tid; h < 32; h += blockDim.x) a.rds_hist[(size_t)c * 32 + h] = 0.0f;
+  }
+  if (parts & RSP_AUDIO) { // sD: k_audio (L/R FIRs, AF post, mono chain, retune mute)
+    if (create || (m & RS_STEREO))
+      for (int h = tid; h < 2 * (FMX_LR_LEN - 1); h += blockDim.x) a.lr_hist[(size_t)c * 2 * (FMX_LR_LEN - 1) + h] = 0.0f;
+    if (create || (m & RS_DEMOD)) {
+      if (tid == 0) {
+        a.mono_iir[2 * c] = 0.0f;
+        a.mono_iir[2 * c + 1] = 0.0f;
+      }
+      for (int h = tid; h < 32; h += blockDim.x) a.mono_win[(size_t)c * 32 + h] = 0.0f;
+    }
+    if (create || (m & RS_AF)) {
+      for (int h = tid; h < 64; h += blockDim.x) a.af_win[(size_t)c * 64 + h] = 0.0f;
+      if (tid < 4) a.af_iir[(size_t)c * 4 + tid] = 0.0f;
+    }
+    if (tid == 0 && (m & RS_DEEMPH)) {
+      a.af_iir[(size_t)c * 4 + 0] = 0.0f;
+      a.af_iir[(size_t)c * 4 + 1] = 0.0f;
+      a.mono_iir[2 * c] = 0.0f;
+    }
+    // retune fade/mute (main.cpp:1034-1035): remaining = total = mute length
+    if (tid == 0 && (create || (m & RS_MUTE))) {
+      const int len = (m & RS_MUTE) ? (int)((uint32_t)m >> 16) : 0;
+      a.mute[2 * c] = len;
+      a.mute[2 * c + 1] = len;
     }
   }
-  // retune fade/mute (main.cpp:1034-1035): remaining = total = mute length
-  if (tid == 0 && (create || (m & RS_MUTE))) {
-    const int len = (m & RS_MUTE) ? (int)((uint32_t)m >> 16) : 0;
-    a.mute[2 * c] = len;
-    a.mute[2 * c + 1] = len;
-  }
+}
+// every part of every channel with a nonzero mask (the joined path: creation,
+// stage entry points, resets of many channels at once)
+__global__ void k_reset(ResetArgs a) {
+  const int c = blockIdx.x;
+  const int m = a.mask[c];
+  if (m != 0) reset_channel(a, c, m, RSP_ALL, -1);
+}
+// the listed channels, one part (process_block: on that part's stream)
+__global__ void k_reset_list(ResetArgs a, ResetList L, int parts, int st_buf) {
+  const int i = blockIdx.x;
+  if (i < L.n) reset_channel(a, L.ch[i], L.m[i], parts, st_buf);
 }
 
 /* ComplexDecimator::execute's requantisation (liquid_primitives.cpp:448-452):
@@ -2282,6 +2320,7 @@ __global__ void k_synth(fmx_synth_config cfg, uint32_t ch0, int n_ch, int64_t sa
  * ~58 KB of LDS per workgroup: two workgroups (8 waves) per CU leave room
  * for a k_pll or k_rds workgroup beside them. */
 #define FE8_T 2048
+#define FE8_MIN_N 1024 // config.cpp:240 clamps dsp_block_samples to 1024..32768
 #ifndef FMX_DEC_UNROLL
 #define FMX_DEC_UNROLL 1
 #endif
@@ -2363,12 +2402,16 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
 __device__ __forceinline__ int fir8_len(int P) { return ((P + 6) & ~7) + 1; }
 // register budget: two workgroups (8 waves) per CU beside a k_pll / k_rds /
 // k_rs wave -- <= 168 VGPRs (3 waves per SIMD); M = 8 (the reference's
-// 2.048 MS/s rate) keeps its longer decimator window at 2
+// 2.048 MS/s rate) keeps its longer decimator window at 2, and so does the
+// RS = true instance (the resampler and the pilot BPF inside: stage entry
+// points and RDS steps past k_rs's window, never process_block at 240 / 256
+// kHz), which with round 5's per-channel cold start and any-n chunks no
+// longer fits 168 without scratch
 template <int M, int TPP, bool RS>
 #ifndef FMX_FE_PRIO
 #define FMX_FE_PRIO 0 // k_fe8's wave priority (s_setprio) beside the other streams' waves
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 : 3))) void k_fe8(FeArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || RS) ? 2 : 3))) void k_fe8(FeArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   using LY = Fe8Layout<M, TPP, RS>;
   if (FMX_FE_PRIO > 0) __builtin_amdgcn_s_setprio(FMX_FE_PRIO);
@@ -2521,29 +2564,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       rsb[pr][m] = f32x2{h0, h1};
     }
   }
+  // Chunks (round 5): ceil(n / FE8_T) chunks of one size cs (a multiple of 8,
+  // <= FE8_T; the last one takes the rest), so any call of n >= FE8_MIN_N
+  // (the reference's dsp_block_samples clamp, 1024) has every chunk >= 904
+  // samples: the histories the call hands on (IQ FIR 120, stereo rows 512,
+  // RDS window 32) always lie inside its last chunk.
+  const int nch = (n + FE8_T - 1) / FE8_T;
+  const int cs = (((n + nch - 1) / nch) + 7) & ~7;
+  // per-channel decimator warmth (round 5): after a reset the reference's
+  // window holds complex zeros (ComplexDecimator::reset re-creates the
+  // firdecim_crcf, liquid_primitives.cpp:405-420); the coldk oldest history
+  // positions of this channel are such zeros (below: bytes 128 in the MFMA,
+  // and the 0.5 * taps of the 127.5 centre taken back out of the outputs that
+  // reach them).  Read where it is used (first chunk only): SGPRs are scarce.
+  auto cold_k = [&]() __attribute__((always_inline)) { return (L - 1) - min(max(a.dec_valid[c], 0), L - 1); };
   dma_chunk(0, PAll0{}, PAll{});
   int e_pos = 0;
 
-  for (int n0 = 0; n0 < n; n0 += FE8_T) {
+  for (int n0 = 0; n0 < n; n0 += cs) {
+    const int cnt = min(cs, n - n0); // samples of this chunk (a multiple of 4)
     if (rs && tid == 0) sh->e_end = e_pos;
     // ================= decimator =================
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
     FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
-    if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (full history)
+    if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (cold ones: byte 128, i.e. b - 128 = 0)
+      const int coldk = cold_k();
       for (int h = tid; h < L; h += 256) {
         const int hh = h - 1;
         uint16_t v = 0;
-        if (hh >= 0) v = (uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8);
+        if (hh >= 0) v = hh < coldk ? (uint16_t)0x8080u : (uint16_t)((uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8));
         reinterpret_cast<uint16_t *>(raw)[h] = v;
       }
       __syncthreads();
+      if (coldk > 0 && tid < (coldk + M - 1) / M) {
+        // the outputs whose window reaches the zeroed positions, in f32 from
+        // the bytes (the window's real samples only, oldest first, as the
+        // reference's zeroed firdecim window): the MFMA form's 127.5 centre
+        // (dec_dc16) is exact only up to its f32 rounding, which these small
+        // outputs (the window's taper over a few real samples) feel
+        // relatively at weak carriers.  Staged in sh->cold_y, they replace
+        // the MFMA outputs at the staging step.
+        float sI = 0.0f, sQ = 0.0f;
+        for (int d = L; d >= 1; --d) {
+          const int t = M * tid + d; // raw position: 1 .. L-1 history, L.. the call
+          if (t <= coldk) continue;
+          const float h = D->dec_taps[L - d];
+          sI = sI + h * ((float)raw[2 * t] - 127.5f);
+          sQ = sQ + h * ((float)raw[2 * t + 1] - 127.5f);
+        }
+        sh->cold_y[tid] = make_float2(sI * D->dec_scale, sQ * D->dec_scale);
+      }
     }
     if (want_sig) {
 #pragma unroll
       for (int j = 0; j < LY::NPF; ++j) {
         const int off = 16 * (tid + 256 * j);
-        if (off >= LY::HB && off < LY::HB + 2 * FE8_T * M) {
+        if (off >= LY::HB && off < LY::HB + 2 * cnt * M) {
           const u32x4 w = *reinterpret_cast<const u32x4 *>(raw + off);
           sig.word4(w);
         }
@@ -2623,6 +2700,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
         }
       }
       __syncthreads();
+      const int coldk = n0 == 0 ? cold_k() : 0;
+      if (coldk > 0) { // workgroup-uniform: a cold channel's first chunk (values from the halo step)
+        if (tid < (coldk + M - 1) / M) stg[fe8_stg(tid)] = sh->cold_y[tid];
+        __syncthreads();
+      }
       int myclip = 0;
 #pragma unroll
       for (int r = 0; r < 8; r += 2) {
@@ -2632,7 +2714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       }
 #pragma unroll
       for (int r = 0; r < 8; ++r)
-        if (fabsf(xv[r].x) >= 0.995f || fabsf(xv[r].y) >= 0.995f) myclip++;
+        if (j0 + r < cnt && (fabsf(xv[r].x) >= 0.995f || fabsf(xv[r].y) >= 0.995f)) myclip++;
       if (myclip) atomicAdd(&sh->clip, myclip);
     }
     __syncthreads(); // raw is dead: xin / yb alias it from here on
@@ -2682,6 +2764,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       vQ = eA * vQ + eQ;
       // the state before this thread's first element, then the reference's op order
       f16x8_t ih, il, qh, ql;
+      const int rlast = (tid == (cnt - 1) >> 3) ? ((cnt - 1) & 7) : -1; // the chunk's last sample
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const float tI = dc_a1 * vI, tQ = dc_a1 * vQ;
@@ -2693,18 +2776,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
         qh[r] = (_Float16)sQ;
         ql[r] = (_Float16)(sQ - (float)qh[r]);
         // the next chunk's IQ FIR history (f32; read above before the scan's barrier)
-        if (j0 + r >= FE8_T - FE_HALO_IQ) hx[j0 + r - (FE8_T - FE_HALO_IQ)] = make_float2(oI, oQ);
+        if (j0 + r >= cnt - FE_HALO_IQ && j0 + r < cnt) hx[j0 + r - (cnt - FE_HALO_IQ)] = make_float2(oI, oQ);
         vI = nI;
         vQ = nQ;
+        if (r == rlast) {
+          sh->carry_n[0] = nI;
+          sh->carry_n[1] = nQ;
+        }
       }
       *reinterpret_cast<f16x8_t *>(xih + FE_HALO_IQ + j0) = ih;
       *reinterpret_cast<f16x8_t *>(xil + FE_HALO_IQ + j0) = il;
       *reinterpret_cast<f16x8_t *>(xqh + FE_HALO_IQ + j0) = qh;
       *reinterpret_cast<f16x8_t *>(xql + FE_HALO_IQ + j0) = ql;
       __syncthreads();
-      if (tid == 255) {
-        sh->carry_i = vI;
-        sh->carry_q = vQ;
+      if (tid == 0) {
+        sh->carry_i = sh->carry_n[0];
+        sh->carry_q = sh->carry_n[1];
       }
     }
     __syncthreads();
@@ -2764,7 +2851,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     // ================= AGC (serial, only when enabled) =================
     if (par.agc != 0) {
       if (tid == 0) {
-        for (int j = 0; j < FE8_T; ++j) {
+        for (int j = 0; j < cnt; ++j) {
           const float2 x = yb[1 + j];
           const float yr = x.x * agc_g, yi = x.y * agc_g;
           const float y2 = yr * yr + yi * yi;
@@ -2795,11 +2882,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
           xh[FMX_HIST + j] = hv;
           xl[FMX_HIST + j] = (_Float16)(m - (float)hv);
         }
-        if (a.mpx_out) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
+        if (a.mpx_out && j < cnt) a.mpx_out[(size_t)c * a.mpx_stride + n0 + j] = m;
       }
       if (tid == 0) {
-        sh->fd_re = yb[FE8_T].x;
-        sh->fd_im = yb[FE8_T].y;
+        sh->fd_re = yb[cnt].x;
+        sh->fd_im = yb[cnt].y;
       }
     }
     __syncthreads(); // xin / yb are dead: the next chunk may land in raw (below uc)
@@ -2813,8 +2900,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
         en[k] = (e < sched_n) ? sched[e] : FmxSched{0xFFFF, 0.0f};
       }
     }
-    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PAll0{}, PEarly{});
-    const bool last_chunk = n0 + FE8_T >= n;
+    if (n0 + cnt < n) dma_chunk(n0 + cnt, PAll0{}, PEarly{});
+    const bool last_chunk = n0 + cnt >= n;
     if (rds || hist_out) { // unpadded f32 copy: the RDS resampler's input (its own window history first), the history rows
 #pragma unroll
       for (int k = 0; k < 8; ++k) uc[32 + tid + 256 * k] = mv[k];
@@ -2822,7 +2909,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     if (rs) {
       if (tid < 32) {
         uc[tid] = (n0 == 0) ? rds_keep : tl32[tid];
-        uc[32 + FE8_T + tid] = 0.0f;
+        uc[32 + cnt + tid] = 0.0f;
       }
     }
     FE_STAMP(3)
@@ -2833,7 +2920,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int e = e_pos + tid + 256 * k;
-        if (e < sched_n && (en[k].packed & 0xFFFF) < n0 + FE8_T) {
+        if (e < sched_n && (en[k].packed & 0xFFFF) < n0 + cnt) {
           const int i = (en[k].packed & 0xFFFF) - n0;
           const int b = (en[k].packed >> 16) & 0xFF;
           const bool boundary = (en[k].packed >> 24) & 1;
@@ -2879,16 +2966,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       if (hist_out) {
         static_assert(FMX_HIST == 512, "two history words per thread");
         const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.st_hist_wr + (size_t)c * FMX_HIST, FMX_HIST * 4);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + FE8_T - FMX_HIST + tid]), rh,
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + cnt - FMX_HIST + tid]), rh,
                                               4u * tid, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + FE8_T - 256 + tid]), rh,
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, uc[32 + cnt - 256 + tid]), rh,
                                               4u * tid, 1024, 0);
       }
-      if (rds && tid < 32) a.rds_hist[(size_t)c * 32 + tid] = uc[FE8_T + tid];
+      if (rds && tid < 32) a.rds_hist[(size_t)c * 32 + tid] = uc[cnt + tid];
     }
-    if (rs && tid < 32) tl32[tid] = uc[FE8_T + tid];
+    if (rs && tid < 32) tl32[tid] = uc[cnt + tid];
     __syncthreads(); // uc is dead: the rest of the next chunk may land (behind the pilot FIR)
-    if (n0 + FE8_T < n) dma_chunk(n0 + FE8_T, PEarly{}, PAll{});
+    if (n0 + cnt < n) dma_chunk(n0 + cnt, PEarly{}, PAll{});
     if (rs) e_pos = sh->e_end;
     FE_STAMP(5)
     // ================= 19 kHz pilot band-pass =================
@@ -2908,6 +2995,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       const f16x8_t *bh = reinterpret_cast<const f16x8_t *>(xh + xb);
       const f16x8_t *bl = reinterpret_cast<const f16x8_t *>(xl + xb);
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->pilot_frag[0][0][0][0]) + lane;
+      const __amdgpu_buffer_rsrc_t prow = make_rsrc(a.pilot_out + (size_t)c * a.pilot_stride, 4u * (uint32_t)n);
       f32x4_t pacc[2];
       pacc[0] = pacc[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
       u32x4 ah = fa[0], al = fa[64];
@@ -2928,10 +3016,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       constexpr float kInv = 1.0f / 4096.0f;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3
-        float4 *po = reinterpret_cast<float4 *>(a.pilot_out + (size_t)c * a.pilot_stride + n0 + 256 * (2 * wave + u) +
-                                                16 * col + 4 * g);
-        *po = make_float4(pacc[u][0] * kInv, pacc[u][1] * kInv, pacc[u][2] * kInv, pacc[u][3] * kInv);
+        // lane: outputs 256 (2 wave + u) + 16 col + 4 g + i, i = 0..3, as a
+        // buffer store over the call's row: outputs past n (a shorter last
+        // chunk; cnt is a multiple of 4) are dropped by the range check, no branch
+        const int o = n0 + 256 * (2 * wave + u) + 16 * col + 4 * g;
+        const u32x4 pv = u32x4{__builtin_bit_cast(uint32_t, pacc[u][0] * kInv), __builtin_bit_cast(uint32_t, pacc[u][1] * kInv),
+                               __builtin_bit_cast(uint32_t, pacc[u][2] * kInv), __builtin_bit_cast(uint32_t, pacc[u][3] * kInv)};
+        __builtin_amdgcn_raw_buffer_store_b128(pv, prow, 4u * (uint32_t)o, 0, 0);
       }
     }
     FE_STAMP(4)
@@ -2941,8 +3032,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
     if (RS) {
       // the chunk's last FMX_HIST samples become the f16 images' history
       static_assert(FMX_HIST == 2 * 256, "one f16 pair per thread");
-      const uint32_t ch = reinterpret_cast<const uint32_t *>(xh)[FE8_T / 2 + tid];
-      const uint32_t cl = reinterpret_cast<const uint32_t *>(xl)[FE8_T / 2 + tid];
+      const uint32_t ch = reinterpret_cast<const uint32_t *>(xh)[cnt / 2 + tid];
+      const uint32_t cl = reinterpret_cast<const uint32_t *>(xl)[cnt / 2 + tid];
       __syncthreads();
       reinterpret_cast<uint32_t *>(xh)[tid] = ch;
       reinterpret_cast<uint32_t *>(xl)[tid] = cl;
@@ -2964,7 +3055,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M == 8 ? 2 
       dh[2 * h] = (uint8_t)(v & 255);
       dh[2 * h + 1] = (uint8_t)(v >> 8);
     }
-    if (tid == 0) a.dec_valid[c] = L - 1;
+    if (tid == 0) a.dec_valid[c] = L - 1; // n M >= 1024 M > L - 1 new samples
   }
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
     const float2 v = hx[h];
@@ -3055,21 +3146,23 @@ namespace fmx {
 // steady state: whole 2048-sample chunks, full history, no complex
 // decimator output, 16-B pilot rows, RDS rate ratio < 0.9 (<= 8 resampler
 // outputs per thread and chunk) -> k_fe8
-static bool fe8_ok(const FeArgs &a, int M, bool vec) {
+// k_fe8 takes any call of n >= FE8_MIN_N samples (chunks of one size, see
+// k_fe8) on 16-B aligned IQ rows, cold or warm decimator history per channel
+static bool fe8_ok(const FeArgs &a, int M) {
   if (a.in_mode != FE_IN_U8_DECIM) return false;
-  vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
-  return vec && a.n > 0 && a.n % FE8_T == 0 && a.do_demod && !a.bb_out &&
+  const bool aligned = ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
+  return aligned && a.n >= FE8_MIN_N && a.do_demod && !a.bb_out &&
          (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
          a.des_fs >= 190000;
 }
-bool frontend_is_fe8(const FeArgs &a, int M, int tpp, bool vec) {
-  return fe8_ok(a, M, vec) && ((M == 10 && tpp == 28) || (M == 8 && tpp == 28) || (M == 4 && tpp == 20) ||
+bool frontend_is_fe8(const FeArgs &a, int M, int tpp) {
+  return fe8_ok(a, M) && ((M == 10 && tpp == 28) || (M == 8 && tpp == 28) || (M == 4 && tpp == 20) ||
                                (M == 2 && tpp == 12));
 }
 int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (a.in_mode != FE_IN_U8_DECIM) return fe_launch<1, 1, false>(a, st);
-  const bool fe8 = fe8_ok(a, M, vec);
+  const bool fe8 = fe8_ok(a, M);
   vec = vec && ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
   if (fe8) {
     if (M == 10 && tpp == 28) return fe8_launch<10, 28>(a, st);
@@ -3428,6 +3521,11 @@ int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, 
 }
 int launch_reset(const ResetArgs &a, void *stream) {
   hipLaunchKernelGGL(k_reset, dim3(a.C), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+int launch_reset_list(const ResetArgs &a, const ResetList &L, int parts, int st_buf, void *stream) {
+  if (L.n <= 0) return FMX_OK;
+  hipLaunchKernelGGL(k_reset_list, dim3(L.n), dim3(256), 0, static_cast<hipStream_t>(stream), a, L, parts, st_buf);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-/* ABI history: 7 (round 5) adds fmx_host_stats; 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+/* ABI history: 7 (round 5) adds fmx_host_stats and FMX_K_FRONTEND_GENERIC (FMX_K_COUNT 7); 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
  * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
  * which changed that struct's size: callers must be rebuilt against this
  * header. */
@@ -217,7 +217,10 @@ enum {
                          kernel (k_rs, on the RDS stream ahead of k_rds)                        */
   FMX_K_PILOT = 5,    /* the 19 kHz pilot BPF when process_block runs it as its own kernel
                          (k_pilot, on the front-end stream after k_fe8)                         */
-  FMX_K_COUNT = 6
+  FMX_K_FRONTEND_GENERIC = 6, /* process_block's front end when it runs as the generic k_frontend
+                         (calls of n < 1024 samples, unaligned IQ rows) instead of k_fe8;
+                         FMX_K_FRONTEND then counts k_fe8 launches only                           */
+  FMX_K_COUNT = 7
 };
 /* enable: 0 off, 1 every step's launches, N > 1 the launches of every N-th
  * step only (a sample: fewer event packets on the streams in the timed region) */

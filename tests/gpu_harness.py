@@ -4,10 +4,12 @@ block and returns both outputs."""
 import numpy as np
 
 
-def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None, retunes=None):
+def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None, retunes=None, ktimes=None):
     """iq: uint8 [C][nblk * 2*B*M]. Returns per-block lists of numpy outputs.
     resets {block: channel}, retunes {block: (channel, mute_samples)},
-    params {block: [(key, value, channel)]} are applied before that block."""
+    params {block: [(key, value, channel)]} are applied before that block.
+    ktimes (a dict): filled with fmx_kernel_times ({kernel: (ms, launches)})
+    of the whole run."""
     C = iq.shape[0]
     B = cfg.block
     M = cfg.iq_rate // cfg.dsp_rate
@@ -31,6 +33,8 @@ def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None
                        gcnt.data_ptr(), None, ind.data_ptr())
     res = []
     row = iq.shape[1]
+    if ktimes is not None:
+        h.timing_enable(True)
     for b in range(nblk):
         if resets and b in resets:
             h.reset(resets[b])
@@ -57,6 +61,8 @@ def run_gpu_pipeline(fmx, torch, cfg, iq, nblk, n=None, resets=None, params=None
                         stereo=st.cpu().numpy().copy(), pilot=pil.cpu().numpy().copy(),
                         clip=clip.cpu().numpy().copy(), indicator=ind.cpu().numpy().copy(),
                         groups=groups))
+    if ktimes is not None:
+        ktimes.update(h.kernel_times())
     h.close()
     return res
 
@@ -141,7 +147,8 @@ def _groups_of(grp_rows, gcnt_rows, GS):
     return out
 
 
-def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=False, warmup=5, all_groups=None):
+def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=False, warmup=5, all_groups=None,
+                      retunes=None):
     """The bench's timed mode (bench.py step()): every block through
     fmx_process_block back to back, NO host synchronisation between blocks,
     kernel timing switched on after `warmup` blocks as the bench does, the
@@ -153,7 +160,9 @@ def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=Fals
     indexed by position in keep, host IQ rows of keep, transmitted groups of
     keep, per-block stereo fraction over all C channels).  all_groups: a list
     that receives every channel's decoded groups over all blocks (full-size
-    property checks)."""
+    property checks).  retunes {block: [(channel, mute_samples), ...]}:
+    fmx_retune calls queued before that block's fmx_process_block (no
+    synchronisation, as a live receiver retunes)."""
     B = cfg.block
     M = cfg.iq_rate // cfg.dsp_rate
     n_iq = B * M
@@ -179,6 +188,8 @@ def run_gpu_pipelined(fmx, torch, cfg, C, scfg, nblk, keep, ch0=0, with_mpx=Fals
     for b in range(nblk):
         if b == warmup:
             h.timing_enable(True)
+        for (ch, mute) in (retunes or {}).get(b, []):
+            h.retune(ch, mute)
         out = fmx.BlockOut(mpx[b].data_ptr() if with_mpx else None, B if with_mpx else 0,
                            pl[b].data_ptr(), pr[b].data_ptr(), B, ints[0, b].data_ptr(), ints[1, b].data_ptr(),
                            ints[2, b].data_ptr(), clip[b].data_ptr(), grp[b].data_ptr(), GS, ints[3, b].data_ptr(),

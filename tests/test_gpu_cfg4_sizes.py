@@ -29,7 +29,7 @@ def _run(fmx, oracle, torch, C, keep, all_groups=None):
     scfg = fmx.make_synth(kind=2, n_bits=8192)
     g, iq_keep, tx, stereo_all, kt = H.run_gpu_pipelined(fmx, torch, cfg, C, scfg, NBLK, keep,
                                                          all_groups=all_groups)
-    assert all(v[1] == NBLK - 5 for v in kt.values()), kt
+    assert all(v[1] == NBLK - 5 for k, v in kt.items() if k != "frontend_generic") and kt["frontend_generic"][1] == 0, kt
     ngroups = 0
     for j, c in enumerate(keep):
         o = H.run_oracle_pipeline(oracle, oracle.make_cfg(), iq_keep[j], NBLK)

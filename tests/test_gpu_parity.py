@@ -88,9 +88,11 @@ def check(g, o, c, nblk, tag="", pilot_tol=0, pcm_blocks=None, gc=None, narrow=F
     return st
 
 
-def run_both(fmx, oracle, torch, cfgkw, iq, nblk, n=None, resets=None, params=None, per_channel_resets=None):
+def run_both(fmx, oracle, torch, cfgkw, iq, nblk, n=None, resets=None, params=None, per_channel_resets=None,
+             ktimes=None):
     C = iq.shape[0]
-    g = H.run_gpu_pipeline(fmx, torch, fmx.make_config(**cfgkw), iq, nblk, n=n, resets=resets, params=params)
+    g = H.run_gpu_pipeline(fmx, torch, fmx.make_config(**cfgkw), iq, nblk, n=n, resets=resets, params=params,
+                           ktimes=ktimes)
     outs = []
     for c in range(C):
         rs = None
@@ -539,3 +541,21 @@ def test_graft_smoke(torch_cuda):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+def test_rds_resampler_inside_the_front_end_with_k_pilot(fmx, oracle, torch_cuda):
+    """The process_block combination the Cfg runs never take: an
+    RDS resampling step past k_rs's 64-sample tile window (rds_del > 2.1, here
+    a 384 kHz DSP rate: 2.25) keeps the resampler inside k_fe8 (its RS=true
+    instance) while the pilot BPF still runs as k_pilot -- k_fe8 then writes
+    no pilot and the stereo history rows k_pilot starts from.  MPX, pilot
+    level, PCM and RDS groups against the oracle at the full bars."""
+    C, nblk = 4, 10
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=3_072_000, M=8)
+    kw = dict(iq_rate=3_072_000, dsp_rate=384_000)
+    kt = {}
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk, ktimes=kt)
+    assert kt["rs"][1] == 0, kt          # no k_rs launch: the resampler ran inside k_fe8
+    assert kt["pilot"][1] >= nblk - 1, kt  # the pilot BPF as k_pilot (every block on k_fe8)
+    for c in range(C):
+        check(g, outs[c], c, nblk, tag="fe8_rs_with_k_pilot")

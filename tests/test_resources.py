@@ -58,7 +58,9 @@ def test_front_end_register_budget(tmp_path):
     ks = _kernels(tmp_path)
     for name, f in _find(ks, r"k_fe8ILi10ELi28").items():
         regs = f.get("vgpr_count", 0) + f.get("agpr_count", 0)
-        assert regs <= 168, (name, f)
+        # process_block's instance (RS = false, "Lb0"): 3 waves per SIMD; the
+        # RS = true instance (stage calls, RDS steps past k_rs): 2
+        assert regs <= (168 if "Lb0" in name else 256), (name, f)
         assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
 
 
