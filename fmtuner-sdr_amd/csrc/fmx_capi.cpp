@@ -346,7 +346,11 @@ static int tset_alloc_slots(Handle *h, TimingSet &t) {
   }
   return FMX_OK;
 }
-static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
+// cap: timing groups the slots hold before a reallocation (which synchronises
+// the device): the AF / mono sets take a group per distinct post-reset
+// timing state -- a live receiver's retunes leave a bounded number of them
+// (the 240k -> 32k phase repeats every 15 blocks of 4096) -- the RDS set one
+static int tset_init(Handle *h, TimingSet &t, float del, int max_in, int cap) {
   t.del = del;
   ResampTiming r;
   timing_reset(r);
@@ -354,7 +358,7 @@ static int tset_init(Handle *h, TimingSet &t, float del, int max_in) {
   t.groups.assign(1, r);
   t.chan_group.assign(static_cast<size_t>(h->C), 0);
   t.stride = static_cast<int>(std::ceil(static_cast<double>(max_in) / std::max(0.5, (double)del))) + 8;
-  t.cap_groups = 4;
+  t.cap_groups = std::max(1, std::min(cap, h->C));
   return tset_alloc_slots(h, t);
 }
 // channel c's resampler was reset (liquid resamp_reset): move it to a group
@@ -624,8 +628,10 @@ static int launch_reset_parts(Handle *h, int part, hipStream_t s) {
 // before that stream's kernel of this step -- after the previous step's
 // kernel of the same stream, before this step's.  A reset of a handle's
 // every channel, object creation, or more channels than the lists hold take
-// the joined path (prepare).  A retune per block at 4096 channels: 1.01 ->
-// see profiles/r05*_ab_retune* (round 4's join drained the pipeline).
+// the joined path (prepare).  One retune per block at 4096 channels costs
+// nothing measurable: 0.638 against 0.640 ms per step (profiles/
+// r05h_retune_ab.txt); with round 4's join (and the handle on k_frontend)
+// 1.01 ms (r05d), with the join alone 0.82 (r05e).
 #define FMX_RESET_LISTS_MAX 4
 static int prepare_pipelined(Handle *h) {
   int rc = sync_params(h);
@@ -880,9 +886,9 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     if ((rc = dalloc(h, &h->lraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rraw[b], ((C + 7) & ~static_cast<size_t>(7)) * B)) != FMX_OK) return rc;
   }
-  if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block)) != FMX_OK) return rc;
-  if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
-  if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_rds, h->hdes->rds_del, cfg->block, 4)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block, 64)) != FMX_OK) return rc;
+  if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block, 64)) != FMX_OK) return rc;
   h->rds_stride = (h->t_rds.stride + 63) & ~63; // 256-B rows: k_rds stages 16-B aligned pieces
   for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;

@@ -34,10 +34,10 @@
 #include "fmx_math.h"
 #include "fmx_synth.h"
 
-// k_rds's FIR partial sums: FMX_RDS_FMA (default) one packed FMA per product; 0 the
+// k_rds's FIR partial sums: one packed FMA per product instead of the
 // reference's separate multiply and add (its dotprod order, rounded twice).
 // The RDS path is held to bit-exact groups, not to bit-exact floats (its
-// mix-down sine is already the hardware one).
+// mix-down sine is the hardware one).
 
 namespace fmx {
 

@@ -8,7 +8,8 @@
 #        bench with the CPU baseline), trace (rocprofv3 kernel trace + gaps),
 #        stats (rocprofv3 --kernel-trace --stats), pmc (FETCH / WRITE passes),
 #        ubench (tools/ubench/chainlat), sweep (channel sweep), stamps (stage clocks,
-#        diagnostics library), iso (isolated kernel times, diagnostics library)
+#        diagnostics library), iso (isolated kernel times, diagnostics library),
+#        units (unit counters for bench.py's roofline), retune_ab (a retune per step vs none)
 TAG=$1
 shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -92,6 +93,22 @@ for step in "$@"; do
     sweep)
       bash tools/gpu_sweep.sh $TAG > $O/sweep_$TAG.log 2>&1; rc=$?
       cat $O/sweep_$TAG.log ;;
+    units)
+      # per-kernel unit counters (VALU / MFMA / LDS / HBM) for bench.py's roofline units
+      bash tools/gpu_units.sh $TAG > $O/units_$TAG.log 2>&1 && \
+      UNITS_ARGS="--channels 2048" bash tools/gpu_units.sh ${TAG}_2048 >> $O/units_$TAG.log 2>&1; rc=$?
+      cat $O/units_$TAG.log ;;
+    retune_ab)
+      # a retune of one channel before every step against none, interleaved, 3 x 20 steps each
+      rc=0
+      for rep in 1 2 3; do
+        for arm in off on; do
+          X=""; [ $arm = on ] && X="--retune-per-step"
+          timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $X > $O/retune_${TAG}_${arm}_$rep.json \
+            2> $O/retune_${TAG}_${arm}_$rep.err || { rc=$?; break 2; }
+          python3 -c "import json; r=json.load(open('$O/retune_${TAG}_${arm}_$rep.json')); print('$arm', r['ms_per_step'], {k: (v['avg_ms'], v['launches']) for k, v in r['kernels'].items()})"
+        done
+      done ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"
