@@ -146,6 +146,10 @@ struct Handle {
   float *rds_win[FMX_NBUF] = {};  // [C][32] the previous call's last MPX samples, k_fe8 -> k_rs
   float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
+  // the call's PSK2 symbols, k_rds -> k_bits (at most one per decimation period)
+  float *rds_sym = nullptr, *rds_sym_im = nullptr;
+  int *rds_sym_count = nullptr;
+  int sym_stride = 0;
   uint32_t block_index = 0;
   TimingSet t_af, t_mono, t_rds;
   // kernel timing
@@ -890,6 +894,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = tset_init(h, h->t_af, h->hdes->af_del, cfg->block, 64)) != FMX_OK) return rc;
   if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block, 64)) != FMX_OK) return rc;
   h->rds_stride = (h->t_rds.stride + 63) & ~63; // 256-B rows: k_rds stages 16-B aligned pieces
+  h->sym_stride = (h->rds_stride / FMX_RDS_DECIM + 8 + 3) & ~3;
+  if ((rc = dalloc(h, &h->rds_sym, C * static_cast<size_t>(h->sym_stride))) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rds_sym_im, C)) != FMX_OK) return rc;
+  if ((rc = dalloc(h, &h->rds_sym_count, C)) != FMX_OK) return rc;
   for (int b = 0; b < FMX_NBUF; ++b) {
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
@@ -1002,6 +1010,10 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
+  a.sym = h->rds_sym;
+  a.sym_stride = h->sym_stride;
+  a.sym_count = h->rds_sym_count;
+  a.sym_last_im = h->rds_sym_im;
   return a;
 }
 

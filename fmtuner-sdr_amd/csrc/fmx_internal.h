@@ -155,6 +155,11 @@ struct RdsArgs {
   int *group_count;
   uint32_t block_index;
   unsigned long long *dbg; // [8] stage clocks (diagnostic, FMX_STAMPS=1), may be null
+  // the call's PSK2 symbols, k_rds -> k_bits (the bit decoders)
+  float *sym;         // [C][sym_stride] real parts
+  int sym_stride;
+  int *sym_count;     // [C]
+  float *sym_last_im; // [C] the last symbol's imaginary part (BiphaseDecoder's prev)
 };
 
 // k_pilot: the 19 kHz pilot BPF of a process_block step (after k_fe8)

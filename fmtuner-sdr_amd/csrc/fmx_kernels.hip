@@ -1010,6 +1010,14 @@ __device__ __forceinline__ void dma_dword_s(const float *base, uint32_t voff, ui
                : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
                : "memory");
 }
+// three dwords per lane (12 B, landing at m0 + 12 lane) from a per-lane address
+__device__ __forceinline__ void dma_dwordx3(const float *src, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx3 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p);
 }
@@ -1606,20 +1614,22 @@ __device__ __forceinline__ void rds_bits_store(FmxRdsState &g, const RdsBits &b)
   g.bs_bits_since_lost = b.bs_bits_since_lost;
 }
 struct RdsLds {
-  // tap columns: hq[j0][i][q] = h[23 - (j0 + 8 q) + 24 i] (zeros past tap 254),
+  // tap columns: hq[j0][i][q] = h[23 - (3 j0 + q) + 24 i] (zeros past tap 254),
   // q padded to 4 (one 16-B read per accumulator)
   float hq[RDS_LPC][FMX_RDS_NACC][4] __attribute__((aligned(16)));
   float mf[FMX_NPFB * FMX_SS_SUB];
   float dmf[FMX_NPFB * FMX_SS_SUB];
-  uint32_t esyn[5][52];
-  uint32_t eerr[5][52];
   // symsync window ring per channel, newest at wp, every sample written at
   // wp and wp + FMX_SS_SUB: the window oldest-first is win[w0 .. w0 + 17],
   // contiguous (constant read offsets, no wrap per tap)
   f32x2 win[2 * FMX_SS_SUB][RDS_CPW];
-  float symq[RDS_SYMQ][RDS_CPW];   // symbols (real part) awaiting biphase / block sync
-  float xin[RDS_NR][3][64];        // input ring: round r's sample j0 + 8 q of lane's channel at [r % RDS_NR][q][lane]
-  RdsCold cold[RDS_CPW];
+  float xin[RDS_NR][3][64];        // input ring: round r's sample 3 j0 + q of lane's channel at [r % RDS_NR][q][lane]
+};
+// k_bits: the bit decoders' LDS (burst-error tables, one bit state per lane)
+struct BitsLds {
+  uint32_t esyn[5][52];
+  uint32_t eerr[5][52];
+  RdsCold cold[64];
 };
 
 __device__ __forceinline__ void rds_emit_group(RdsBits &s, const RdsArgs &a, int c, int &ng) {
@@ -1645,7 +1655,7 @@ __device__ __forceinline__ void rds_emit_group(RdsBits &s, const RdsArgs &a, int
 
 // BlockStream::pushBit / findBlockInInputRegister / acquireSync
 // (block_sync.cpp:235-313) and Group::setBlock (group.cpp:103-128)
-__device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &L, const RdsArgs &a, int c, int &ng) {
+__device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const BitsLds &L, const RdsArgs &a, int c, int &ng) {
   s.bs_reg = (s.bs_reg << 1u) + (uint32_t)bit;
   s.bs_until_next--;
   s.bs_bitcount++;
@@ -1714,9 +1724,14 @@ __device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &
       }
       if (off == s.bs_expected) {
         const int bn = bs_block_number(s.bs_expected);
-        s.bs_blk_raw[bn] = raw;
-        s.bs_blk_data[bn] = data;
-        s.bs_blk_flags[bn] = (uint8_t)(1 | (had ? 2 : 0));
+        // (static indices: the state lives in registers in k_bits)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i == bn) {
+            s.bs_blk_raw[i] = raw;
+            s.bs_blk_data[i] = data;
+            s.bs_blk_flags[i] = (uint8_t)(1 | (had ? 2 : 0));
+          }
       }
       const int next = bs_next(s.bs_expected);
       if (next == OA) {
@@ -1734,18 +1749,23 @@ __device__ __forceinline__ void rds_push_bit(RdsBits &s, int bit, const RdsLds &
 }
 
 
-// the sum of a value over the 8 lanes of a channel group (DPP butterfly:
+// the sums of two values over the 8 lanes of a channel group (DPP butterfly:
 // quad_perm xor 1, xor 2, then row_half_mirror): every lane of the group
-// gets the same bits (each step adds two identical pairs in swapped order)
-__device__ __forceinline__ float rds_sum8(float x) {
-  auto dpp = [](float v, auto ctrl_c) __attribute__((always_inline)) {
-    constexpr int ctrl = decltype(ctrl_c)::value;
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false));
-  };
-  x = x + dpp(x, std::integral_constant<int, 0xB1>{});  // quad_perm [1, 0, 3, 2]
-  x = x + dpp(x, std::integral_constant<int, 0x4E>{});  // quad_perm [2, 3, 0, 1]
-  x = x + dpp(x, std::integral_constant<int, 0x141>{}); // row_half_mirror
-  return x;
+// gets the same bits (each step adds two identical pairs in swapped order).
+// Round 5: one v_add_f32_dpp per step and value (a VALU write is read by DPP
+// two wait states later: the s_nops) instead of v_mov_dpp + v_add, and never
+// packed by the vectoriser beside LDS returns (tests/test_isa_scan.py)
+__device__ __forceinline__ f32x2 rds_sum8x2(float x, float y) {
+#define RDS_DPP(C) " row_mask:0xf bank_mask:0xf\n\t"
+  asm volatile("s_nop 1\n\t"
+               "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2]" RDS_DPP() "v_add_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2]" RDS_DPP()
+               "s_nop 0\n\t"
+               "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1]" RDS_DPP() "v_add_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1]" RDS_DPP()
+               "s_nop 0\n\t"
+               "v_add_f32_dpp %0, %0, %0 row_half_mirror" RDS_DPP() "v_add_f32_dpp %1, %1, %1 row_half_mirror" RDS_DPP()
+               : "+v"(x), "+v"(y));
+#undef RDS_DPP
+  return f32x2{x, y};
 }
 
 __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
@@ -1759,8 +1779,9 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   extern __shared__ __align__(16) unsigned char rds_smem[];
   RdsLds &L = *reinterpret_cast<RdsLds *>(rds_smem);
 #ifdef FMX_STAMPS
-  // stage clocks (diagnostics build): 0 setup, 1 mix + FIR products, 2 FIR
-  // output -> AGC -> symsync -> PLL, 3 bit decoders, 4 state store
+  // stage clocks (diagnostics build): 0 setup + state store, 1 input moves
+  // and their wait, 2 mix-down, 3 FIR products, 4 FIR output + AGC, 5
+  // symsync, 6 PSK2 / NCO update, 7 bit decoders
   unsigned long long rs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long rs_last = __builtin_amdgcn_s_memtime();
 #define RDS_STAMP(k)                                            \
@@ -1786,23 +1807,10 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   }
   for (int idx = lane; idx < RDS_LPC * FMX_RDS_NACC * 4; idx += 64) {
     const int jj = idx / (FMX_RDS_NACC * 4), i = (idx / 4) % FMX_RDS_NACC, q = idx % 4;
-    L.hq[jj][i][q] = (q < 3) ? D->rds_fir[FMX_RDS_DECIM - 1 - (jj + 8 * q) + FMX_RDS_DECIM * i] : 0.0f;
+    L.hq[jj][i][q] = (q < 3) ? D->rds_fir[FMX_RDS_DECIM - 1 - (3 * jj + q) + FMX_RDS_DECIM * i] : 0.0f;
   }
-  // burst-error syndromes per offset word: entry idx < 26 a single-bit error
-  // at bit idx, idx >= 26 a two-bit burst at bit idx - 26 (all lanes; five
-  // serial lanes cost ~10 us at every launch)
-  for (int k = lane; k < 5 * 52; k += 64) {
-    const int w = k / 52, idx = k % 52;
-    const uint32_t word = w == 0 ? 0x0FCu : w == 1 ? 0x198u : w == 2 ? 0x168u : w == 3 ? 0x350u : 0x1B4u;
-    const uint32_t bits = idx < 26 ? 1u : 3u, sh = idx < 26 ? idx : idx - 26;
-    const uint32_t e = (bits << sh) & ((1u << 26) - 1u);
-    L.esyn[w][idx] = bs_syndrome(e ^ word);
-    L.eerr[w][idx] = e;
-  }
-  RdsBits &S = L.cold[g].s;
   const FmxRdsState G = act ? a.st[c] : FmxRdsState{}; // the compiler loads only the fields used
   const int count = act ? a.in_count[c] : 0;
-  if (lead) rds_bits_load(S, G);
   float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
   // ---- hot state -> registers ----
   uint32_t theta = G.theta, dtheta = G.dtheta;
@@ -1875,23 +1883,25 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, __shfl_xor(rmax, d));
   // the NCO word at period position 0 of round 0 (virtual for o0 < 23)
   uint32_t thp = theta - (uint32_t)(FMX_RDS_DECIM - 1 - o0) * dtheta;
-  int nq = 0;
+  int nsym = 0; // symbols of this call (k_bits decodes them)
   float last_symi = 0.0f;
+  float *symrow = a.sym + (size_t)(act ? c : 0) * a.sym_stride;
   // input: the channel rows of this workgroup, sample t of the lane's channel
-  // at inb[g * stride + t]; samples outside [0, count) read the row's first
-  // word (every use masks them: vq below).  Each round's three samples per
-  // lane are moved by LDS-DMA into the ring L.xin, RDS_PF rounds ahead, and
-  // read back when the round runs: the wave's only vector-memory loads, so a
-  // counted s_waitcnt finds them (round 3 rotated a register ring, and the
-  // rotation waited for the loads of the round before: one memory latency
-  // per round, half of the mix + FIR stage's clocks)
+  // at inb[g * stride + t]; the lane takes the period's positions 3 j0 .. 3 j0
+  // + 2 (round 5: contiguous); samples outside [0, count) read the row's
+  // first word (every use masks them: vq below).  Each round's three samples
+  // per lane are moved by LDS-DMA into the ring L.xin, RDS_PF rounds ahead,
+  // and read back when the round runs: the wave's only vector-memory loads,
+  // so a counted s_waitcnt finds them (round 3 rotated a register ring, and
+  // the rotation waited for the loads of the round before: one memory
+  // latency per round)
   const float *inb = a.in + (size_t)c0 * a.in_stride;
   const uint32_t xin0 = lds_addr(&L.xin[0][0][0]);
   auto dma_round = [&](int r) __attribute__((always_inline)) {
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int t = base + j0 + 8 * q;
+      const int t = base + 3 * j0 + q;
       const bool v = act && r < R && t >= 0 && t < count;
       dma_dword(inb + (act ? g * a.in_stride : 0) + (v ? t : 0),
                 xin0 + (uint32_t)(((r & (RDS_NR - 1)) * 3 + q) * 64 * 4));
@@ -1899,36 +1909,6 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   };
 #pragma unroll
   for (int p = 0; p < RDS_PF; ++p) dma_round(p);
-  // biphase + delta (subcarrier.cpp:50-92) -> block sync, for the queued
-  // symbols, in the channel's first lane
-  auto flush_symbols = [&]() __attribute__((always_inline)) {
-    if (lead && act) {
-      for (int k = 0; k < nq; ++k) {
-        const float symr = L.symq[k][g];
-        const float bir = (symr - S.bi_prev_re) * 0.5f;
-        const int val = bir >= 0.0f;
-        const bool has = (S.bi_clock % 2u) == S.bi_polarity;
-        S.bi_prev_re = symr;
-        if ((S.bi_clock & 1u) == 0) S.bi_even += fabsf(bir);
-        else S.bi_odd += fabsf(bir);
-        S.bi_clock++;
-        if (S.bi_clock == 128u) {
-          if (S.bi_even > S.bi_odd) S.bi_polarity = 0;
-          else if (S.bi_odd > S.bi_even) S.bi_polarity = 1;
-          S.bi_even = 0.0f;
-          S.bi_odd = 0.0f;
-          S.bi_clock = 0;
-        }
-        if (has) {
-          const int bit = (val != S.delta_prev) ? 1 : 0;
-          S.delta_prev = val;
-          rds_push_bit(S, bit, L, a, c, ng);
-        }
-      }
-      if (nq > 0) S.bi_prev_im = last_symi;
-    }
-    nq = 0;
-  };
   __syncthreads(); // LDS tables and per-channel state written
   RDS_STAMP(0)
   for (int r = 0; r < rmax; ++r) {
@@ -1939,6 +1919,21 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     float xr0[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) xr0[q] = L.xin[r & (RDS_NR - 1)][q][lane];
+    // this lane's tap columns for the FIR products below: all eleven reads
+    // issued here, ahead of the mix-down, which hides their latency (round 4
+    // interleaved one read per accumulator with its packed FMAs: eleven LDS
+    // latencies per round); the scheduling barrier keeps them together, so
+    // none lands over the sources of a packed op (tests/test_isa_scan.py)
+    float hr[FMX_RDS_NACC][3];
+#pragma unroll
+    for (int i = 0; i < FMX_RDS_NACC; ++i) {
+      const float4 h = *reinterpret_cast<const float4 *>(&L.hq[j0][i][0]);
+      hr[i][0] = h.x;
+      hr[i][1] = h.y;
+      hr[i][2] = h.z;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    RDS_STAMP(1)
     const bool live = r < R;
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
     // ---- mix-down and FIR products of this lane's samples (oldest first) ----
@@ -1946,7 +1941,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     bool vq[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int j = j0 + 8 * q;
+      const int j = 3 * j0 + q;
       const int t = base + j;
       vq[q] = live && t >= 0 && t < count;
       const uint32_t w = thp + (uint32_t)j * dtheta;
@@ -1960,22 +1955,22 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
         *reinterpret_cast<f32x2 *>(ring + 2 * idx) = mq[q];
       }
     }
+    RDS_STAMP(2)
     if (live) {
 #pragma unroll
       for (int i = 0; i < FMX_RDS_NACC; ++i) {
-        const float4 h = *reinterpret_cast<const float4 *>(&L.hq[j0][i][0]);
         // the lane's samples oldest first, as the window dot product (a
         // sample outside the call is 0 and adds +0)
-        acc[i] = __builtin_elementwise_fma(f32x2{h.x, h.x}, mq[0], acc[i]);
-        acc[i] = __builtin_elementwise_fma(f32x2{h.y, h.y}, mq[1], acc[i]);
-        acc[i] = __builtin_elementwise_fma(f32x2{h.z, h.z}, mq[2], acc[i]);
+        acc[i] = __builtin_elementwise_fma(f32x2{hr[i][0], hr[i][0]}, mq[0], acc[i]);
+        acc[i] = __builtin_elementwise_fma(f32x2{hr[i][1], hr[i][1]}, mq[1], acc[i]);
+        acc[i] = __builtin_elementwise_fma(f32x2{hr[i][2], hr[i][2]}, mq[2], acc[i]);
       }
     }
-    RDS_STAMP(1)
+    RDS_STAMP(3)
     const bool has_out = live && base + FMX_RDS_DECIM - 1 < count;
     if (has_out) {
       // ---- FIR output (every 24th sample) -> AGC -> symsync -> PSK2 PLL ----
-      const f32x2 f = f32x2{rds_sum8(acc[0].x), rds_sum8(acc[0].y)} * fscale2;
+      const f32x2 f = rds_sum8x2(acc[0].x, acc[0].y) * fscale2;
 #pragma unroll
       for (int i = 0; i < FMX_RDS_NACC - 1; ++i) acc[i] = acc[i + 1];
       acc[FMX_RDS_NACC - 1] = f32x2{0.0f, 0.0f};
@@ -1984,6 +1979,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       agc_y2p = (float)((1.0 - (double)agc_bw) * (double)agc_y2p + (double)(agc_bw * y2));
       if (agc_y2p > 1e-6f) agc_g *= expf(-0.5f * agc_bw * logf(agc_y2p));
       if (agc_g > 1e6f) agc_g = 1e6f;
+      RDS_STAMP(4)
       // ---- symsync: push into both MF banks' window ----
       wp = (wp == FMX_SS_SUB - 1) ? 0 : wp + 1;
       if (lead) L.win[wp][g] = L.win[wp + FMX_SS_SUB][g] = f32x2{yr, yi};
@@ -2011,7 +2007,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
               p = __builtin_elementwise_fma(f32x2{h, h}, wat(m), p);
             }
           }
-          return f32x2{rds_sum8(p.x), rds_sum8(p.y)};
+          return rds_sum8x2(p.x, p.y);
         };
         const f32x2 acm = mf_dot(hm);
         // x / 3 as fmx_div_const (bit-identical for every normal x,
@@ -2040,6 +2036,7 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
       }
       ss_tau -= 1.0f;
       ss_b -= FMX_NPFB;
+      RDS_STAMP(5)
       // the NCO word of the instant's sample; step() follows the PLL update
       uint32_t tho = thp + (uint32_t)(FMX_RDS_DECIM - 1) * dtheta;
       if (ns == 1) {
@@ -2062,29 +2059,24 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
         const float dphi = pe * 12.0f;
         dtheta += d_nco_constrain(dphi * alpha);
         tho += d_nco_constrain(dphi * beta);
-        // biphase / delta / block sync only consume symbols: queue them and
-        // run those decoders outside the sample loop (flush_symbols)
-        if (lead) L.symq[nq][g] = symr;
+        // biphase / delta / block sync only consume symbols: they go to
+        // HBM and k_bits decodes them (one lane per channel, round 5: the
+        // decoders ran in each channel's first lane here, 8 of 64 lanes,
+        // ~14 % of this kernel's serial time, profiles/r05i_stamps.txt)
+        if (lead && act && nsym < a.sym_stride) symrow[nsym] = symr;
         last_symi = symi;
-        nq++;
+        nsym++;
       }
       thp = tho + dtheta; // period position 0 of the next round
     } else if (live) {
       // tail: samples base .. count-1 stepped, no decimation instant
       thp = thp + (uint32_t)(count - base) * dtheta;
     }
-    RDS_STAMP(2)
-    // decoders every RDS_SYMQ - 2 rounds (at most one symbol per round)
-    if (r % (RDS_SYMQ - 2) == RDS_SYMQ - 3) {
-      flush_symbols();
-      RDS_STAMP(3)
-    }
+    RDS_STAMP(6)
   }
-  flush_symbols();
-  RDS_STAMP(3)
   // the channel's partial sums: the lanes' shares added (every lane gets them)
 #pragma unroll
-  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = f32x2{rds_sum8(acc[i].x), rds_sum8(acc[i].y)};
+  for (int i = 0; i < FMX_RDS_NACC; ++i) acc[i] = rds_sum8x2(acc[i].x, acc[i].y);
   if (!act || !lead) return;
   // ---- registers -> state ----
   FmxRdsState *out = a.st + c;
@@ -2119,14 +2111,84 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   out->ss_v2 = G.ss_v2;
   out->ss_b = ss_b;
   out->ss_decim = ss_decim;
-  rds_bits_store(*out, S);
-  if (a.group_count) a.group_count[c] = ng;
-  RDS_STAMP(4)
+  a.sym_count[c] = min(nsym, a.sym_stride);
+  a.sym_last_im[c] = last_symi;
+  RDS_STAMP(0)
 #ifdef FMX_STAMPS
   if (a.dbg && lane == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, rs_acc[k]);
 #endif
 #undef RDS_STAMP
+}
+
+// k_bits (round 5): the RDS bit decoders of one call -- BiphaseDecoder::push
+// (subcarrier.cpp:50-86), DeltaDecoder (:88-92) and BlockStream::pushBit /
+// Group (block_sync.cpp:235-313, group.cpp:103-128) -- over the symbols
+// k_rds wrote, one lane per channel (64 channels per wave instead of k_rds's
+// 8 first lanes), on the RDS stream right after k_rds.
+__global__ __launch_bounds__(64) void k_bits(RdsArgs a) {
+  extern __shared__ __align__(16) unsigned char bits_smem[];
+  BitsLds &L = *reinterpret_cast<BitsLds *>(bits_smem);
+  const int lane = threadIdx.x;
+  const int c = blockIdx.x * 64 + lane;
+  const bool act = c < a.C;
+  // burst-error syndromes per offset word: entry idx < 26 a single-bit error
+  // at bit idx, idx >= 26 a two-bit burst at bit idx - 26 (all lanes)
+  for (int k = lane; k < 5 * 52; k += 64) {
+    const int w = k / 52, idx = k % 52;
+    const uint32_t word = w == 0 ? 0x0FCu : w == 1 ? 0x198u : w == 2 ? 0x168u : w == 3 ? 0x350u : 0x1B4u;
+    const uint32_t bits = idx < 26 ? 1u : 3u, sh = idx < 26 ? idx : idx - 26;
+    const uint32_t e = (bits << sh) & ((1u << 26) - 1u);
+    L.esyn[w][idx] = bs_syndrome(e ^ word);
+    L.eerr[w][idx] = e;
+  }
+  __syncthreads();
+  if (!act) return;
+  RdsBits S; // in registers
+  rds_bits_load(S, a.st[c]);
+  const int nsym = a.sym_count[c];
+  // the symbols four at a time, the next four loaded while these decode (a
+  // dependent load per symbol cost a memory latency each)
+  const float4 *srow = reinterpret_cast<const float4 *>(a.sym + (size_t)c * a.sym_stride);
+  const int nq4 = a.sym_stride / 4;
+  float4 nx = nsym > 0 ? srow[0] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  int ng = 0;
+  for (int k0 = 0; k0 < nsym; k0 += 4) {
+    // this chunk in four scalars (the chunk shifts down one symbol per step:
+    // no indexing, no scratch), the next one loading meanwhile
+    float q0 = nx.x, q1 = nx.y, q2 = nx.z, q3 = nx.w;
+    if (k0 + 4 < nsym && k0 / 4 + 1 < nq4) nx = srow[k0 / 4 + 1];
+    const int nj = min(4, nsym - k0);
+#pragma unroll 1
+    for (int j = 0; j < nj; ++j) {
+      const float symr = q0;
+      q0 = q1;
+      q1 = q2;
+      q2 = q3;
+      const float bir = (symr - S.bi_prev_re) * 0.5f;
+      const int val = bir >= 0.0f;
+      const bool has = (S.bi_clock % 2u) == S.bi_polarity;
+      S.bi_prev_re = symr;
+      if ((S.bi_clock & 1u) == 0) S.bi_even += fabsf(bir);
+      else S.bi_odd += fabsf(bir);
+      S.bi_clock++;
+      if (S.bi_clock == 128u) {
+        if (S.bi_even > S.bi_odd) S.bi_polarity = 0;
+        else if (S.bi_odd > S.bi_even) S.bi_polarity = 1;
+        S.bi_even = 0.0f;
+        S.bi_odd = 0.0f;
+        S.bi_clock = 0;
+      }
+      if (has) {
+        const int bit = (val != S.delta_prev) ? 1 : 0;
+        S.delta_prev = val;
+        rds_push_bit(S, bit, L, a, c, ng);
+      }
+    }
+  }
+  if (nsym > 0) S.bi_prev_im = a.sym_last_im[c];
+  rds_bits_store(a.st[c], S);
+  if (a.group_count) a.group_count[c] = ng;
 }
 
 /* ================================================================== */
@@ -3500,7 +3562,17 @@ int launch_rds(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
   // k_rds workgroups fit beside them
   static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
-  return fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
+  static_assert(sizeof(BitsLds) <= 16 * 1024, "k_bits LDS");
+  // the bound events (set_launch_events): the start on k_rds, the stop on
+  // k_bits, so that the RDS timer and the stream's completion event span both
+  hipEvent_t e0 = t_ev_start, e1 = t_ev_stop;
+  t_ev_start = t_ev_stop = nullptr;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  set_launch_events(e0, nullptr);
+  int rc = fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), st, a);
+  if (rc != FMX_OK) return rc;
+  set_launch_events(nullptr, e1);
+  return fmx_launch(k_bits, dim3((a.C + 63) / 64), dim3(64), sizeof(BitsLds), st, a);
 }
 // 16-B words src -> dst (the schedule upload from mapped pinned memory)
 __global__ void k_copy16(const uint4 *src, uint4 *dst, size_t n16) {

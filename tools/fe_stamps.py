@@ -58,12 +58,13 @@ tot = sum(v[:8])
 print(f"k_fe8 (thread 0 of each workgroup; {nblk} blocks after {NW} warm-up blocks)")
 for k in range(8):
     print(f"  {NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
-RN = ["setup", "mix+fir", "out+agc+ss+pll", "decode", "store", "-", "-", "-"]
+RN = ["setup+store", "dma_wait+ld", "mix", "fir", "sum+agc", "symsync", "psk+nco", "decode"]
 tot = sum(v[8:16]) or 1
 nwg = (Cn + 7) // 8
-print("k_rds (lane 0 of each workgroup of 8 channels)")
+print("k_rds (lane 0 of each workgroup of 8 channels; per decimation period = ticks / 121.6 at 4096 samples)")
 for k in range(8):
-    print(f"  {RN[k]:10s} {v[8 + k] / tot * 100:6.1f} %  {v[8 + k] / (nwg * nblk):10.0f} ticks/launch-WG")
+    print(f"  {RN[k]:12s} {v[8 + k] / tot * 100:6.1f} %  {v[8 + k] / (nwg * nblk):10.0f} ticks/launch-WG"
+          f"  {v[8 + k] / (nwg * nblk) / (B * 0.7125 / 24):8.1f} per period")
 nwg = (Cn + PLL_CH - 1) // PLL_CH
 print(f"k_pll per wave (lane 0): work / barrier-wait ticks per launch-WG ({PLL_CH} channels per workgroup)")
 for w, nm in enumerate(["W0 chain", "WB blend", "P0", "P1", "P2", "P3"]):

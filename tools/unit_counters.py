@@ -43,7 +43,7 @@ COUNTERS = {
 
 
 def short(name):
-    for k in ("k_fe8", "k_frontend", "k_pll", "k_pilot", "k_audio", "k_rds", "k_rs", "k_reset", "k_synth", "k_copy16"):
+    for k in ("k_fe8", "k_frontend", "k_pll", "k_pilot", "k_audio", "k_rds", "k_bits", "k_rs", "k_reset", "k_synth", "k_copy16"):
         if k in name:
             return k
     return None
