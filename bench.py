@@ -61,9 +61,11 @@ PER_IQ = {
     "rs": (0.4 + 4.0 * 0.7125 / 10.0, 7.4),
     "pilot": (0.4 + 0.4, 61.0),
     "frontend_generic": (2.0 + 0.4, 112.0 + 32.4),
+    # k_bits: the PSK2 symbols (2 375 / s, f32) k_rds wrote; bit logic, no FLOP
+    "bits": (4.0 * 2375.0 / 2.4e6, 0.0),
 }
 KNAME = {"frontend": "k_fe8", "stereo": "k_pll", "audio": "k_audio", "rds": "k_rds", "rs": "k_rs", "pilot": "k_pilot",
-         "frontend_generic": "k_frontend"}
+         "frontend_generic": "k_frontend", "bits": "k_bits"}
 
 
 def pmc_bytes(pmc, k):

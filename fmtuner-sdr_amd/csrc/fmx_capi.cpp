@@ -146,9 +146,10 @@ struct Handle {
   float *rds_win[FMX_NBUF] = {};  // [C][32] the previous call's last MPX samples, k_fe8 -> k_rs
   float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
-  // the call's PSK2 symbols, k_rds -> k_bits (at most one per decimation period)
-  float *rds_sym = nullptr, *rds_sym_im = nullptr;
-  int *rds_sym_count = nullptr;
+  // the call's PSK2 symbols, k_rds (sC) -> k_bits (sD), per slot (at most one
+  // per decimation period)
+  float *rds_sym[FMX_NBUF] = {}, *rds_sym_im[FMX_NBUF] = {};
+  int *rds_sym_count[FMX_NBUF] = {};
   int sym_stride = 0;
   uint32_t block_index = 0;
   TimingSet t_af, t_mono, t_rds;
@@ -895,10 +896,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = tset_init(h, h->t_mono, h->hdes->af_del, cfg->block, 64)) != FMX_OK) return rc;
   h->rds_stride = (h->t_rds.stride + 63) & ~63; // 256-B rows: k_rds stages 16-B aligned pieces
   h->sym_stride = (h->rds_stride / FMX_RDS_DECIM + 8 + 3) & ~3;
-  if ((rc = dalloc(h, &h->rds_sym, C * static_cast<size_t>(h->sym_stride))) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->rds_sym_im, C)) != FMX_OK) return rc;
-  if ((rc = dalloc(h, &h->rds_sym_count, C)) != FMX_OK) return rc;
   for (int b = 0; b < FMX_NBUF; ++b) {
+    if ((rc = dalloc(h, &h->rds_sym[b], C * static_cast<size_t>(h->sym_stride))) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rds_sym_im[b], C)) != FMX_OK) return rc;
+    if ((rc = dalloc(h, &h->rds_sym_count[b], C)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_in[b], C * static_cast<size_t>(h->rds_stride))) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_count[b], C)) != FMX_OK) return rc;
     if ((rc = dalloc(h, &h->rds_win[b], C * 32)) != FMX_OK) return rc;
@@ -1010,10 +1011,10 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.ring = h->ring;
   a.block_index = h->block_index;
   a.dbg = h->dbg ? h->dbg + 8 : nullptr;
-  a.sym = h->rds_sym;
+  a.sym = h->rds_sym[buf];
   a.sym_stride = h->sym_stride;
-  a.sym_count = h->rds_sym_count;
-  a.sym_last_im = h->rds_sym_im;
+  a.sym_count = h->rds_sym_count[buf];
+  a.sym_last_im = h->rds_sym_im[buf];
   return a;
 }
 
@@ -1043,7 +1044,7 @@ static void step_done(Handle *h, bool stereo_hist_written) {
 //   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evF(k), k_pilot -> evP(k)
 //   sC: [wait evF(k)] k_rs, k_rds -> evC(k)
 //   sB: [wait evP(k)] k_pll -> evB(k)
-//   sD: [wait evB(k), evC(k)] [audio schedule copy] k_audio -> evD(k)
+//   sD: [wait evB(k), evC(k)] k_bits, [audio schedule copy] k_audio -> evD(k)
 // evD(k) therefore marks every reader of slot buf done (k_audio waits for
 // k_rds as well as k_pll), so the front end of step k+3 -- the next writer of
 // the slot, and through evP of the raw L/R slot k_pll writes -- needs ONE
@@ -1196,7 +1197,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
     KBind t(h, FMX_K_RDS, h->sC, h->evC[buf]);
     if (!FMX_SKIP(rds)) {
-      if ((rc = launch_rds(a, h->sC)) != FMX_OK) {
+      if ((rc = launch_rds_sym(a, h->sC)) != FMX_OK) {
         h->err = "rds launch failed";
         return rc;
       }
@@ -1234,8 +1235,23 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   // after k_rds, so that evD closes the step ----
   HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0));
   HIP_TRY(hipStreamWaitEvent(h->sD, h->evC[buf], 0));
-  if ((rc = launch_reset_parts(h, RSP_AUDIO, h->sD)) != FMX_OK) return rc;
+  if ((rc = launch_reset_parts(h, RSP_AUDIO | RSP_BITS, h->sD)) != FMX_OK) return rc;
   h->rl_pending.clear();
+  // the RDS bit decoders (k_bits) over k_rds's symbols of slot buf, here
+  // rather than behind k_rds on sC: the RDS stream's step is k_rs + k_rds
+  // only, k_bits runs beside the next step's k_rs
+  if (rds && !FMX_SKIP(rds)) {
+    RdsArgs a = rds_args(h, buf);
+    a.groups = o->d_groups;
+    a.groups_stride = o->d_groups ? o->groups_stride : 0;
+    a.group_count = o->d_group_count;
+    KBind t(h, FMX_K_BITS, h->sD, nullptr);
+    if ((rc = launch_bits(a, h->sD)) != FMX_OK) {
+      h->err = "rds bit decoder launch failed";
+      return rc;
+    }
+    t.launched();
+  }
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
   if ((rc = tset_advance(h, *tau, n, buf, h->sD, nullptr)) != FMX_OK) return rc;
   {

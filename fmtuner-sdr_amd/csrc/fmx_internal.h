@@ -207,7 +207,9 @@ bool frontend_is_fe8(const FeArgs &a, int M, int tpp);
 int launch_pll(const PllArgs &a, void *stream);
 int launch_pilot(const PilotArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
-int launch_rds(const RdsArgs &a, void *stream);
+int launch_rds(const RdsArgs &a, void *stream);      // k_rds then k_bits (one timer over both)
+int launch_rds_sym(const RdsArgs &a, void *stream);  // k_rds alone: the call's symbols
+int launch_bits(const RdsArgs &a, void *stream);     // k_bits alone: the bit decoders
 #ifndef FMX_RS_TMAX
 #define FMX_RS_TMAX 24 // k_rs: output tiles (of 16) per workgroup at most; parts = ceil(tiles / FMX_RS_TMAX)
 #endif
@@ -257,9 +259,10 @@ enum ResetParts {
 enum ResetStreamPart {
   RSP_FRONT = 1,  // sA: decimator / IQ FIR / DC / AGC / discriminator state, stereo history rows
   RSP_STEREO = 2, // sB: FmxStereoState (k_pll)
-  RSP_RDS = 4,    // sC: FmxRdsState, mix-down ring (k_rds)
+  RSP_RDS = 4,    // sC: FmxRdsState up to the bit decoders, mix-down ring (k_rds)
   RSP_AUDIO = 8,  // sD: L/R FIR history, AF / mono resampler + IIRs, retune mute (k_audio)
-  RSP_ALL = 15
+  RSP_BITS = 16,  // sD: FmxRdsState's bit decoders, bi_prev_re on (k_bits)
+  RSP_ALL = 31
 };
 #define FMX_RESET_LIST 64 // channels per k_reset_list launch (a kernel argument, no upload)
 struct ResetList {

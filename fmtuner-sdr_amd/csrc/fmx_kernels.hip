@@ -28,6 +28,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <type_traits>
 
 #include "fmx_internal.h"
@@ -1864,7 +1865,6 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
   if (lead)
     for (int m = 0; m < FMX_SS_SUB; ++m) L.win[m][g] = L.win[m + FMX_SS_SUB][g] = f32x2{G.ss_win_re[m], G.ss_win_im[m]};
   int wp = FMX_SS_SUB - 1; // newest window sample at wp
-  int ng = 0;
   const f32x2 fscale2 = f32x2{D->rds_fir_scale, D->rds_fir_scale};
   const float agc_bw = D->agc_bw;
   const float ss_b0 = D->ss_b0, ss_a1 = D->ss_a1, ss_adj = D->ss_rate_adj;
@@ -2238,6 +2238,12 @@ __device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int s
     s.pll_freq = D->nominal;
     a.st[c] = s;
   }
+  // FmxRdsState in two parts by owner: k_rds's (the fields before
+  // bi_prev_re, on sC) and k_bits's (bi_prev_re on, on sD, round 5); each part
+  // writes only its own dwords, so a reset on one stream never rewrites the
+  // other kernel's fields while that kernel may run
+  constexpr int kBitsW = (int)(offsetof(FmxRdsState, bi_prev_re) / 4), kRdsW = (int)(sizeof(FmxRdsState) / 4);
+  static_assert(offsetof(FmxRdsState, bi_prev_re) % 4 == 0 && sizeof(FmxRdsState) % 4 == 0, "FmxRdsState parts");
   if ((parts & RSP_RDS) && (create || (m & RS_RDS))) { // sC: k_rds
     if (tid == 0) {
       FmxRdsState s;
@@ -2247,7 +2253,7 @@ __device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int s
         s.agc_y2p = 1.0f;
         s.rebuild = 0;
       } else {
-        s = a.rds[c];
+        s = a.rds[c]; // (the bit decoders' dwords are read but not written back)
         s.rebuild = 1;
       }
       s.theta = 0;
@@ -2268,27 +2274,37 @@ __device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int s
       s.ss_v1 = 0.0f;
       s.ss_v2 = 0.0f;
       s.ss_decim = 0;
-      // fresh BlockStream
-      s.bs_bitcount = 0;
-      s.bs_until_next = 1;
-      s.bs_reg = 0;
-      s.bs_err_mask_lo = 0;
-      s.bs_err_mask_hi = 0;
-      s.bs_expected = OA;
-      s.bs_in_sync = 0;
-      s.bs_err_ptr = 0;
-      for (int i = 0; i < 4; ++i) {
-        s.bs_pulse_pos[i] = 0;
-        s.bs_pulse_off[i] = OINV;
-        s.bs_blk_raw[i] = 0;
-        s.bs_blk_data[i] = 0;
-        s.bs_blk_flags[i] = 0;
-      }
-      s.bs_bits_since_lost = 0;
-      a.rds[c] = s;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(&s);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(a.rds + c);
+      for (int w = 0; w < kBitsW; ++w) dst[w] = src[w];
     }
     if (create)
       for (int h = tid; h < 2 * FMX_RDS_RING; h += blockDim.x) a.ring[(size_t)c * 2 * FMX_RDS_RING + h] = 0.0f;
+  }
+  if ((parts & RSP_BITS) && tid == 0 && (create || (m & RS_RDS))) { // sD: k_bits
+    FmxRdsState s;
+    if (create) s = FmxRdsState{}; // biphase / delta decoders from zero
+    else s = a.rds[c];
+    // fresh BlockStream
+    s.bs_bitcount = 0;
+    s.bs_until_next = 1;
+    s.bs_reg = 0;
+    s.bs_err_mask_lo = 0;
+    s.bs_err_mask_hi = 0;
+    s.bs_expected = OA;
+    s.bs_in_sync = 0;
+    s.bs_err_ptr = 0;
+    for (int i = 0; i < 4; ++i) {
+      s.bs_pulse_pos[i] = 0;
+      s.bs_pulse_off[i] = OINV;
+      s.bs_blk_raw[i] = 0;
+      s.bs_blk_data[i] = 0;
+      s.bs_blk_flags[i] = 0;
+    }
+    s.bs_bits_since_lost = 0;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&s);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(a.rds + c);
+    for (int w = kBitsW; w < kRdsW; ++w) dst[w] = src[w];
   }
   if (parts & RSP_AUDIO) { // sD: k_audio (L/R FIRs, AF post, mono chain, retune mute)
     if (create || (m & RS_STEREO))
@@ -3558,21 +3574,26 @@ int launch_rs(const RsArgs &a, void *stream) {
   static_assert(RS_XS >= RS_KS && RS_XP >= 4 * RS_XS && RS_XS % 4 == 0, "k_rs window layout");
   return fmx_launch(k_rs, dim3((a.C + 15) / 16, a.parts), dim3(64), sizeof(RsLds), static_cast<hipStream_t>(stream), a);
 }
-int launch_rds(const RdsArgs &a, void *stream) {
+int launch_rds_sym(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
   // k_rds workgroups fit beside them
   static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
+  return fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
+}
+int launch_bits(const RdsArgs &a, void *stream) {
   static_assert(sizeof(BitsLds) <= 16 * 1024, "k_bits LDS");
+  return fmx_launch(k_bits, dim3((a.C + 63) / 64), dim3(64), sizeof(BitsLds), static_cast<hipStream_t>(stream), a);
+}
+int launch_rds(const RdsArgs &a, void *stream) {
   // the bound events (set_launch_events): the start on k_rds, the stop on
-  // k_bits, so that the RDS timer and the stream's completion event span both
+  // k_bits, so that the timer and a completion event span both
   hipEvent_t e0 = t_ev_start, e1 = t_ev_stop;
   t_ev_start = t_ev_stop = nullptr;
-  hipStream_t st = static_cast<hipStream_t>(stream);
   set_launch_events(e0, nullptr);
-  int rc = fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), st, a);
+  int rc = launch_rds_sym(a, stream);
   if (rc != FMX_OK) return rc;
   set_launch_events(nullptr, e1);
-  return fmx_launch(k_bits, dim3((a.C + 63) / 64), dim3(64), sizeof(BitsLds), st, a);
+  return launch_bits(a, stream);
 }
 // 16-B words src -> dst (the schedule upload from mapped pinned memory)
 __global__ void k_copy16(const uint4 *src, uint4 *dst, size_t n16) {

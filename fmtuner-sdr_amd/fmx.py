@@ -17,8 +17,8 @@ FMX_BLEND_SOFT, FMX_BLEND_NORMAL, FMX_BLEND_AGGRESSIVE = 0, 1, 2
 FMX_DEEMPH_50US, FMX_DEEMPH_75US, FMX_DEEMPH_OFF = 0, 1, 2
 PARAM = dict(bandwidth_hz=1, w0_hz=2, deemphasis=3, dsp_agc=4, blend=5,
              force_mono=6, force_stereo=7, bandwidth_mode=8, deemph_us=9, deviation_hz=10)
-K_FRONTEND, K_STEREO, K_AUDIO, K_RDS, K_RS, K_PILOT, K_FRONTEND_GENERIC = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ["frontend", "stereo", "audio", "rds", "rs", "pilot", "frontend_generic"]
+K_FRONTEND, K_STEREO, K_AUDIO, K_RDS, K_RS, K_PILOT, K_FRONTEND_GENERIC, K_BITS = 0, 1, 2, 3, 4, 5, 6, 7
+KERNEL_NAMES = ["frontend", "stereo", "audio", "rds", "rs", "pilot", "frontend_generic", "bits"]
 
 
 class Config(C.Structure):

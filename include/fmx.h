@@ -38,11 +38,11 @@
 extern "C" {
 #endif
 
-/* ABI history: 7 (round 5) adds fmx_host_stats and FMX_K_FRONTEND_GENERIC (FMX_K_COUNT 7); 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+/* ABI history: 8 (round 5) adds FMX_K_BITS (FMX_K_COUNT 8); 7 (round 5) adds fmx_host_stats and FMX_K_FRONTEND_GENERIC (FMX_K_COUNT 7); 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
  * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
  * which changed that struct's size: callers must be rebuilt against this
  * header. */
-#define FMX_ABI_VERSION 7
+#define FMX_ABI_VERSION 8
 
 enum {
   FMX_OK = 0,
@@ -212,7 +212,7 @@ enum {
                          resample when process_block does not run them as kernels of their own) */
   FMX_K_STEREO = 1,   /* pilot PLL + blend + L-R matrix (one lane per channel)                 */
   FMX_K_AUDIO = 2,    /* L/R 15 kHz FIRs + 32 kHz resampler + de-emphasis + DC + clamp         */
-  FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync + biphase + block sync                     */
+  FMX_K_RDS = 3,      /* 57 kHz BPSK demod + symsync (+ biphase + block sync in fmx_rds)        */
   FMX_K_RS = 4,       /* the 240k -> 171k RDS resampler when process_block runs it as its own
                          kernel (k_rs, on the RDS stream ahead of k_rds)                        */
   FMX_K_PILOT = 5,    /* the 19 kHz pilot BPF when process_block runs it as its own kernel
@@ -220,7 +220,9 @@ enum {
   FMX_K_FRONTEND_GENERIC = 6, /* process_block's front end when it runs as the generic k_frontend
                          (calls of n < 1024 samples, unaligned IQ rows) instead of k_fe8;
                          FMX_K_FRONTEND then counts k_fe8 launches only                           */
-  FMX_K_COUNT = 7
+  FMX_K_BITS = 7,     /* process_block's RDS bit decoders (biphase, delta, block sync, groups:
+                         k_bits, on the audio stream ahead of k_audio)                          */
+  FMX_K_COUNT = 8
 };
 /* enable: 0 off, 1 every step's launches, N > 1 the launches of every N-th
  * step only (a sample: fewer event packets on the streams in the timed region) */
