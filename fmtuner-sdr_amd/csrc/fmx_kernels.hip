@@ -995,7 +995,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 // One dword per lane from a per-lane global address into LDS m0 + 4 lane
 // (LDS-DMA as inline asm: the compiler's wait-count pass does not see it, so
 // the issuing wave's own counted s_waitcnt vmcnt are the only waits and the
-// moves stay in flight across loop iterations; k_pll, k_rds)
+// moves stay in flight across loop iterations; k_rds, k_pll's first tiles)
 __device__ __forceinline__ void dma_dword(const float *src, uint32_t lds) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -1003,13 +1003,13 @@ __device__ __forceinline__ void dma_dword(const float *src, uint32_t lds) {
                : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
                : "memory");
 }
-// the same from a wave-uniform base plus a per-lane byte offset (saddr form)
+// the same from a wave-uniform base plus a per-lane byte offset (saddr form;
+// k_pll's P waves): the compiler's LDS-DMA builtin, which sets M0 itself (no
+// save / restore around each move) and, in k_pll's loop, adds no wait of its
+// own (round 5; in k_rds's loop it adds a vmcnt(0) after the moves: asm there)
 __device__ __forceinline__ void dma_dword_s(const float *base, uint32_t voff, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(base) + voff,
+                                   (__attribute__((address_space(3))) void *)(uintptr_t)__builtin_amdgcn_readfirstlane(lds), 4, 0, 0);
 }
 // three dwords per lane (12 B, landing at m0 + 12 lane) from a per-lane address
 __device__ __forceinline__ void dma_dwordx3(const float *src, uint32_t lds) {
@@ -2541,6 +2541,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int j0 = 8 * tid;
+#ifdef FMX_STAMPS // setup split (dbg[42..47], first chunk only)
+  unsigned long long su_last = st_last;
+#define FE_SETUP_STAMP(k)                                                     \
+  if (a.dbg && tid == 0) {                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+    atomicAdd(a.dbg + 42 + (k), t_ - su_last);                                \
+    su_last = t_;                                                             \
+  }
+#else
+#define FE_SETUP_STAMP(k)
+#endif
   const FmxDesign *__restrict__ D = a.des;
   const int n = a.n;
   const FmxChanParam par = a.par[c];
@@ -2589,6 +2600,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
     hx[h] = make_float2(v.x, v.y);
   }
+  FE_SETUP_STAMP(0)
   if (tid == 0) {
     sh->carry_i = a.dc_v[2 * c];
     sh->carry_q = a.dc_v[2 * c + 1];
@@ -2596,6 +2608,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     sh->fd_im = a.fd_prev[2 * c + 1];
     sh->clip = 0;
   }
+  FE_SETUP_STAMP(1)
   if (RS) {
     const float *hist = a.st_hist_rd + (size_t)c * FMX_HIST;
     for (int h = tid; h < FMX_HIST; h += 256) {
@@ -2605,6 +2618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       xl[h] = (_Float16)(v - (float)hv);
     }
   }
+  FE_SETUP_STAMP(2)
   float agc_g = 1.0f, agc_y2p = 1.0f;
   if (par.agc != 0 && tid == 0) {
     agc_g = a.agc[2 * c];
@@ -2623,6 +2637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     if (tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
     if (!rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
   }
+  FE_SETUP_STAMP(3)
   if (rs) {
     // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
     // (boundary): branch 31 on the window, branch 0 on the window shifted by
@@ -2657,14 +2672,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   // reach them).  Read where it is used (first chunk only): SGPRs are scarce.
   auto cold_k = [&]() __attribute__((always_inline)) { return (L - 1) - min(max(a.dec_valid[c], 0), L - 1); };
   dma_chunk(0, PAll0{}, PAll{});
+  FE_SETUP_STAMP(4)
   int e_pos = 0;
 
   for (int n0 = 0; n0 < n; n0 += cs) {
     const int cnt = min(cs, n - n0); // samples of this chunk (a multiple of 4)
     if (rs && tid == 0) sh->e_end = e_pos;
     // ================= decimator =================
+#ifdef FMX_STAMPS
+    // the DMA wait alone (dbg[40] first chunk, dbg[41] later chunks)
+    unsigned long long tw0_ = (a.dbg && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+    if (n0 == 0) { FE_SETUP_STAMP(5) }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
+#ifdef FMX_STAMPS
+    if (a.dbg && tid == 0) atomicAdd(a.dbg + (n0 == 0 ? 40 : 41), __builtin_amdgcn_s_memtime() - tw0_);
+#endif
     FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
     if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (cold ones: byte 128, i.e. b - 128 = 0)
       const int coldk = cold_k();

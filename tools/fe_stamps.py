@@ -58,6 +58,9 @@ tot = sum(v[:8])
 print(f"k_fe8 (thread 0 of each workgroup; {nblk} blocks after {NW} warm-up blocks)")
 for k in range(8):
     print(f"  {NAMES[k]:10s} {v[k] / tot * 100:6.1f} %  {v[k] / (Cn * nblk):10.0f} ticks/launch-WG")
+print(f"  (of which DMA wait + barrier: first chunk {v[40] / (Cn * nblk):8.0f}, later chunks {v[41] / (Cn * nblk):8.0f} ticks/launch-WG)")
+print("  setup split (ticks/launch-WG): " + ", ".join(f"{nm} {v[42 + i] / (Cn * nblk):.0f}" for i, nm in enumerate(
+    ["images+iq_hist", "carry words", "st_hist images", "agc+rds setup", "rs bank+dma issue", "to first wait"])))
 RN = ["setup+store", "dma_wait+ld", "mix", "fir", "sum+agc", "symsync", "psk+nco", "decode"]
 tot = sum(v[8:16]) or 1
 nwg = (Cn + 7) // 8
