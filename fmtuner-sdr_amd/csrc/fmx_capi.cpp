@@ -1141,7 +1141,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     h->t_rds.ev_use[h->t_rds.spec_img] = evFE;
     h->t_rds.ev_h_set[h->t_rds.spec_img] = true;
   }
-  // ---- pilot BPF (sA, after the front end; read by k_pll) ----
+  // ---- pilot BPF (after the front end; read by k_pll): on sA, or with
+  // FMX_PILOT_ON_B on sB ahead of k_pll ----
+#ifndef FMX_PILOT_ON_B
+#define FMX_PILOT_ON_B 0
+#endif
+  hipStream_t sPil = FMX_PILOT_ON_B ? h->sB : h->sA;
+  if (pil_k && FMX_PILOT_ON_B) HIP_TRY(hipStreamWaitEvent(h->sB, evFE, 0));
   if (pil_k) {
     PilotArgs p{};
     p.des = h->ddes;
@@ -1153,9 +1159,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     p.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
     p.out = h->pilot[buf];
     p.out_stride = h->cfg.block;
-    KBind t(h, FMX_K_PILOT, h->sA, h->evP[buf]);
+    KBind t(h, FMX_K_PILOT, sPil, h->evP[buf]);
     if (!FMX_SKIP(pll)) {
-      if ((rc = launch_pilot(p, h->sA)) != FMX_OK) {
+      if ((rc = launch_pilot(p, sPil)) != FMX_OK) {
         h->err = "pilot launch failed";
         return rc;
       }
@@ -1209,7 +1215,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   }
   h->evC_set[buf] = true;
   // ---- stereo PLL (sB) ----
-  HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : evFE, 0));
+  if (!(pil_k && FMX_PILOT_ON_B)) HIP_TRY(hipStreamWaitEvent(h->sB, pil_k ? h->evP[buf] : evFE, 0));
   if ((rc = launch_reset_parts(h, RSP_STEREO, h->sB)) != FMX_OK) return rc;
   if (stereo) {
     PllArgs a = pll_args(h, n, mpx, mpx_stride, buf);
@@ -1260,6 +1266,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
       a.in_l = h->lraw[buf];
       a.in_r = h->rraw[buf];
       a.in_stride = h->cfg.block;
+#ifdef FMX_AB_NO_LR // A/B only: every channel reads the first pair's rows (L2-resident)
+      a.in_stride = 0;
+#endif
       a.in_tiled = lr_tiled(h);
       a.cap = h->cfg.block;
     } else {
