@@ -1541,8 +1541,13 @@ __device__ __forceinline__ bool pulse_follows(uint32_t pos, int off, uint32_t op
 #define RDS_LPC 8                  // lanes per channel
 #define RDS_CPW (64 / RDS_LPC)     // channels per wave / workgroup
 #define RDS_SYMQ 12                // symbols queued per channel before the bit decoders run
+#ifndef RDS_PF
 #define RDS_PF 3                   // input rounds moved ahead (LDS-DMA)
+#endif
+#ifndef RDS_NR
 #define RDS_NR 4                   // input ring slots (> RDS_PF, a power of two)
+#endif
+static_assert(RDS_PF < RDS_NR && (RDS_NR & (RDS_NR - 1)) == 0 && 3 * RDS_PF <= 63, "k_rds input ring");
 static_assert(FMX_RDS_DECIM == 3 * RDS_LPC, "three samples per lane and decimation period");
 // The bit-decoder state of FmxRdsState (biphase, delta, block sync) -- the
 // only state k_rds keeps in LDS; the per-sample state lives in registers.
@@ -1915,7 +1920,8 @@ __global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
     dma_round(r + RDS_PF);
     // the moves of rounds r + 1 .. r + RDS_PF may stay in flight (anything
     // the compiler issued after them only makes the wait stricter)
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * RDS_PF)); // vmcnt(3 RDS_PF), lgkmcnt / expcnt untouched
+    // vmcnt(3 RDS_PF) (its bits 3:0 and 15:14), lgkmcnt / expcnt untouched
+    __builtin_amdgcn_s_waitcnt(0x0F70 | ((3 * RDS_PF) & 15) | (((3 * RDS_PF) >> 4) << 14));
     float xr0[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) xr0[q] = L.xin[r & (RDS_NR - 1)][q][lane];
