@@ -1122,7 +1122,10 @@ __device__ __forceinline__ void au_scan_prev(float A, float BL, float BR, float 
   __syncthreads(); // ws reusable
 }
 
-__global__ __launch_bounds__(256) void k_audio(AudioArgs a) {
+#ifndef FMX_AU_WPE
+#define FMX_AU_WPE 1 // k_audio waves per SIMD the register budget allows (A/B switch; 1 = the compiler's choice)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE))) void k_audio(AudioArgs a) {
   // dynamic LDS, as k_rds: a static 45 KB made the backend pad the VGPR
   // allocation from 111 to 129 (occupancy 3 by LDS)
   extern __shared__ __align__(16) unsigned char au_smem[];
@@ -1774,7 +1777,10 @@ __device__ __forceinline__ f32x2 rds_sum8x2(float x, float y) {
   return f32x2{x, y};
 }
 
-__global__ __launch_bounds__(64, 3) void k_rds(RdsArgs a) {
+#ifndef FMX_RDS_WPE
+#define FMX_RDS_WPE 3 // k_rds waves per SIMD the register budget allows (A/B switch)
+#endif
+__global__ __launch_bounds__(64, FMX_RDS_WPE) void k_rds(RdsArgs a) {
 #ifndef FMX_RDS_PRIO
 #define FMX_RDS_PRIO 2
 #endif
