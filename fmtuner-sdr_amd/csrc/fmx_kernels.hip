@@ -2553,12 +2553,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int j0 = 8 * tid;
-#ifdef FMX_STAMPS // setup split (dbg[42..47], first chunk only)
-  unsigned long long su_last = st_last;
+#ifdef FMX_STAMPS // setup split (dbg[42..47], first chunk only; flushed with the stage clocks)
+  unsigned long long su_last = st_last, su_acc[6] = {0, 0, 0, 0, 0, 0}, su_w0 = 0, su_w1 = 0;
 #define FE_SETUP_STAMP(k)                                                     \
   if (a.dbg && tid == 0) {                                                    \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
-    atomicAdd(a.dbg + 42 + (k), t_ - su_last);                                \
+    su_acc[k] += t_ - su_last;                                                \
     su_last = t_;                                                             \
   }
 #else
@@ -2699,7 +2699,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads(); // this chunk's DMA has landed (every wave)
 #ifdef FMX_STAMPS
-    if (a.dbg && tid == 0) atomicAdd(a.dbg + (n0 == 0 ? 40 : 41), __builtin_amdgcn_s_memtime() - tw0_);
+    if (a.dbg && tid == 0) { if (n0 == 0) su_w0 += __builtin_amdgcn_s_memtime() - tw0_; else su_w1 += __builtin_amdgcn_s_memtime() - tw0_; }
 #endif
     FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
     if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (cold ones: byte 128, i.e. b - 128 = 0)
@@ -3189,8 +3189,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   if (tid == 0 && a.clip_out) a.clip_out[c] = (float)sh->clip / (float)n;
   FE_STAMP(6)
 #ifdef FMX_STAMPS
-  if (a.dbg && tid == 0)
+  if (a.dbg && tid == 0) {
     for (int k = 0; k < 8; ++k) atomicAdd(a.dbg + k, st_acc[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(a.dbg + 42 + k, su_acc[k]);
+    atomicAdd(a.dbg + 40, su_w0);
+    atomicAdd(a.dbg + 41, su_w1);
+  }
 #endif
 #undef FE_STAMP
 #undef FE_STAMP_D
