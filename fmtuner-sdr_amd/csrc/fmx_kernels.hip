@@ -964,7 +964,7 @@ __global__ __launch_bounds__(256) void k_frontend(FeArgs a) {
 /* ================================================================== */
 /* k_pll (round 4): only the two recurrences the reference makes serial stay
  * serial, one channel per lane; everything else runs one item (channel row,
- * sample t) per lane.  A workgroup takes PLL_CH = 16 channels in tiles of
+ * sample t) per lane.  A workgroup takes CH = 16 (24) channels in tiles of
  * PLL_T = 16 samples (256 items: one 16-lane DPP row per channel in each of
  * the four P waves), so 2 048 channels are 128 workgroups and 4 096 are 256:
  *   W0 (serial)   the PLL feedback chain only: error = pilot * sin(phase),
@@ -3296,7 +3296,24 @@ int launch_frontend_m(const FeArgs &a, int M, int tpp, void *stream, bool vec) {
 }
 
 int launch_pll(const PllArgs &a, void *stream) {
-  return fmx_launch(k_pll, dim3((a.C + PLL_CH - 1) / PLL_CH), dim3(64 * PLL_WAVES), 0, static_cast<hipStream_t>(stream), a);
+  // 16 channels per workgroup while that leaves at least half the CUs
+  // without one, else 24: eight waves, two per SIMD, and a third fewer
+  // workgroups beside the other streams' (round 5: 4096 channels 0.635 ->
+  // 0.618 ms per step, 8192 1.170 -> 1.134; at 2048 24 was 0.357 -> 0.363,
+  // profiles/r05za_ab_pll_ch24.txt)
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0, v = 0;
+    n_cu = (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#ifndef FMX_PLL_CH_FORCE // A/B variants only
+  const int ch = 2 * ((a.C + 15) / 16) <= n_cu ? 16 : 24;
+#else
+  const int ch = FMX_PLL_CH_FORCE;
+#endif
+  if (ch == 16) return fmx_launch(k_pll<16>, dim3((a.C + 15) / 16), dim3(64 * PLL_WAVES(16)), 0, st, a);
+  return fmx_launch(k_pll<24>, dim3((a.C + 23) / 24), dim3(64 * PLL_WAVES(24)), 0, st, a);
 }
 int launch_audio(const AudioArgs &a, void *stream) {
   return fmx_launch(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);

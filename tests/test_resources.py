@@ -66,13 +66,16 @@ def test_front_end_register_budget(tmp_path):
 
 def test_pll_register_and_lds_budget(tmp_path):
     ks = _kernels(tmp_path)
-    hits = _find(ks, r"k_pllENS_7PllArgs")
-    assert len(hits) == 1  # one tile shape (16 channels x 16 samples, fmx_pll.inc)
+    hits = _find(ks, r"k_pllILi(16|24)EEEvNS_7PllArgs")
+    # two workgroup shapes (16 or 24 channels x 16-sample tiles, fmx_pll.inc)
+    assert len(hits) == 2, sorted(hits)
     for name, f in hits.items():
         assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 80, (name, f)
-        # LDS: the tile rings (round 4) take 31.2 KB: one k_pll workgroup beside
-        # two k_fe8 (52.4 KB each) and a k_rs (16.5 KB) in 160 KB
-        assert f.get("group_segment_fixed_size", 0) <= 32 * 1024, (name, f)
+        # LDS: the tile rings take 31.2 KB at 16 channels, 46.8 KB at 24: one
+        # k_pll workgroup beside two k_fe8 (43.3 KB each in process_block's
+        # instance) and a k_rs (16.5 KB) in 160 KB
+        lds = 32 * 1024 if "ILi16E" in name else 47 * 1024
+        assert f.get("group_segment_fixed_size", 0) <= lds, (name, f)
         assert f.get("vgpr_spill_count", 0) == 0 and f.get("private_segment_fixed_size", 0) == 0, (name, f)
 
 

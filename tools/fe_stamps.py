@@ -18,7 +18,8 @@ L = fmx.lib()
 L.fmx_debug_stamps.restype = C.c_int
 L.fmx_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
 Cn, B, M, nblk = int(os.environ.get("C", "4096")), 4096, 10, int(os.environ.get("NBLK", "4"))
-PLL_CH = int(os.environ.get("PLL_CH", "16"))  # channels per k_pll workgroup of the library under test
+# channels per k_pll workgroup (launch_pll: 16 up to 2 048 channels on 256 CUs, else 24)
+PLL_CH = int(os.environ.get("PLL_CH", "16" if int(os.environ.get("C", "4096")) <= 2048 else "24"))
 h = fmx.Handle(fmx.make_config(), Cn)
 dev = torch.device("cuda")
 scfg = fmx.make_synth(kind=2, n_bits=6000)
@@ -70,6 +71,6 @@ for k in range(8):
           f"  {v[8 + k] / (nwg * nblk) / (B * 0.7125 / 24):8.1f} per period")
 nwg = (Cn + PLL_CH - 1) // PLL_CH
 print(f"k_pll per wave (lane 0): work / barrier-wait ticks per launch-WG ({PLL_CH} channels per workgroup)")
-for w, nm in enumerate(["W0 chain", "WB blend", "P0", "P1", "P2", "P3"]):
-    wk, wt = v[16 + 2 * w], v[17 + 2 * w]
-    print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}")
+for w, nm in enumerate(["W0 chain", "WB blend", "P0", "P1", "P2", "P3", "P4", "P5"]):
+    wk, wt, vm = v[16 + 2 * w], v[17 + 2 * w], v[32 + w]
+    print(f"  {nm:14s} work {wk / (nwg * nblk):10.0f}  wait {wt / (nwg * nblk):10.0f}  (P waves: move wait {vm / (nwg * nblk):9.0f})")
