@@ -3313,6 +3313,10 @@ int launch_pll(const PllArgs &a, void *stream) {
   const int ch = FMX_PLL_CH_FORCE;
 #endif
   if (ch == 16) return fmx_launch(k_pll<16>, dim3((a.C + 15) / 16), dim3(64 * PLL_WAVES(16)), 0, st, a);
+#if defined(FMX_PLL_CH_FORCE) && FMX_PLL_CH_FORCE != 16 && FMX_PLL_CH_FORCE != 24
+  return fmx_launch(k_pll<FMX_PLL_CH_FORCE>, dim3((a.C + FMX_PLL_CH_FORCE - 1) / FMX_PLL_CH_FORCE),
+                    dim3(64 * PLL_WAVES(FMX_PLL_CH_FORCE)), 0, st, a);
+#endif
   return fmx_launch(k_pll<24>, dim3((a.C + 23) / 24), dim3(64 * PLL_WAVES(24)), 0, st, a);
 }
 int launch_audio(const AudioArgs &a, void *stream) {
