@@ -65,3 +65,24 @@ def test_synth_host_deterministic_and_per_channel(fmx):
     assert np.array_equal(a[0, 2 * 2000:], d[0])
     assert groups.shape == (3, 2000 // 104, 4)
     assert (groups[:, :, 0] == (0x1000 + np.arange(5, 8))[:, None]).all()  # PI = 0x1000 + ch
+
+
+def test_kernel_timer_ids_match_header_and_bench(fmx):
+    """fmx_kernel_times ids (FMX_K_* in include/fmx.h) against fmx.py's
+    KERNEL_NAMES order, and bench.py's per-kernel tables (design bytes per IQ
+    sample, kernel names) cover every timer: a timer added to the ABI without
+    them would break the bench line or mislabel a kernel."""
+    src = open(os.path.join(ROOT, "include", "fmx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"FMX_K_([A-Z_]+)\s*=\s*(\d+)", src)}
+    count = ids.pop("COUNT")
+    assert count == len(ids) == len(fmx.KERNEL_NAMES)
+    assert sorted(ids.values()) == list(range(count))
+    for name, k in ids.items():
+        assert fmx.KERNEL_NAMES[k] == name.lower(), (name, k)
+        assert getattr(fmx, "K_" + name) == k
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert set(bench.PER_IQ) == set(fmx.KERNEL_NAMES) == set(bench.KNAME)
