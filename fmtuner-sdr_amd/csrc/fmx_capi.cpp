@@ -1044,7 +1044,7 @@ static void step_done(Handle *h, bool stereo_hist_written) {
 //   sA: [wait evD(k-3)] [RDS schedule copy] k_fe8 -> evF(k), k_pilot -> evP(k)
 //   sC: [wait evF(k)] k_rs, k_rds -> evC(k)
 //   sB: [wait evP(k)] k_pll -> evB(k)
-//   sD: [wait evB(k), evC(k)] k_bits, [audio schedule copy] k_audio -> evD(k)
+//   sD: [wait evC(k)] k_bits, [wait evB(k)] [audio schedule copy] k_audio -> evD(k)
 // evD(k) therefore marks every reader of slot buf done (k_audio waits for
 // k_rds as well as k_pll), so the front end of step k+3 -- the next writer of
 // the slot, and through evP of the raw L/R slot k_pll writes -- needs ONE
@@ -1239,13 +1239,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   h->evB_set[buf] = true;
   // ---- audio (sD): after the PLL (stereo) / the front end (mono), and
   // after k_rds, so that evD closes the step ----
-  HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0));
-  HIP_TRY(hipStreamWaitEvent(h->sD, h->evC[buf], 0));
-  if ((rc = launch_reset_parts(h, RSP_AUDIO | RSP_BITS, h->sD)) != FMX_OK) return rc;
-  h->rl_pending.clear();
   // the RDS bit decoders (k_bits) over k_rds's symbols of slot buf, here
   // rather than behind k_rds on sC: the RDS stream's step is k_rs + k_rds
-  // only, k_bits runs beside the next step's k_rs
+  // only, k_bits runs beside the next step's k_rs.  It waits for k_rds
+  // alone, ahead of the PLL wait, so that it runs beside the tail of k_pll
+  // and k_audio starts as soon as k_pll ends
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evC[buf], 0));
+  if ((rc = launch_reset_parts(h, RSP_BITS, h->sD)) != FMX_OK) return rc;
   if (rds && !FMX_SKIP(rds)) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
@@ -1258,6 +1258,9 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
     t.launched();
   }
+  HIP_TRY(hipStreamWaitEvent(h->sD, h->evB[buf], 0));
+  if ((rc = launch_reset_parts(h, RSP_AUDIO, h->sD)) != FMX_OK) return rc;
+  h->rl_pending.clear();
   TimingSet *tau = stereo ? &h->t_af : &h->t_mono;
   if ((rc = tset_advance(h, *tau, n, buf, h->sD, nullptr)) != FMX_OK) return rc;
   {
