@@ -367,10 +367,13 @@ def main():
             h.sync()
 
     # what runs between the warmup and the timed steps is made ready first:
-    # the timing event pool (fmx_timing_enable creates 256 events) and torch's
-    # reduction kernel (its code object loads on first use).  Left to after
-    # the warmup they kept the GPU idle for ~100 ms there (rocprofv3 trace),
-    # long enough for the timed steps to start from a cold GPU
+    # the timing event pool (fmx_timing_enable creates 256 events), torch's
+    # reduction kernel (its code object loads on first use) and, at N > 1,
+    # the process group's first collective (RCCL sets up its communicator on
+    # it).  Left to after the warmup they kept the GPU idle for ~100 ms there
+    # (rocprofv3 trace), long enough for the timed steps to start from a cold GPU
+    if world > 1:
+        dist.barrier()
     if not args.no_kernel_timing:
         h.timing_enable(True, every=args.kernel_timing_every)
         h.timing_enable(False)
