@@ -76,10 +76,13 @@ def _run_gpu(fmx, torch, cfg, iq, nblk, n, params=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("iq_rate,n,noise", [(2_400_000, 4096, 0.0), (2_400_000, 1500, 0.3), (256_000, 4096, 0.1)])
+@pytest.mark.parametrize("iq_rate,n,noise", [(2_400_000, 4096, 0.0), (2_400_000, 1500, 0.3), (256_000, 4096, 0.1),
+                                             (2_400_000, 4096, 0.3), (2_048_000, 4096, 0.2), (2_400_000, 3000, 0.25)])
 def test_gpu_signal_level(fmx, oracle, torch_cuda, iq_rate, n, noise):
-    """VEC (aligned, 16-B loads), generic decimator path (ragged n) and the
-    M = 1 direct path; reference signal_level.cpp as the checker."""
+    """k_fe8 (whole and ragged chunks; its decimator-fused byte sums with the
+    near-clip counts in full waves and in the halo / partial waves' exact
+    path, at M = 10 and 8) and the M = 1 direct path; reference
+    signal_level.cpp as the checker."""
     C_, nblk = 3, 6
     M = iq_rate // (240_000 if iq_rate % 240_000 == 0 else 256_000)
     dsp = iq_rate // M
