@@ -3346,8 +3346,12 @@ struct PilLds {
   _Float16 xh[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
   _Float16 xl[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
 };
+#ifndef FMX_PILOT_PRIO
+#define FMX_PILOT_PRIO 0 // k_pilot's wave priority (s_setprio) beside the other streams' waves
+#endif
 __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
   __shared__ PilLds L;
+  if (FMX_PILOT_PRIO > 0) __builtin_amdgcn_s_setprio(FMX_PILOT_PRIO);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
