@@ -591,7 +591,8 @@ def main():
         "check": {"rds_groups_last_step": ngroups, "rds_groups_warmup": groups_warm,
                   "stereo_fraction": stereo_frac},
         # the library this run loaded (fmx.LIB_PATH; FMX_LIB selects A/B builds)
-        "library": {"path": os.path.relpath(fmx.LIB_PATH, ROOT), "sha256_16": _sha16(fmx.LIB_PATH)},
+        "library": {"path": os.path.relpath(fmx.LIB_PATH, ROOT), "sha256_16": _sha16(fmx.LIB_PATH),
+                    "build_info": fmx.build_info()},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

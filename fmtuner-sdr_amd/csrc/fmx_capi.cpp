@@ -88,6 +88,7 @@ struct TimingSet {
 struct Handle {
   fmx_config cfg{};
   int C = 0, device = 0, M = 1;
+  int n_cu = 256;  // compute units of `device` (queried at create)
   // decimator input samples every channel has seen since its last reset
   // (capped at L-1): a full history lets the frontend take its VEC path
   long dec_fill = 0;
@@ -631,9 +632,12 @@ static int launch_reset_parts(Handle *h, int part, hipStream_t s) {
 // FMX_RESET_LISTS_MAX lists of FMX_RESET_LIST channels (kernel arguments, no
 // upload) whose parts run on the stream that owns each part's state, right
 // before that stream's kernel of this step -- after the previous step's
-// kernel of the same stream, before this step's.  A reset of a handle's
-// every channel, object creation, or more channels than the lists hold take
-// the joined path (prepare).  One retune per block at 4096 channels costs
+// kernel of the same stream, before this step's.  Object creation, or more
+// channels than the lists hold (FMX_RESET_LISTS_MAX x FMX_RESET_LIST), take
+// the joined path (prepare).  Lists a failed call left with parts unlaunched
+// (an error return between the part launches below) go back into hmask whole:
+// the next call resets those channels again in every part, so no channel is
+// left half reset.  One retune per block at 4096 channels costs
 // nothing measurable: 0.638 against 0.640 ms per step (profiles/
 // r05h_retune_ab.txt); with round 4's join (and the handle on k_frontend)
 // 1.01 ms (r05d), with the join alone 0.82 (r05e).
@@ -641,6 +645,8 @@ static int launch_reset_parts(Handle *h, int part, hipStream_t s) {
 static int prepare_pipelined(Handle *h) {
   int rc = sync_params(h);
   if (rc != FMX_OK) return rc;
+  for (const ResetList &L : h->rl_pending)
+    for (int i = 0; i < L.n; ++i) h->hmask[static_cast<size_t>(L.ch[i])] |= L.m[i];
   h->rl_pending.clear();
   int cnt = 0;
   bool create = false;
@@ -769,6 +775,10 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     return FMX_E_INVALID;
   }
   HIP_TRY(hipSetDevice(device));
+  {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && v > 0) h->n_cu = v;
+  }
   h->hdes = new FmxDesign();
   int rc = design_build(*cfg, h->hdes, &h->ex, &h->err);
   if (rc != FMX_OK) return rc;
@@ -997,6 +1007,7 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
+  a.n_cu = h->n_cu;
   return a;
 }
 

@@ -24,6 +24,14 @@
 
 #include "../../include/fmx.h"
 
+#ifndef FMX_SRC_SHA
+#define FMX_SRC_SHA "unknown"
+#endif
+#ifndef FMX_KDEFS
+#define FMX_KDEFS ""
+#endif
+extern "C" const char *fmx_build_info(void) { return "src=" FMX_SRC_SHA " defs=" FMX_KDEFS; }
+
 namespace {
 
 // PI confidence of `value` over the debounce buffer (the rule of

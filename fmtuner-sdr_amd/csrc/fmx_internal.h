@@ -106,6 +106,7 @@ struct PllArgs {
   int *stereo_out, *pilot_tenths_out;
   int *indicator_out;      // [C] XDR stereo indicator (main.cpp:1298-1300), may be null
   unsigned long long *dbg; // [16] per-wave work / barrier clocks (diagnostic, FMX_STAMPS=1), may be null
+  int n_cu;                // CUs of the handle's device (launch_pll's workgroup shape)
 };
 
 struct AudioArgs {

@@ -3264,12 +3264,16 @@ namespace fmx {
 // steady state: whole 2048-sample chunks, full history, no complex
 // decimator output, 16-B pilot rows, RDS rate ratio < 0.9 (<= 8 resampler
 // outputs per thread and chunk) -> k_fe8
-// k_fe8 takes any call of n >= FE8_MIN_N samples (chunks of one size, see
-// k_fe8) on 16-B aligned IQ rows, cold or warm decimator history per channel
+// k_fe8 takes any call of n >= FE8_MIN_N samples with n % 4 == 0 (chunks
+// of one size, a multiple of 8, see k_fe8: the last chunk's length is n mod
+// 8 off a multiple of 8, and its 16-B pilot stores and f16-pair history carry
+// need a multiple of 4) on 16-B aligned IQ rows, cold or warm decimator
+// history per channel; other n (e.g. 1025 at M = 8, where every n passes the
+// IQ alignment test) take k_frontend
 static bool fe8_ok(const FeArgs &a, int M) {
   if (a.in_mode != FE_IN_U8_DECIM) return false;
   const bool aligned = ((((uintptr_t)a.iq) | (uintptr_t)a.iq_stride) & 15) == 0 && ((2L * a.n * M) & 15) == 0;
-  return aligned && a.n >= FE8_MIN_N && a.do_demod && !a.bb_out &&
+  return aligned && a.n >= FE8_MIN_N && (a.n & 3) == 0 && a.do_demod && !a.bb_out &&
          (!a.pilot_out || ((((uintptr_t)a.pilot_out) | (uintptr_t)a.pilot_stride * 4) & 15) == 0) &&
          a.des_fs >= 190000;
 }
@@ -3300,12 +3304,9 @@ int launch_pll(const PllArgs &a, void *stream) {
   // without one, else 24: eight waves, two per SIMD, and a third fewer
   // workgroups beside the other streams' (round 5: 4096 channels 0.635 ->
   // 0.618 ms per step, 8192 1.170 -> 1.134; at 2048 24 was 0.357 -> 0.363,
-  // profiles/r05za_ab_pll_ch24.txt)
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0, v = 0;
-    n_cu = (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
-  }
+  // profiles/r05za_ab_pll_ch24.txt); the CU count is the handle's device's
+  // (PllArgs::n_cu, queried once per handle at create)
+  const int n_cu = a.n_cu > 0 ? a.n_cu : 256;
   hipStream_t st = static_cast<hipStream_t>(stream);
 #ifndef FMX_PLL_CH_FORCE // A/B variants only
   const int ch = 2 * ((a.C + 15) / 16) <= n_cu ? 16 : 24;

@@ -73,6 +73,39 @@ FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
   return (s >= 4294967296.0f) ? 0u : fmx_cvt_u32(s);
 }
 
+// Forms of the stereo PLL's sine / constrain arithmetic (k_pll), chosen at
+// compile time; the shipped library is built with the defaults and
+// tests/hip/libpllmath.so sweeps whatever forms it is built with.  Round 6
+// A/B (profiles/r06a_*): see DESIGN.md section 3.
+//   FMX_PLL_CHAIN  W0's feedback sine of the word:
+//     0  round 5: the word's top 23 bits truncated (v_alignbit_b32 into a
+//        float in [1, 2)), one op; a phase bias of up to -2^-23 turn
+//     1  the same with the word carried +256 by W0 (FMX_CHAIN_TOFF): the top
+//        23 bits rounded to nearest, still one op
+//     2  round 4: (float)(int32)theta 2^-32, a signed 24-bit turn (two ops)
+//     3  (float)(uint32)theta 2^-32: the reference's own rounding of the word
+//        ((float)theta in nco_crcf_get_phase, as oracle Nco::get_phase) (two ops)
+//   FMX_WORD_SINCOS  the P waves' sine / cosine of the word (vcoI / vcoQ,
+//     cos 2 phase): 0 signed 24-bit turn, 1 (float)(uint32)theta as the reference
+//   FMX_PLL_WORDS  pll_step's constrain words: 0 truncating converts (e < 0:
+//     within 130 / 144 words of the reference's 256-word steps); 1 e < 0
+//     rounded to the reference's 256-word grid by one f32 add of 2^32
+//     (saturating converts, no compare; e >= 0 one word low)
+#ifndef FMX_PLL_CHAIN
+#define FMX_PLL_CHAIN 0
+#endif
+#ifndef FMX_WORD_SINCOS
+#define FMX_WORD_SINCOS 0
+#endif
+#ifndef FMX_PLL_WORDS
+#define FMX_PLL_WORDS 0
+#endif
+#if FMX_PLL_CHAIN == 1
+#define FMX_CHAIN_TOFF 256u
+#else
+#define FMX_CHAIN_TOFF 0u
+#endif
+
 #ifdef __HIPCC__
 // The stereo PLL's feedback chain (k_pll W0, stereo_decoder.cpp:178-192), one
 // sample: vcoQ = sin(phase) of the NCO word theta, then liquid's pll_step
@@ -83,34 +116,64 @@ FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
 // phase / double-precision constrain (tests/test_gpu_pllmath.py,
 // tests/golden/pllmath_gpu.json).
 //
-// fmx_chain_sin: v_sin_f32 takes turns; the word's top 23 bits become the
-// mantissa of a float in [1, 2) with one v_alignbit_b32 ({0x7F, theta} >> 9 =
-// 0x3F800000 | theta >> 9), so sin(2 pi (1 + theta / 2^32)) = sin(2 pi theta /
-// 2^32) up to the truncated 9 bits (< 2^-23 turn) and v_sin's own error.  One
-// VALU op instead of a convert and a multiply on the serial chain.
-__device__ __forceinline__ float fmx_chain_sin(uint32_t theta) {
-  return __builtin_amdgcn_sinf(__builtin_bit_cast(float, __builtin_amdgcn_alignbit(0x7Fu, theta, 9u)));
+// fmx_chain_sin(theta + FMX_CHAIN_TOFF) = sin(2 pi theta / 2^32): v_sin_f32
+// takes turns.  Forms 0 / 1: the word's top 23 bits become the mantissa of a
+// float in [1, 2) with one v_alignbit_b32 ({0x7F, w} >> 9 = 0x3F800000 | w >>
+// 9), so sin(2 pi (1 + w / 2^32)) = sin(2 pi w / 2^32) up to the dropped 9
+// bits and v_sin's own error -- truncated (form 0), or rounded when the word
+// is carried + 256 (form 1).  Forms 2 / 3 convert and scale.
+__device__ __forceinline__ float fmx_chain_sin(uint32_t w) {
+#if FMX_PLL_CHAIN == 2
+  return __builtin_amdgcn_sinf((float)(int32_t)w * 2.3283064365386963e-10f);
+#elif FMX_PLL_CHAIN == 3
+  return __builtin_amdgcn_sinf((float)w * 2.3283064365386963e-10f);
+#else
+  return __builtin_amdgcn_sinf(__builtin_bit_cast(float, __builtin_amdgcn_alignbit(0x7Fu, w, 9u)));
+#endif
 }
 // fmx_word_sincos: sine and cosine of an NCO word (phase 2 pi theta / 2^32)
-// by v_sin / v_cos, which take turns: the word as a signed fraction of a
-// turn in [-0.5, 0.5) (rounded to 24 bits: < 2^-25 turn).  k_pll's outputs
-// (vcoI / vcoQ of the pilot I/Q, cos 2 phase of the L-R mix,
+// by v_sin / v_cos, which take turns: form 0 the word as a signed fraction of
+// a turn in [-0.5, 0.5) (rounded to 24 bits: < 2^-25 turn), form 1 as
+// (float)theta 2^-32 in [0, 1], the reference's rounding of the word.
+// k_pll's outputs (vcoI / vcoQ of the pilot I/Q, cos 2 phase of the L-R mix,
 // stereo_decoder.cpp:178-180,194-195,218-220), swept with the chain.
 __device__ __forceinline__ void fmx_word_sincos(uint32_t theta, float *s, float *c) {
+#if FMX_WORD_SINCOS == 1
+  const float r = (float)theta * 2.3283064365386963e-10f;
+#else
   const float r = (float)(int32_t)theta * 2.3283064365386963e-10f;
+#endif
   *s = __builtin_amdgcn_sinf(r);
   *c = __builtin_amdgcn_cosf(r);
 }
+// v_cvt_u32_f32 with its hardware saturation (negative / NaN -> 0, >= 2^32 ->
+// 0xFFFFFFFF), which a C++ conversion of an out-of-range float does not promise
+__device__ __forceinline__ uint32_t fmx_cvt_u32_sat(float x) {
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // fmx_chain_words: the two constrain words of pll_step from the pilot's
 // pre-products pa = pilot alpha/2pi 2^32, pb = pilot beta/2pi 2^32 (one packed
-// multiply by vcoQ, then truncating converts): for |e k| < 1/2 the word
+// multiply by vcoQ).  Form 0, truncating converts: for |e k| < 1/2 the word
 // constrain(e k) = frac(e k / 2 pi) 2^32 equals (uint32)(int32)(e k / 2 pi 2^32)
-// up to the float roundings, which the sweep bounds.
+// up to the float roundings (and, for e < 0, the reference's rounding of
+// 1 + frac to 24 bits), which the sweep bounds.  Form 1: x = e k / 2 pi 2^32
+// as two saturating converts, cvt(x) + cvt(x + 2^32): for x < 0 the first is
+// 0 and the second the f32 sum 2^32 + x rounded to the 256-word grid, which
+// is the reference's (float)(fpart + 1) 2^32; for x >= 0 the second
+// saturates to 2^32 - 1, so the word is trunc(x) - 1.
 __device__ __forceinline__ void fmx_chain_words(float pa, float pb, float vcoQ, uint32_t *ca, uint32_t *cb) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 x = f2{pa, pb} * f2{vcoQ, vcoQ};
+#if FMX_PLL_WORDS == 1
+  const f2 y = x + f2{4294967296.0f, 4294967296.0f};
+  *ca = fmx_cvt_u32_sat(x.x) + fmx_cvt_u32_sat(y.x);
+  *cb = fmx_cvt_u32_sat(x.y) + fmx_cvt_u32_sat(y.y);
+#else
   *ca = (uint32_t)(int32_t)x.x;
   *cb = (uint32_t)(int32_t)x.y;
+#endif
 }
 #endif
 

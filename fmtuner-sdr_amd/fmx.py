@@ -76,6 +76,7 @@ def lib():
     L = C.CDLL(LIB_PATH)
     vp, i, sz, fp = C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_float)
     sig = {
+        "fmx_build_info": (C.c_char_p, []),
         "fmx_device_count": (i, []),
         "fmx_create": (i, [C.POINTER(Config), i, i, C.POINTER(vp)]),
         "fmx_destroy": (i, [vp]),
@@ -120,6 +121,11 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def build_info():
+    """fmx_build_info(): "src=<sources' SHA-256, 16 hex> defs=<variant defines>"."""
+    return lib().fmx_build_info().decode()
 
 
 def make_config(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=4096,

@@ -116,6 +116,14 @@ typedef struct {
                               stereo && pilot >= 2.0 kHz), main.cpp:1298-1300 */
 } fmx_block_out;
 
+/* ---- build record ----
+ * "src=<16 hex> defs=<A/B defines>": the first 16 hex digits of the SHA-256
+ * of the sources this library was compiled from (fmtuner-sdr_amd/Makefile
+ * FMX_SRC_SHA: csrc/, include/fmx.h, include/fmx_blocks.hpp and the Makefile,
+ * concatenated in sorted path order) and the variant defines (empty for the
+ * shipped library).  __graft_entry__.smoke() checks it against the tree. */
+const char *fmx_build_info(void);
+
 /* ---- lifetime ---- */
 int fmx_device_count(void);
 int fmx_create(const fmx_config *cfg, int n_channels, int device, void **handle);

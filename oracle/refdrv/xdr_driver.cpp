@@ -21,9 +21,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
-#include <chrono>
 #include <string>
-#include <thread>
 #include <vector>
 
 namespace refdrv {
@@ -119,13 +117,15 @@ int ref_xdr_session(const uint16_t *groups, const uint8_t *errors, int n, const 
     if (!refdrv::read_line(fd, buf, line)) return fail(-3);
     if (line == "I1000,0") break;
   }
-  // batches of groups (the server queue keeps 256 lines), each closed by a
-  // sentinel scan line.  The client loop (xdr_server.cpp:808-844) takes the
-  // RDS queue and the scan queue under two locks in one pass: a pass that
-  // reads the RDS queue while a batch is still being pushed can send the
-  // batch's sentinel before the batch's tail, which then arrives (in order)
-  // before the next batch's lines.  So after the last batch a second sentinel
-  // is pushed after a pause longer than a loop pass: every RDS line precedes it.
+  // batches of groups (the server queue keeps 256 lines), each closed by two
+  // sentinel scan lines.  The client loop (xdr_server.cpp:802-844) sends, per
+  // pass, the RDS queue's new lines and then the scan queue's: a pass that
+  // read the RDS queue while a batch was still being pushed can send the
+  // batch's first sentinel before the batch's tail.  The second sentinel is
+  // pushed only after the first has arrived, i.e. after the pass that sent it
+  // ended, and every updateRDS of the batch came before that pass's scan read,
+  // so the pass that sends the second sentinel reads the whole rest of the
+  // batch first: every RDS line of the batch precedes it (no wall-clock wait).
   auto drain_to = [&](const std::string &sentinel) -> bool {
     for (;;) {
       if (!refdrv::read_line(fd, buf, line)) return false;
@@ -141,18 +141,17 @@ int ref_xdr_session(const uint16_t *groups, const uint8_t *errors, int n, const 
       got.push_back(line);
     }
   };
+  auto flush = [&](const std::string &s) -> bool {
+    srv.pushScanLine(s + "-a");
+    if (!drain_to(s + "-a")) return false;
+    srv.pushScanLine(s + "-b");
+    return drain_to(s + "-b");
+  };
   constexpr int kBatch = 100;
   for (int g0 = 0, k = 0; g0 < n; g0 += kBatch, ++k) {
     for (int g = g0; g < std::min(n, g0 + kBatch); ++g)
       srv.updateRDS(groups[4 * g], groups[4 * g + 1], groups[4 * g + 2], groups[4 * g + 3], errors[g]);
-    const std::string s = "#fmx-batch-" + std::to_string(k);
-    srv.pushScanLine(s);
-    if (!drain_to(s)) return fail(-3);
-  }
-  if (n > 0) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(250));
-    srv.pushScanLine("#fmx-rds-end");
-    if (!drain_to("#fmx-rds-end")) return fail(-3);
+    if (!flush("#fmx-batch-" + std::to_string(k))) return fail(-3);
   }
   const char *sp = scan;
   for (int i = 0; i < nscan; ++i) {

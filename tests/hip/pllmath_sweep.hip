@@ -45,14 +45,17 @@ __device__ void wave_sum(double v, double *dst) {
 
 // mx[0] chain sin vs the reference float phase, [1] vs the exact phase,
 // [2] / [3] word sin / cos vs the reference float phase, [4] / [5] vs exact;
-// sums[0] signed chain-sine error vs exact (its bias), sums[1] |error|
+// sums[0] signed chain-sine error vs exact (its bias), sums[1] |error|,
+// sums[2] the error times cos of the exact phase: over all words, sum / 2^31
+// is the chain sine's mean PHASE error in radians (a truncated word lags by
+// half its dropped bits; the PLL locks to that lag)
 __global__ void k_sine(uint64_t w0, uint64_t count, unsigned *mx, double *sums) {
   float m[6] = {0, 0, 0, 0, 0, 0};
-  double bias = 0.0, mag = 0.0;
+  double bias = 0.0, mag = 0.0, pbias = 0.0;
   const uint64_t gsz = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gsz) {
     const uint32_t th = (uint32_t)(w0 + i);
-    const float cs = fmx_chain_sin(th);
+    const float cs = fmx_chain_sin(th + FMX_CHAIN_TOFF); // the word as W0 carries it
     float ws, wc;
     fmx_word_sincos(th, &ws, &wc);
     const double ph = (double)fmx_nco_phase_ref(th);
@@ -67,10 +70,12 @@ __global__ void k_sine(uint64_t w0, uint64_t count, unsigned *mx, double *sums) 
     m[5] = fmaxf(m[5], (float)fabs((double)wc - ec));
     bias += (double)cs - es;
     mag += fabs((double)cs - es);
+    pbias += ((double)cs - es) * ec;
   }
   for (int k = 0; k < 6; ++k) wave_max(m[k], mx + k);
   wave_sum(bias, sums);
   wave_sum(mag, sums + 1);
+  wave_sum(pbias, sums + 2);
 }
 
 // every positive float bit pattern in [b0, b0 + nb) as the pilot, both signs,
@@ -110,10 +115,12 @@ extern "C" {
 
 // out[0..5]: sine maxima (see k_sine), out[6]: mean signed chain-sine error,
 // out[7]: mean |chain-sine error|, out[8]: words swept; out[9..14]: word
-// maxima (see k_words), out[15]: (pilot, vcoQ) pairs checked.  Returns 0, or
-// a negative HIP error.
+// maxima (see k_words), out[15]: (pilot, vcoQ) pairs checked, out[16]: the
+// chain sine's mean phase error (radians, see k_sine), out[17..19]: the forms
+// built (FMX_PLL_CHAIN, FMX_WORD_SINCOS, FMX_PLL_WORDS).  Returns 0, or a
+// negative HIP error.
 int pllmath_sweep(float alpha, float beta, double *out, int nout) {
-  if (nout < 16) return -100;
+  if (nout < 20) return -100;
   unsigned *d_mx = nullptr;
   double *d_sum = nullptr;
   float *d_vq = nullptr;
@@ -122,10 +129,10 @@ int pllmath_sweep(float alpha, float beta, double *out, int nout) {
   const int nvq = (int)(sizeof(vq) / sizeof(vq[0]));
   hipError_t e;
   if ((e = hipMalloc(&d_mx, sizeof(unsigned) * (kNS + kNW))) != hipSuccess) return -(int)e;
-  if ((e = hipMalloc(&d_sum, sizeof(double) * 2)) != hipSuccess) return -(int)e;
+  if ((e = hipMalloc(&d_sum, sizeof(double) * 3)) != hipSuccess) return -(int)e;
   if ((e = hipMalloc(&d_vq, sizeof(vq))) != hipSuccess) return -(int)e;
   hipMemset(d_mx, 0, sizeof(unsigned) * (kNS + kNW));
-  hipMemset(d_sum, 0, sizeof(double) * 2);
+  hipMemset(d_sum, 0, sizeof(double) * 3);
   hipMemcpy(d_vq, vq, sizeof(vq), hipMemcpyHostToDevice);
   const uint64_t words = 1ull << 32;
   hipLaunchKernelGGL(k_sine, dim3(8192), dim3(256), 0, 0, (uint64_t)0, words, d_mx, d_sum);
@@ -134,7 +141,7 @@ int pllmath_sweep(float alpha, float beta, double *out, int nout) {
   hipLaunchKernelGGL(k_words, dim3(8192), dim3(256), 0, 0, b0, nb, d_vq, nvq, alpha, beta, d_mx + kNS);
   if ((e = hipDeviceSynchronize()) != hipSuccess) return -(int)e;
   unsigned mx[kNS + kNW];
-  double sums[2];
+  double sums[3];
   hipMemcpy(mx, d_mx, sizeof(mx), hipMemcpyDeviceToHost);
   hipMemcpy(sums, d_sum, sizeof(sums), hipMemcpyDeviceToHost);
   hipFree(d_mx);
@@ -147,6 +154,10 @@ int pllmath_sweep(float alpha, float beta, double *out, int nout) {
   out[8] = (double)words;
   for (int k = 0; k < 6; ++k) out[9 + k] = f(kNS + k);
   out[15] = (double)nb * 2.0 * nvq;
+  out[16] = sums[2] / 2147483648.0;
+  out[17] = FMX_PLL_CHAIN;
+  out[18] = FMX_WORD_SINCOS;
+  out[19] = FMX_PLL_WORDS;
   return 0;
 }
 

@@ -53,3 +53,22 @@ def test_block_size_on_k_fe8(fmx, oracle, torch_cuda, n):
     assert kt["frontend"][1] == nblk and kt["frontend_generic"][1] == 0, kt  # the cold first block too
     for c in range(C):
         check(g, outs[c], c, nblk, tag=f"fe8_block_{n}")
+
+
+@pytest.mark.parametrize("n", [1025, 1028, 3001])
+def test_m8_block_sizes_front_end_choice(fmx, oracle, torch_cuda, n):
+    """M = 8 (2.048 MS/s, the reference's own rate): every n passes k_fe8's
+    IQ-row alignment test there, but its last chunk needs n % 4 == 0
+    (ADVICE r5): 1028 runs on k_fe8 (a last chunk of 4 mod 8), 1025 and 3001
+    on the generic k_frontend; all three against the oracle."""
+    C, nblk = 3, 10
+    kw = dict(iq_rate=2_048_000, dsp_rate=256_000, block=n)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=2_048_000, M=8, B=n)
+    kt = {}
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk, ktimes=kt)
+    if n % 4 == 0:
+        assert kt["frontend"][1] == nblk and kt["frontend_generic"][1] == 0, kt
+    else:
+        assert kt["frontend_generic"][1] == nblk and kt["frontend"][1] == 0, kt
+    for c in range(C):
+        check(g, outs[c], c, nblk, tag=f"m8_block_{n}")

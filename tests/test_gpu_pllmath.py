@@ -29,11 +29,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tests", "hip", "libpllmath.so")
+# FMX_PLLMATH_LIB: a sweep built with other forms (A/B only, tests/hip variant)
+LIB = os.environ.get("FMX_PLLMATH_LIB") or os.path.join(ROOT, "tests", "hip", "libpllmath.so")
 GOLD = os.path.join(ROOT, "tests", "golden", "pllmath_gpu.json")
 KEYS = ["chain_sin_vs_ref_phase", "chain_sin_vs_exact", "word_sin_vs_ref_phase", "word_cos_vs_ref_phase",
         "word_sin_vs_exact", "word_cos_vs_exact", "chain_sin_mean_err", "chain_sin_mean_abs_err", "words",
-        "ca_max_pos", "cb_max_pos", "ca_max_neg", "cb_max_neg", "ca_rel_max", "cb_rel_max", "pairs"]
+        "ca_max_pos", "cb_max_pos", "ca_max_neg", "cb_max_neg", "ca_rel_max", "cb_rel_max", "pairs",
+        "chain_phase_bias", "form_chain", "form_word_sincos", "form_words"]
 # absolute bounds (radian-free: sine units; words: units of 2^-32 turn)
 BOUNDS = {
     # v_sin of the word's top 23 bits as a float in [1, 2): < 2^-23 turn of
@@ -58,11 +60,11 @@ def sweep():
     L = C.CDLL(LIB)
     L.pllmath_sweep.restype = C.c_int
     L.pllmath_sweep.argtypes = [C.c_float, C.c_float, C.POINTER(C.c_double), C.c_int]
-    out = (C.c_double * 16)()
+    out = (C.c_double * len(KEYS))()
     # the design's PLL constants (fmx_design.cpp: bandwidth 0.01, beta = sqrt)
     alpha = np.float32(0.01)
     beta = np.sqrt(alpha, dtype=np.float32)
-    rc = L.pllmath_sweep(C.c_float(alpha), C.c_float(beta), out, 16)
+    rc = L.pllmath_sweep(C.c_float(alpha), C.c_float(beta), out, len(KEYS))
     assert rc == 0, rc
     return {k: out[i] for i, k in enumerate(KEYS)}
 
