@@ -1990,6 +1990,18 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
         }
       break;
     }
+    case 14: { // k_fe8's flat LDS tap window (dec_q16) against the A fragments: 1 where the entry process_block's
+               // decimator reads for (K step, lane, element, hi / lo) equals dec_frag's, for every K step it runs
+      const int M = d->M, KS = (15 * M + d->dec_len + 1 + 31) / 32;
+      for (int ks = 0; ks < KS; ++ks)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j)
+            for (int sh = 0; sh < 2; ++sh) {
+              const int i = 32 * ks + 8 * (l >> 4) + j + 15 * M - M * (l & 15);
+              v.push_back(i >= 0 && i < FMX_DEC_QN && d->dec_q16[sh][i] == d->dec_frag[ks][sh][l][j] ? 1.0f : 0.0f);
+            }
+      break;
+    }
     default: delete d; return FMX_E_INVALID;
   }
   delete d;

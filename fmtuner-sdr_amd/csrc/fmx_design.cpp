@@ -237,6 +237,13 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
           d->dec_frag[ks][0][l][j] = hi;
           d->dec_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
         }
+    for (int i = 0; i < FMX_DEC_QN; ++i) {
+      const int dd = i - 15 * M;
+      const float q = (dd >= 1 && dd <= L) ? d->dec_taps[L - dd] * 65536.0f : 0.0f;
+      const uint16_t hi = f32_to_f16_bits(q);
+      d->dec_q16[0][i] = hi;
+      d->dec_q16[1][i] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+    }
     d->dec_dc16 = static_cast<float>(-0.5 * 65536.0 * dc);
     d->dec_scale16 = d->dec_scale * (1.0f / 65536.0f);
   } else {

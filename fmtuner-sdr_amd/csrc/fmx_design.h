@@ -28,6 +28,7 @@
 #define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
 #define FMX_DEC_KS_MAX 16    // K steps of the f16 MFMA decimator: ceil((15 M + L + 1) / 32)
+#define FMX_DEC_QN (15 * 10 + 32 * FMX_DEC_KS_MAX) // entries of the flat decimator tap window (M <= 10)
 #define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
 #define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
 
@@ -56,6 +57,12 @@ typedef struct {
   // y = (acc - dec_dc16) * dec_scale16, dec_dc16 = -2^16 sum(taps) / 2 (the
   // 127.5 centre of the bytes entering as b - 128), dec_scale16 = dec_scale 2^-16
   uint16_t dec_frag[FMX_DEC_KS_MAX][2][64][8] __attribute__((aligned(16)));
+  // the same q as one flat window (round 6): dec_q16[s][i] = q[i - 15 M] (hi,
+  // lo), so that lane l's fragment at K step ks is the 8 entries from
+  // 32 ks + 8 (l >> 4) + 15 M - M (l & 15) on; process_block's k_fe8 copies
+  // the window (1.2 KB at M = 10) into LDS once per workgroup and reads its
+  // fragments there instead of dec_frag's 2 KB per K step from L2
+  uint16_t dec_q16[2][FMX_DEC_QN] __attribute__((aligned(16)));
   float dec_dc16, dec_scale16;
   // FMDemod IQ FIR designs (fm_demod.cpp:168-204) and discriminator gain
   int iq_len[FMX_IQ_DESIGNS];

@@ -2467,7 +2467,15 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   static constexpr int RST = (TL32 + 32 * 4 + 15) & ~15;             // RDS resampler bank [33][27] float2
   static constexpr int SG = (RST + (RS ? RS_PAIRS * RS_M * 8 : 0) + 15) & ~15;
   static constexpr int SH = SG + 4 * 6 * 8;
-  static constexpr int BYTES = SH + (int)sizeof(FeShared);
+  // RS = false (process_block's variant, round 6): the decimator's tap
+  // window FmxDesign::dec_q16 (hi, lo: QN entries each) in LDS, read as the
+  // A fragments instead of dec_frag from L2 (RS = true keeps dec_frag: no
+  // LDS to spare beside its images and resampler bank)
+  static constexpr int KS = (15 * M + L + 1 + 31) / 32;
+  static constexpr int QN = 15 * M + 32 * KS;
+  static constexpr int QT = (SH + (int)sizeof(FeShared) + 15) & ~15;
+  static constexpr int BYTES = QT + (RS ? 0 : 2 * QN * 2);
+  static_assert(M % 2 == 0 && QN % 2 == 0 && QN <= FMX_DEC_QN, "dword-aligned fragment reads inside the window");
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
   // (fe8_stg order), in the raw region once every wave has read it; read
@@ -2650,6 +2658,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     if (!rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
   }
   FE_SETUP_STAMP(3)
+  if (!RS) { // the decimator's tap window (read after the first chunk's DMA barrier)
+    const uint32_t *qs = reinterpret_cast<const uint32_t *>(&D->dec_q16[0][0]);
+    uint32_t *qd = reinterpret_cast<uint32_t *>(smem + LY::QT);
+    for (int h = tid; h < LY::QN / 2; h += 256) {
+      qd[h] = qs[h];
+      qd[LY::QN / 2 + h] = qs[FMX_DEC_QN / 2 + h];
+    }
+  }
   if (rs) {
     // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
     // (boundary): branch 31 on the window, branch 0 on the window shifted by
@@ -2756,15 +2772,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
       typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
       typedef float f32x4_t __attribute__((ext_vector_type(4)));
-      constexpr int KS = (15 * M + L + 1 + 31) / 32;
+      constexpr int KS = LY::KS;
       static_assert(KS <= FMX_DEC_KS_MAX, "decimator K steps");
       const int col = lane & 15, g = lane >> 4;
-      const int d00 = 8 * g - M * col;             // tap offset of this lane's A fragment at K step 0 (even)
-      // A fragments from the design (FmxDesign::dec_frag, 16-B per lane, one
-      // K step ahead) instead of 8 dword LDS reads per K step
+      // A fragments, one K step ahead: RS = false from the LDS tap window (8
+      // consecutive f16 from 32 ks + 8 g + 15 M - M col, an even index: four
+      // dwords, two ds_read2_b32 per half -- round 5 read dec_frag from L2,
+      // 2 KB per wave and K step, and every K step waited on that load), RS =
+      // true from the design's fragment table (16 B per lane)
+      const uint32_t *qh = reinterpret_cast<const uint32_t *>(smem + LY::QT) + (15 * M + 8 * g - M * col) / 2;
+      const uint32_t *ql = qh + LY::QN / 2;
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag[0][0][0][0]) + lane;
-      u32x4 fh = fa[0], fl = fa[64];
-      (void)d00;
+      auto frag = [&](int ks, int s) __attribute__((always_inline)) {
+        if (RS) return fa[128 * ks + 64 * s];
+        const uint32_t *q = (s ? ql : qh) + 16 * ks;
+        return u32x4{q[0], q[1], q[2], q[3]};
+      };
+      u32x4 fh = frag(0, 0), fl = frag(0, 1);
       const unsigned char *rb = raw + 32 * M * (32 * wave + col) + 16 * g;
       f32x4_t acc[2][2];
 #pragma unroll
@@ -2775,16 +2799,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
         return __builtin_bit_cast(f16x2_t, __builtin_amdgcn_perm(0x64646464u, w, sel)) -
                f16x2_t{(_Float16)1152.0f, (_Float16)1152.0f};
       };
+      // software pipeline (round 6): the next K step's operands -- its bytes
+      // (two ds_read_b128) and fragments -- are issued before this step's
+      // conversions and MFMAs, which hide their latency (the scheduling
+      // barrier keeps the compiler from sinking them back to their uses)
+      u32x4 wcur[2], wnxt[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wnxt[u] = wcur[u] = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u);
 #pragma unroll 7
       for (int ks = 0; ks < KS; ++ks) {
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, fh), alo = __builtin_bit_cast(f16x8_t, fl);
         if (ks + 1 < KS) {
-          fh = fa[128 * (ks + 1)];
-          fl = fa[128 * (ks + 1) + 64];
+          fh = frag(ks + 1, 0);
+          fl = frag(ks + 1, 1);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) wnxt[u] = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * (ks + 1));
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const u32x4 w = *reinterpret_cast<const u32x4 *>(rb + 512 * M * u + 64 * ks);
+          const u32x4 w = wcur[u];
           const f16x2_t i0 = cvt(w.x, 0x04020400u), i1 = cvt(w.y, 0x04020400u);
           const f16x2_t i2 = cvt(w.z, 0x04020400u), i3 = cvt(w.w, 0x04020400u);
           const f16x2_t q0 = cvt(w.x, 0x04030401u), q1 = cvt(w.y, 0x04030401u);
@@ -2799,6 +2833,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
           acc[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bi, alo, acc[u][0], 0, 0, 0);
           acc[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq, alo, acc[u][1], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) wcur[u] = wnxt[u];
       }
       FE_STAMP_D(2)
       __syncthreads(); // every wave is past raw: its outputs go to the (aliased) staging area

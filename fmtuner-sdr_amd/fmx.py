@@ -64,6 +64,7 @@ class SynthConfig(C.Structure):
 
 
 _lib = None
+_OPTIONAL = {"fmx_build_info"}
 
 
 def lib():
@@ -116,6 +117,8 @@ def lib():
         "fmx_iq_replay": (i, [C.c_char_p, C.c_longlong, i, vp]),
     }
     for name, (res, args) in sig.items():
+        if name in _OPTIONAL and not hasattr(L, name):
+            continue  # an older library (A/B runs against a past revision)
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -125,7 +128,8 @@ def lib():
 
 def build_info():
     """fmx_build_info(): "src=<sources' SHA-256, 16 hex> defs=<variant defines>"."""
-    return lib().fmx_build_info().decode()
+    L = lib()
+    return L.fmx_build_info().decode() if hasattr(L, "fmx_build_info") else "n/a (library without fmx_build_info)"
 
 
 def make_config(iq_rate=2_400_000, dsp_rate=240_000, out_rate=32_000, block=4096,

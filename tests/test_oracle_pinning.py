@@ -279,6 +279,21 @@ def test_mfma_decimator_tap_tables(fmx, rates):
 
 
 @pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_decimator_lds_window(fmx, rates):
+    """process_block's k_fe8 (round 6) reads its decimator A fragments from
+    one flat f16 hi / lo tap window in LDS (FmxDesign::dec_q16) instead of
+    dec_frag: every entry it reads -- each K step, lane, element, hi and lo --
+    is bit-identical to the fragment table's, so the MFMAs and the outputs
+    are unchanged."""
+    if rates["iq_rate"] == rates["dsp_rate"]:
+        pytest.skip("no decimator")
+    cfg = fmx.make_config(**rates)
+    eq = fmx.design_taps(cfg, 14)
+    assert eq.size >= 64 * 8 * 2 * 4 and eq.size % (64 * 8 * 2) == 0
+    assert np.all(eq == 1.0), np.flatnonzero(eq != 1.0)[:10]
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
 def test_mfma_pilot_tap_fragments(fmx, rates):
     """k_fe8's MFMA pilot BPF takes its taps as f16 hi + lo fragments (x 2^12,
     FmxDesign::pilot_frag): they give the float taps back to 22 bits."""
