@@ -2002,6 +2002,27 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
             }
       break;
     }
+    case 15: { // k_pilot's flat LDS tap window (pilot_q16) against pilot_frag, as case 14
+      for (int ks = 0; ks < d->pilot_ks; ++ks)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j)
+            for (int sh = 0; sh < 2; ++sh) {
+              const int base = 32 * ks + 8 * (l >> 4) + 15 - (l & 15), c = base & 1, i = base - c + j;
+              v.push_back(i >= 0 && i < FMX_PILOT_QN && d->pilot_q16[c][sh][i] == d->pilot_frag[ks][sh][l][j] ? 1.0f : 0.0f);
+            }
+      break;
+    }
+    case 16: { // k_fe8's flat LDS IQ FIR windows (iq_q16) against iq_frag, every design, as case 15
+      for (int i = 0; i < FMX_IQ_DESIGNS; ++i)
+        for (int ks = 0; ks < d->iq_ks[i]; ++ks)
+          for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j)
+              for (int sh = 0; sh < 2; ++sh) {
+                const int base = 32 * ks + 8 * (l >> 4) + 15 - (l & 15), c = base & 1, e = base - c + j;
+                v.push_back(e >= 0 && e < FMX_IQ_QN && d->iq_q16[i][c][sh][e] == d->iq_frag[i][ks][sh][l][j] ? 1.0f : 0.0f);
+              }
+      break;
+    }
     default: delete d; return FMX_E_INVALID;
   }
   delete d;

@@ -394,6 +394,15 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
           d->iq_frag[i][ks][0][l][j] = hi;
           d->iq_frag[i][ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
         }
+    for (int c = 0; c < 2; ++c)
+      for (int e = 0; e < FMX_IQ_QN; ++e) {
+        const int dd = e + c - 15;
+        const int k = P8 - 1 - dd;
+        const float q = (dd < 32 * d->iq_ks[i] && k >= 0 && k < P) ? d->iq_taps[i][k] * 4096.0f : 0.0f;
+        const uint16_t hi = f32_to_f16_bits(q);
+        d->iq_q16[i][c][0][e] = hi;
+        d->iq_q16[i][c][1][e] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+      }
   }
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_z16[k + 16] = d->pilot_taps[k];
   for (int k = 0; k < d->pilot_len; ++k) d->pilot_pad[k + 5] = d->pilot_taps[k];
@@ -411,6 +420,15 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
           d->pilot_frag[ks][0][l][j] = hi;
           d->pilot_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
         }
+    for (int c = 0; c < 2; ++c)
+      for (int i = 0; i < FMX_PILOT_QN; ++i) {
+        const int dd = i + c - 15;
+        const int k = P8 - 1 - dd;
+        const float q = (dd < 32 * d->pilot_ks && k >= 0 && k < P) ? d->pilot_taps[k] * 4096.0f : 0.0f;
+        const uint16_t hi = f32_to_f16_bits(q);
+        d->pilot_q16[c][0][i] = hi;
+        d->pilot_q16[c][1][i] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+      }
   }
   for (int k = 0; k + 1 < FMX_PILOT_MAX + FMX_PAD; ++k) {
     d->pilot_pair[k][0] = d->pilot_pad[k];

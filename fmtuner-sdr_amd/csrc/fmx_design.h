@@ -31,6 +31,8 @@
 #define FMX_DEC_QN (15 * 10 + 32 * FMX_DEC_KS_MAX) // entries of the flat decimator tap window (M <= 10)
 #define FMX_PILOT_KS_MAX 17  // K steps of the MFMA pilot BPF for up to FMX_PILOT_MAX taps
 #define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
+#define FMX_PILOT_QN (32 * FMX_PILOT_KS_MAX + 16) // entries of the flat pilot tap window
+#define FMX_IQ_QN (32 * FMX_IQ_KS_MAX + 16)       // entries of a flat IQ FIR tap window
 
 typedef struct {
   float x, y;
@@ -74,6 +76,9 @@ typedef struct {
   // 2^12 as f16 hi + lo, iq_ks[i] = ceil((P8 + 15) / 32) K steps
   int iq_ks[FMX_IQ_DESIGNS];
   uint16_t iq_frag[FMX_IQ_DESIGNS][FMX_IQ_KS_MAX][2][64][8] __attribute__((aligned(16)));
+  // the same per design as a flat window for process_block's k_fe8 (round 6),
+  // laid out as pilot_q16: iq_q16[i][c][s][e] = q[e + c - 15]
+  uint16_t iq_q16[FMX_IQ_DESIGNS][2][2][FMX_IQ_QN] __attribute__((aligned(16)));
   float fd_ref;          // 1 / (2 pi kf), kf = 75 kHz / Fs
   float deemph_alpha[2]; // 50 us, 75 us at out_rate (fm_demod.cpp:119-131)
   // StereoDecoder (stereo_decoder.cpp:25-63)
@@ -88,6 +93,10 @@ typedef struct {
   // h[P8 - 1 - d] (P8 = fir8 length, 8k + 1, leading zero taps)
   int pilot_ks; // K steps: ceil((P8 + 15) / 32)
   uint16_t pilot_frag[FMX_PILOT_KS_MAX][2][64][8] __attribute__((aligned(16)));
+  // the same q as a flat window for k_pilot's LDS (round 6): pilot_q16[c][s][i]
+  // = q[i + c - 15] (copy c = 1 shifted by one entry, so that every lane's 8
+  // entries, from 32 ks + 8 (l >> 4) + 15 - (l & 15), start on a dword)
+  uint16_t pilot_q16[2][2][FMX_PILOT_QN] __attribute__((aligned(16)));
   float lr_scale;
   float lr_taps[FMX_LR_LEN];
   // k_audio's MFMA L/R FIR fragments, as pilot_frag: taps * 2^12 as f16 hi +

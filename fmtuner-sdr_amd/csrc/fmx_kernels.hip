@@ -2474,7 +2474,9 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   static constexpr int KS = (15 * M + L + 1 + 31) / 32;
   static constexpr int QN = 15 * M + 32 * KS;
   static constexpr int QT = (SH + (int)sizeof(FeShared) + 15) & ~15;
-  static constexpr int BYTES = QT + (RS ? 0 : 2 * QN * 2);
+  // and the channel's IQ FIR design's window FmxDesign::iq_q16 [2][2][FMX_IQ_QN]
+  static constexpr int QI = QT + (RS ? 0 : 2 * QN * 2);
+  static constexpr int BYTES = QI + (RS ? 0 : 2 * 2 * FMX_IQ_QN * 2);
   static_assert(M % 2 == 0 && QN % 2 == 0 && QN <= FMX_DEC_QN, "dword-aligned fragment reads inside the window");
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
@@ -2665,6 +2667,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       qd[h] = qs[h];
       qd[LY::QN / 2 + h] = qs[FMX_DEC_QN / 2 + h];
     }
+    static_assert(FMX_IQ_QN % 2 == 0, "dword copy");
+    const uint32_t *is = reinterpret_cast<const uint32_t *>(&D->iq_q16[par.iqsel][0][0][0]);
+    uint32_t *id = reinterpret_cast<uint32_t *>(smem + LY::QI);
+    for (int h = tid; h < 2 * FMX_IQ_QN; h += 256) id[h] = is[h];
   }
   if (rs) {
     // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
@@ -2963,14 +2969,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       const f16x8_t *bqh = reinterpret_cast<const f16x8_t *>(xqh + xb);
       const f16x8_t *bql = reinterpret_cast<const f16x8_t *>(xql + xb);
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->iq_frag[par.iqsel][0][0][0][0]) + lane;
+      // RS = false: A fragments from the design's LDS window (round 6), this
+      // lane's 8 entries from 32 ks + 8 g + 15 - col in copy (15 - col) & 1
+      const int qb = 8 * g + 15 - col, qc = qb & 1;
+      const uint32_t *qih = reinterpret_cast<const uint32_t *>(smem + LY::QI) + qc * FMX_IQ_QN + (qb - qc) / 2;
+      const uint32_t *qil = qih + FMX_IQ_QN / 2;
+      auto ifrag = [&](int ks, int s) __attribute__((always_inline)) {
+        if (RS) return fa[128 * ks + 64 * s];
+        const uint32_t *q = (s ? qil : qih) + 16 * ks;
+        return u32x4{q[0], q[1], q[2], q[3]};
+      };
       f32x4_t ai[2], aq[2];
       ai[0] = ai[1] = aq[0] = aq[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-      u32x4 ah = fa[0], al = fa[64];
+      u32x4 ah = ifrag(0, 0), al = ifrag(0, 1);
       for (int ks = 0; ks < KSI; ++ks) {
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
         if (ks + 1 < KSI) {
-          ah = fa[128 * (ks + 1)];
-          al = fa[128 * (ks + 1) + 64];
+          ah = ifrag(ks + 1, 0);
+          al = ifrag(ks + 1, 1);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -3377,12 +3393,17 @@ int launch_audio(const AudioArgs &a, void *stream) {
  * the window halo a neighbour loaded is an L2 hit. */
 #define PIL_TPW 4                  // 256-output tiles per wave: one tap-fragment load feeds PIL_TPW MFMA chains
 #define PIL_SEG (4 * 256 * PIL_TPW) // outputs per workgroup
+#ifndef FMX_PILOT_QLDS
+#define FMX_PILOT_QLDS 1 // A fragments from the LDS tap window (round 6; 0: pilot_frag from L2, A/B)
+#endif
 struct PilLds {
   // sample s0 - FMX_HIST + i at [i]: the history (previous call's MPX rows
   // for s < 0), the segment, 32 zero-slack samples (read by K steps past the
   // filter, against zero taps)
   _Float16 xh[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
   _Float16 xl[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
+  // the tap window FmxDesign::pilot_q16 ([copy][hi, lo][entry])
+  uint16_t q[FMX_PILOT_QLDS ? 2 : 0][2][FMX_PILOT_QN] __attribute__((aligned(16)));
 };
 #ifndef FMX_PILOT_PRIO
 #define FMX_PILOT_PRIO 0 // k_pilot's wave priority (s_setprio) beside the other streams' waves
@@ -3439,6 +3460,15 @@ __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
     *reinterpret_cast<f16x4_t *>(&L.xh[i]) = hv;
     *reinterpret_cast<f16x4_t *>(&L.xl[i]) = lv;
   }
+  const int QW = 32 * KSP + 16; // window entries the K steps reach
+  if (FMX_PILOT_QLDS) {
+    static_assert(FMX_PILOT_QN % 2 == 0, "dword copy");
+    for (int h = tid; h < 2 * 2 * (QW / 2); h += 256) {
+      const int cs = h / (QW / 2), e = h % (QW / 2); // (copy, split) pair, dword
+      reinterpret_cast<uint32_t *>(&L.q[0][0][0])[cs * (FMX_PILOT_QN / 2) + e] =
+          reinterpret_cast<const uint32_t *>(&D->pilot_q16[0][0][0])[cs * (FMX_PILOT_QN / 2) + e];
+    }
+  }
   __syncthreads();
   // tiles PIL_TPW w + u: 16 outputs (rows, A = taps, FmxDesign::pilot_frag)
   // of 16 blocks of 16 outputs (columns, B = MPX), K = P8 + 15 inputs
@@ -3447,15 +3477,25 @@ __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
   const f16x8_t *bh = reinterpret_cast<const f16x8_t *>(&L.xh[xb]);
   const f16x8_t *bl = reinterpret_cast<const f16x8_t *>(&L.xl[xb]);
   const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->pilot_frag[0][0][0][0]) + lane;
+  // (FMX_PILOT_QLDS) this lane's 8 window entries from 32 ks + 8 g + 15 - col:
+  // in copy (15 - col) & 1 they start on an even entry, four dwords
+  const int qb = 8 * g + 15 - col, qc = qb & 1;
+  const uint32_t *qh = reinterpret_cast<const uint32_t *>(&L.q[0][0][0]) + qc * FMX_PILOT_QN + (qb - qc) / 2;
+  const uint32_t *ql = qh + FMX_PILOT_QN / 2;
+  auto frag = [&](int ks, int s) __attribute__((always_inline)) {
+    if (!FMX_PILOT_QLDS) return fa[128 * ks + 64 * s];
+    const uint32_t *q = (s ? ql : qh) + 16 * ks;
+    return u32x4{q[0], q[1], q[2], q[3]};
+  };
   f32x4_t acc[PIL_TPW];
 #pragma unroll
   for (int u = 0; u < PIL_TPW; ++u) acc[u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-  u32x4 ah = fa[0], al = fa[64];
+  u32x4 ah = frag(0, 0), al = frag(0, 1);
   for (int ks = 0; ks < KSP; ++ks) {
     const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
     if (ks + 1 < KSP) {
-      ah = fa[128 * (ks + 1)];
-      al = fa[128 * (ks + 1) + 64];
+      ah = frag(ks + 1, 0);
+      al = frag(ks + 1, 1);
     }
 #pragma unroll
     for (int u = 0; u < PIL_TPW; ++u) {

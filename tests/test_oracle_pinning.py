@@ -294,6 +294,29 @@ def test_mfma_decimator_lds_window(fmx, rates):
 
 
 @pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_pilot_lds_window(fmx, rates):
+    """k_pilot (round 6) reads its A fragments from a flat f16 hi / lo tap
+    window in LDS (FmxDesign::pilot_q16, two copies one entry apart so that
+    every lane's 8 entries start on a dword): every entry it reads is
+    bit-identical to pilot_frag's."""
+    cfg = fmx.make_config(**rates)
+    eq = fmx.design_taps(cfg, 15)
+    assert eq.size >= 64 * 8 * 2 * 8 and eq.size % (64 * 8 * 2) == 0
+    assert np.all(eq == 1.0), np.flatnonzero(eq != 1.0)[:10]
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
+def test_mfma_iq_fir_lds_windows(fmx, rates):
+    """process_block's k_fe8 (round 6) reads the IQ FIR's A fragments from
+    the channel's design's flat tap window in LDS (FmxDesign::iq_q16), for
+    every W0 / XDR-bandwidth design: bit-identical to iq_frag."""
+    cfg = fmx.make_config(**rates)
+    eq = fmx.design_taps(cfg, 16)
+    assert eq.size >= 31 * 3 * 64 * 8 * 2 and eq.size % (64 * 8 * 2) == 0
+    assert np.all(eq == 1.0), np.flatnonzero(eq != 1.0)[:10]
+
+
+@pytest.mark.parametrize("rates", CONFIGS)
 def test_mfma_pilot_tap_fragments(fmx, rates):
     """k_fe8's MFMA pilot BPF takes its taps as f16 hi + lo fragments (x 2^12,
     FmxDesign::pilot_frag): they give the float taps back to 22 bits."""
