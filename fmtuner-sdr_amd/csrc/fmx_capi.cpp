@@ -98,6 +98,7 @@ struct Handle {
   // one lane per channel, a few SIMDs) and step k-1's audio still run; the
   // audio of step k overlaps the PLL of step k+1 (raw L/R double-buffered).
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
+  hipStream_t sP = nullptr; // k_pilot's stream: sA, or its own (FMX_PILOT_STREAM A/B)
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
   hipEvent_t evP[FMX_NBUF] = {}; // k_pilot (sA, after k_fe8): k_pll's input
   hipEvent_t evF[FMX_FRING] = {}; // process_block's front end of step k: evF[k % FMX_FRING]
@@ -726,6 +727,7 @@ static void destroy(Handle *h) {
   if (h->sB) hipStreamSynchronize(h->sB);
   if (h->sC) hipStreamSynchronize(h->sC);
   if (h->sD) hipStreamSynchronize(h->sD);
+  if (h->sP) hipStreamSynchronize(h->sP);
   for (auto &p : h->pending) {
     hipEventDestroy(p.a);
     if (p.b_pool) hipEventDestroy(p.b);
@@ -746,6 +748,7 @@ static void destroy(Handle *h) {
   if (h->evTmpC) hipEventDestroy(h->evTmpC);
   if (h->evTmpD) hipEventDestroy(h->evTmpD);
   if (h->evTmpU) hipEventDestroy(h->evTmpU);
+  if (h->sP && h->sP != h->sA) hipStreamDestroy(h->sP);
   if (h->sD && h->sD != h->sA) hipStreamDestroy(h->sD);
   if (h->sC && h->sC != h->sA) hipStreamDestroy(h->sC);
   if (h->sB && h->sB != h->sA) hipStreamDestroy(h->sB);
@@ -814,12 +817,17 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     HIP_TRY(hipStreamCreateWithPriority(&h->sA, hipStreamNonBlocking, hi));
   }
 #endif
+#ifndef FMX_PILOT_STREAM
+#define FMX_PILOT_STREAM 0 // A/B: k_pilot on a fifth stream (after the front end's event) instead of sA
+#endif
   if (serial) {
-    h->sB = h->sC = h->sD = h->sA;
+    h->sB = h->sC = h->sD = h->sP = h->sA;
   } else {
     HIP_TRY(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&h->sC, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&h->sD, hipStreamNonBlocking));
+    h->sP = h->sA;
+    if (FMX_PILOT_STREAM) HIP_TRY(hipStreamCreateWithFlags(&h->sP, hipStreamNonBlocking));
   }
   for (int b = 0; b < FMX_NBUF; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(true)));
@@ -1164,8 +1172,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
 #ifndef FMX_PILOT_ON_B
 #define FMX_PILOT_ON_B 0
 #endif
-  hipStream_t sPil = FMX_PILOT_ON_B ? h->sB : h->sA;
-  if (pil_k && FMX_PILOT_ON_B) HIP_TRY(hipStreamWaitEvent(h->sB, evFE, 0));
+  hipStream_t sPil = FMX_PILOT_ON_B ? h->sB : h->sP;
+  if (pil_k && (FMX_PILOT_ON_B || sPil != h->sA)) HIP_TRY(hipStreamWaitEvent(sPil, evFE, 0));
   if (pil_k) {
     PilotArgs p{};
     p.des = h->ddes;

@@ -90,7 +90,8 @@ FMX_HD uint32_t fmx_nco_constrain_ref(float x) {
 //   FMX_PLL_WORDS  pll_step's constrain words: 0 truncating converts (e < 0:
 //     within 130 / 144 words of the reference's 256-word steps); 1 e < 0
 //     rounded to the reference's 256-word grid by one f32 add of 2^32
-//     (saturating converts, no compare; e >= 0 one word low)
+//     (saturating converts, no compare; e >= 0 one word low); 3 the alpha
+//     (frequency) word as 1, the beta (phase) word as 0
 #ifndef FMX_PLL_CHAIN
 #define FMX_PLL_CHAIN 0
 #endif
@@ -163,6 +164,7 @@ __device__ __forceinline__ uint32_t fmx_cvt_u32_sat(float x) {
 // 0 and the second the f32 sum 2^32 + x rounded to the 256-word grid, which
 // is the reference's (float)(fpart + 1) 2^32; for x >= 0 the second
 // saturates to 2^32 - 1, so the word is trunc(x) - 1.
+// (form 3: the alpha word as form 1, the beta word as form 0)
 __device__ __forceinline__ void fmx_chain_words(float pa, float pb, float vcoQ, uint32_t *ca, uint32_t *cb) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 x = f2{pa, pb} * f2{vcoQ, vcoQ};
@@ -170,10 +172,44 @@ __device__ __forceinline__ void fmx_chain_words(float pa, float pb, float vcoQ, 
   const f2 y = x + f2{4294967296.0f, 4294967296.0f};
   *ca = fmx_cvt_u32_sat(x.x) + fmx_cvt_u32_sat(y.x);
   *cb = fmx_cvt_u32_sat(x.y) + fmx_cvt_u32_sat(y.y);
+#elif FMX_PLL_WORDS == 3
+  *ca = fmx_cvt_u32_sat(x.x) + fmx_cvt_u32_sat(x.x + 4294967296.0f);
+  *cb = (uint32_t)(int32_t)x.y;
 #else
   *ca = (uint32_t)(int32_t)x.x;
   *cb = (uint32_t)(int32_t)x.y;
 #endif
+}
+// fmx_chain_step: one sample's pll_step + step on the carried words, with
+// the words of fmx_chain_words: dtheta += ca; theta += dtheta(old) + ca + cb
+// (theta + dtheta is off the chain).  Form 1 / 3 sum the saturating
+// converts straight into the words with v_add3_u32 (no separate word sums).
+__device__ __forceinline__ void fmx_chain_step(float pa, float pb, float vcoQ, uint32_t &theta, uint32_t &dtheta) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 x = f2{pa, pb} * f2{vcoQ, vcoQ};
+  const uint32_t T = theta + dtheta; // off the chain
+  uint32_t tn;
+#if FMX_PLL_WORDS == 1
+  const f2 y = x + f2{4294967296.0f, 4294967296.0f};
+  const uint32_t a0 = fmx_cvt_u32_sat(x.x), a1 = fmx_cvt_u32_sat(y.x);
+  const uint32_t b0 = fmx_cvt_u32_sat(x.y), b1 = fmx_cvt_u32_sat(y.y);
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(dtheta) : "v"(dtheta), "v"(a0), "v"(a1));
+  uint32_t s;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(s) : "v"(T), "v"(a0), "v"(a1));
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(s), "v"(b0), "v"(b1));
+#elif FMX_PLL_WORDS == 3
+  const uint32_t a0 = fmx_cvt_u32_sat(x.x), a1 = fmx_cvt_u32_sat(x.x + 4294967296.0f);
+  const uint32_t cb = (uint32_t)(int32_t)x.y;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(dtheta) : "v"(dtheta), "v"(a0), "v"(a1));
+  uint32_t s;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(s) : "v"(T), "v"(a0), "v"(a1));
+  tn = s + cb;
+#else
+  const uint32_t ca = (uint32_t)(int32_t)x.x, cb = (uint32_t)(int32_t)x.y;
+  dtheta += ca;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(T), "v"(ca), "v"(cb));
+#endif
+  theta = tn;
 }
 #endif
 

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 200 
 rc=$?; tail -4 $O/tests_r06b.log; [ $rc -le 1 ] || exit $rc
 bash tools/pll_forms_ab.sh cur c1 c2 c3 c3w c1w > $O/pllab_summary.txt 2>&1; rc=$?
 cat $O/pllab_summary.txt; [ $rc -le 1 ] || exit $rc
-FMX_AB_ARGS="--channels 2048" timeout -k 10 600 bash tools/gpu_abn.sh 3 20 r05 cur c1 c2 c3 c3w > $O/ab2048_r06b.txt 2>&1 || exit 3
+FMX_AB_ARGS="--channels 2048" timeout -k 10 600 bash tools/gpu_abn.sh 3 20 r05 cur nopq c1 c3 c3w > $O/ab2048_r06b.txt 2>&1 || exit 3
 tail -7 $O/ab2048_r06b.txt
-timeout -k 10 600 bash tools/gpu_abn.sh 3 20 r05 cur c1 c2 c3 c3w > $O/ab4096_r06b.txt 2>&1 || exit 3
+timeout -k 10 600 bash tools/gpu_abn.sh 3 20 r05 cur nopq c1 c3 c3w > $O/ab4096_r06b.txt 2>&1 || exit 3
 tail -7 $O/ab4096_r06b.txt
