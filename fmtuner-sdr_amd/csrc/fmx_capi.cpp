@@ -101,6 +101,7 @@ struct Handle {
   hipStream_t sP = nullptr; // k_pilot's stream: sA, or its own (FMX_PILOT_STREAM A/B)
   hipEvent_t evA[FMX_NBUF] = {}, evB[FMX_NBUF] = {}, evC[FMX_NBUF] = {}, evD[FMX_NBUF] = {};
   hipEvent_t evP[FMX_NBUF] = {}; // k_pilot (sA, after k_fe8): k_pll's input
+  hipEvent_t evR[FMX_NBUF] = {}; // k_rs on sA (FMX_RS_ON_A_MAXC): k_rds's input
   hipEvent_t evF[FMX_FRING] = {}; // process_block's front end of step k: evF[k % FMX_FRING]
   // host waits on pinned-image reuse (fmx_host_stats): waits, waits that
   // found the event pending (the host blocked), milliseconds blocked
@@ -740,7 +741,7 @@ static void destroy(Handle *h) {
   }
   for (void *p : h->allocs) hipFree(p);
   for (int b = 0; b < FMX_NBUF; ++b)
-    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evP[b]})
+    for (hipEvent_t e : {h->evA[b], h->evB[b], h->evC[b], h->evD[b], h->evP[b], h->evR[b]})
       if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->evF)
     if (e) hipEventDestroy(e);
@@ -833,6 +834,7 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     HIP_TRY(hipEventCreateWithFlags(&h->evA[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evB[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evP[b], ev_flags(true)));
+    HIP_TRY(hipEventCreateWithFlags(&h->evR[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evC[b], ev_flags(true)));
     HIP_TRY(hipEventCreateWithFlags(&h->evD[b], ev_flags(true)));
   }
@@ -1195,38 +1197,47 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     }
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
-  HIP_TRY(hipStreamWaitEvent(h->sC, evFE, 0));
+  // (FMX_RS_ON_A_MAXC: up to that many channels k_rs runs on sA behind
+  // k_pilot instead, so that the RDS stream holds only k_rds -- A/B)
+#ifndef FMX_RS_ON_A_MAXC
+#define FMX_RS_ON_A_MAXC 0
+#endif
+  const bool rs_on_a = rds && use_rs && h->C <= FMX_RS_ON_A_MAXC && h->sA != h->sC;
+  auto run_rs = [&](hipStream_t s, hipEvent_t done) -> int {
+    RsArgs r{};
+    r.des = h->ddes;
+    r.C = h->C;
+    r.n = n;
+    r.mpx = mpx;
+    r.mpx_stride = mpx_stride;
+    r.win = h->rds_win[buf];
+    r.sched = h->t_rds.d_sched[h->t_rds.cur];
+    r.sched_n = h->t_rds.d_count[h->t_rds.cur];
+    r.group = h->t_rds.d_group[h->t_rds.cur];
+    r.sched_stride = h->t_rds.stride;
+    r.out = h->rds_in[buf];
+    r.out_stride = h->rds_stride;
+    // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
+    r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
+    KBind t(h, FMX_K_RS, s, done);
+    if (!FMX_SKIP(rds)) {
+      if (launch_rs(r, s) != FMX_OK) {
+        h->err = "rds resampler launch failed";
+        return FMX_E_HIP;
+      }
+      t.launched();
+    }
+    return FMX_OK;
+  };
+  if (rs_on_a && (rc = run_rs(h->sA, h->evR[buf])) != FMX_OK) return rc;
+  HIP_TRY(hipStreamWaitEvent(h->sC, rs_on_a ? h->evR[buf] : evFE, 0));
   if ((rc = launch_reset_parts(h, RSP_RDS, h->sC)) != FMX_OK) return rc;
   if (rds) {
     RdsArgs a = rds_args(h, buf);
     a.groups = o->d_groups;
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
-    if (use_rs) {
-      RsArgs r{};
-      r.des = h->ddes;
-      r.C = h->C;
-      r.n = n;
-      r.mpx = mpx;
-      r.mpx_stride = mpx_stride;
-      r.win = h->rds_win[buf];
-      r.sched = h->t_rds.d_sched[h->t_rds.cur];
-      r.sched_n = h->t_rds.d_count[h->t_rds.cur];
-      r.group = h->t_rds.d_group[h->t_rds.cur];
-      r.sched_stride = h->t_rds.stride;
-      r.out = h->rds_in[buf];
-      r.out_stride = h->rds_stride;
-      // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
-      r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
-      KBind t(h, FMX_K_RS, h->sC, nullptr);
-      if (!FMX_SKIP(rds)) {
-        if ((rc = launch_rs(r, h->sC)) != FMX_OK) {
-          h->err = "rds resampler launch failed";
-          return rc;
-        }
-        t.launched();
-      }
-    }
+    if (use_rs && !rs_on_a && (rc = run_rs(h->sC, nullptr)) != FMX_OK) return rc;
     KBind t(h, FMX_K_RDS, h->sC, h->evC[buf]);
     if (!FMX_SKIP(rds)) {
       if ((rc = launch_rds_sym(a, h->sC)) != FMX_OK) {
@@ -2029,6 +2040,16 @@ int fmx_design_taps(const fmx_config *cfg, int which, float *out, int cap) {
                 const int base = 32 * ks + 8 * (l >> 4) + 15 - (l & 15), c = base & 1, e = base - c + j;
                 v.push_back(e >= 0 && e < FMX_IQ_QN && d->iq_q16[i][c][sh][e] == d->iq_frag[i][ks][sh][l][j] ? 1.0f : 0.0f);
               }
+      break;
+    }
+    case 17: { // k_audio's flat LDS L/R FIR window (lr_q16) against lr_frag, as case 15
+      for (int ks = 0; ks < FMX_LR_KS; ++ks)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j)
+            for (int sh = 0; sh < 2; ++sh) {
+              const int base = 32 * ks + 8 * (l >> 4) + 15 - (l & 15), c = base & 1, e = base - c + j;
+              v.push_back(e >= 0 && e < FMX_LR_QN && d->lr_q16[c][sh][e] == d->lr_frag[ks][sh][l][j] ? 1.0f : 0.0f);
+            }
       break;
     }
     default: delete d; return FMX_E_INVALID;

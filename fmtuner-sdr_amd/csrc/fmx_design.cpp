@@ -450,6 +450,14 @@ int design_build(const fmx_config &cfg, FmxDesign *d, DesignExtras *ex, std::str
           d->lr_frag[ks][0][l][j] = hi;
           d->lr_frag[ks][1][l][j] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
         }
+    for (int c = 0; c < 2; ++c)
+      for (int e = 0; e < FMX_LR_QN; ++e) {
+        const int k = P8 - 1 - (e + c - 15);
+        const float q = (k >= 0 && k < P) ? d->lr_taps[k] * 4096.0f : 0.0f;
+        const uint16_t hi = f32_to_f16_bits(q);
+        d->lr_q16[c][0][e] = hi;
+        d->lr_q16[c][1][e] = f32_to_f16_bits(q - f16_bits_to_f32(hi));
+      }
   }
   for (int k = 0; k + 1 < FMX_LR_LEN + FMX_PAD; ++k) {
     d->lr_pair[k][0] = d->lr_pad[k];

@@ -33,6 +33,7 @@
 #define FMX_IQ_KS_MAX 5      // K steps of the MFMA IQ FIR for up to FMX_IQ_MAXLEN taps
 #define FMX_PILOT_QN (32 * FMX_PILOT_KS_MAX + 16) // entries of the flat pilot tap window
 #define FMX_IQ_QN (32 * FMX_IQ_KS_MAX + 16)       // entries of a flat IQ FIR tap window
+#define FMX_LR_QN (32 * FMX_LR_KS + 16)           // entries of the flat L/R FIR tap window
 
 typedef struct {
   float x, y;
@@ -102,6 +103,9 @@ typedef struct {
   // k_audio's MFMA L/R FIR fragments, as pilot_frag: taps * 2^12 as f16 hi +
   // lo, lr_frag[ks][s][l][j] = q[32 ks + 8 (l >> 4) + j - (l & 15)]
   uint16_t lr_frag[FMX_LR_KS][2][64][8] __attribute__((aligned(16)));
+  // the same q as a flat window for k_audio's LDS (round 6), as pilot_q16:
+  // lr_q16[c][s][e] = q[e + c - 15]
+  uint16_t lr_q16[2][2][FMX_LR_QN] __attribute__((aligned(16)));
   float lr_pad[FMX_LR_LEN + FMX_PAD];
   float lr_pair[FMX_LR_LEN + FMX_PAD][2] __attribute__((aligned(8)));
   float nominal, pll_min, pll_max, pll_alpha, pll_beta;

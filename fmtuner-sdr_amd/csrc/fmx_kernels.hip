@@ -1061,6 +1061,7 @@ struct AuShared {
   float ws[3][4][2];                           // scan scratch (A, BL, BR per wave)
   float iir[4];                                // de_L, de_R, dc_L, dc_R
   int eb, ee, count;
+  uint16_t lrq[2][2][FMX_LR_QN] __attribute__((aligned(16))); // the L/R FIR tap window (FmxDesign::lr_q16)
 };
 
 // DPP move of x (CTRL, rows ROWS); lanes that receive nothing get id
@@ -1184,6 +1185,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE)
       S.hT[nn][b] = D->af_h[k];
     }
   }
+  if (lrfir) { // the L/R FIR tap window (read after the chunk loop's first barrier)
+    static_assert(FMX_LR_QN % 2 == 0, "dword copy");
+    for (int h = tid; h < 2 * FMX_LR_QN; h += 256)
+      reinterpret_cast<uint32_t *>(&S.lrq[0][0][0])[h] = reinterpret_cast<const uint32_t *>(&D->lr_q16[0][0][0])[h];
+  }
   if (tid == 0) {
     S.eb = 0;
     S.count = 0;
@@ -1273,16 +1279,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE)
       const f16x8_t *bLl = reinterpret_cast<const f16x8_t *>(im + AU_IMG + xb);
       const f16x8_t *bRh = reinterpret_cast<const f16x8_t *>(im + 2 * AU_IMG + xb);
       const f16x8_t *bRl = reinterpret_cast<const f16x8_t *>(im + 3 * AU_IMG + xb);
-      const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->lr_frag[0][0][0][0]) + lane;
+      // A fragments from the LDS tap window (round 6; lr_frag's per-K-step
+      // L2 loads before): this lane's 8 entries from 32 ks + 8 g + 15 - col
+      // in copy (15 - col) & 1, four dwords
+      const int qb = 8 * g + 15 - col, qc = qb & 1;
+      const uint32_t *qh = reinterpret_cast<const uint32_t *>(&S.lrq[0][0][0]) + qc * FMX_LR_QN + (qb - qc) / 2;
+      const uint32_t *ql = qh + FMX_LR_QN / 2;
+      auto frag = [&](int ks, const uint32_t *q) __attribute__((always_inline)) {
+        return u32x4{q[16 * ks], q[16 * ks + 1], q[16 * ks + 2], q[16 * ks + 3]};
+      };
       f32x4_t aL[2], aR[2];
       aL[0] = aL[1] = aR[0] = aR[1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-      u32x4 ah = fa[0], al = fa[64];
+      u32x4 ah = frag(0, qh), al = frag(0, ql);
 #pragma unroll
       for (int ks = 0; ks < FMX_LR_KS; ++ks) {
         const f16x8_t ahi = __builtin_bit_cast(f16x8_t, ah), alo = __builtin_bit_cast(f16x8_t, al);
         if (ks + 1 < FMX_LR_KS) {
-          ah = fa[128 * (ks + 1)];
-          al = fa[128 * (ks + 1) + 64];
+          ah = frag(ks + 1, qh);
+          al = frag(ks + 1, ql);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {

@@ -181,13 +181,14 @@ __device__ __forceinline__ void fmx_chain_words(float pa, float pb, float vcoQ, 
 #endif
 }
 // fmx_chain_step: one sample's pll_step + step on the carried words, with
-// the words of fmx_chain_words: dtheta += ca; theta += dtheta(old) + ca + cb
-// (theta + dtheta is off the chain).  Form 1 / 3 sum the saturating
-// converts straight into the words with v_add3_u32 (no separate word sums).
+// the words of fmx_chain_words: dtheta += ca; theta += dtheta(new) + cb --
+// the reference's order (pll_step adds ca to dtheta and cb to theta, step
+// then adds the updated dtheta), so that theta's update is one v_add3_u32 of
+// the updated dtheta and no theta + dtheta is formed.  Form 1 / 3 sum the
+// saturating converts straight into dtheta with v_add3_u32.
 __device__ __forceinline__ void fmx_chain_step(float pa, float pb, float vcoQ, uint32_t &theta, uint32_t &dtheta) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 x = f2{pa, pb} * f2{vcoQ, vcoQ};
-  const uint32_t T = theta + dtheta; // off the chain
   uint32_t tn;
 #if FMX_PLL_WORDS == 1
   const f2 y = x + f2{4294967296.0f, 4294967296.0f};
@@ -195,19 +196,17 @@ __device__ __forceinline__ void fmx_chain_step(float pa, float pb, float vcoQ, u
   const uint32_t b0 = fmx_cvt_u32_sat(x.y), b1 = fmx_cvt_u32_sat(y.y);
   asm("v_add3_u32 %0, %1, %2, %3" : "=v"(dtheta) : "v"(dtheta), "v"(a0), "v"(a1));
   uint32_t s;
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(s) : "v"(T), "v"(a0), "v"(a1));
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(s), "v"(b0), "v"(b1));
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(s) : "v"(theta), "v"(dtheta), "v"(b0));
+  tn = s + b1;
 #elif FMX_PLL_WORDS == 3
   const uint32_t a0 = fmx_cvt_u32_sat(x.x), a1 = fmx_cvt_u32_sat(x.x + 4294967296.0f);
   const uint32_t cb = (uint32_t)(int32_t)x.y;
   asm("v_add3_u32 %0, %1, %2, %3" : "=v"(dtheta) : "v"(dtheta), "v"(a0), "v"(a1));
-  uint32_t s;
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(s) : "v"(T), "v"(a0), "v"(a1));
-  tn = s + cb;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(theta), "v"(dtheta), "v"(cb));
 #else
   const uint32_t ca = (uint32_t)(int32_t)x.x, cb = (uint32_t)(int32_t)x.y;
   dtheta += ca;
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(T), "v"(ca), "v"(cb));
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(tn) : "v"(theta), "v"(dtheta), "v"(cb));
 #endif
   theta = tn;
 }

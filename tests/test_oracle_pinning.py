@@ -316,6 +316,14 @@ def test_mfma_iq_fir_lds_windows(fmx, rates):
     assert np.all(eq == 1.0), np.flatnonzero(eq != 1.0)[:10]
 
 
+def test_mfma_lr_fir_lds_window(fmx):
+    """k_audio (round 6) reads the L/R FIR's A fragments from a flat tap
+    window in LDS (FmxDesign::lr_q16): bit-identical to lr_frag."""
+    eq = fmx.design_taps(fmx.make_config(), 17)
+    assert eq.size == 5 * 64 * 8 * 2
+    assert np.all(eq == 1.0), np.flatnonzero(eq != 1.0)[:10]
+
+
 @pytest.mark.parametrize("rates", CONFIGS)
 def test_mfma_pilot_tap_fragments(fmx, rates):
     """k_fe8's MFMA pilot BPF takes its taps as f16 hi + lo fragments (x 2^12,
