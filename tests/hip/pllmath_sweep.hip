@@ -81,8 +81,12 @@ __global__ void k_sine(uint64_t w0, uint64_t count, unsigned *mx, double *sums) 
 // every positive float bit pattern in [b0, b0 + nb) as the pilot, both signs,
 // times vq[0 .. nvq): word differences (int32) of ca / cb against the
 // reference; mx[0] / [1] |d ca| / |d cb| for e >= 0, [2] / [3] for e < 0,
-// [4] / [5] |d| relative to max(|ref word|, 2^10)
-__global__ void k_words(uint32_t b0, uint32_t nb, const float *vq, int nvq, float alpha, float beta, unsigned *mx) {
+// [4] / [5] |d| relative to max(|ref word|, 2^10); sums[0] / [1] the sums of
+// |d ca| / |d cb| over the e < 0 pairs (their mean: the typical word error,
+// where the maxima show only the worst case)
+__global__ void k_words(uint32_t b0, uint32_t nb, const float *vq, int nvq, float alpha, float beta, unsigned *mx,
+                        double *sums) {
+  double sa = 0.0, sb = 0.0;
   const float ka = alpha * 0.159154943091895f, kb = beta * 0.159154943091895f; // as k_pll W0
   const float kaw = ka * 4294967296.0f, kbw = kb * 4294967296.0f;
   float m[6] = {0, 0, 0, 0, 0, 0};
@@ -101,12 +105,18 @@ __global__ void k_words(uint32_t b0, uint32_t nb, const float *vq, int nvq, floa
         const int o = (e < 0.0f) ? 2 : 0;
         m[o] = fmaxf(m[o], da);
         m[o + 1] = fmaxf(m[o + 1], db);
+        if (e < 0.0f) {
+          sa += (double)da;
+          sb += (double)db;
+        }
         m[4] = fmaxf(m[4], da / fmaxf(fabsf((float)(int32_t)ra), 1024.0f));
         m[5] = fmaxf(m[5], db / fmaxf(fabsf((float)(int32_t)rb), 1024.0f));
       }
     }
   }
   for (int k = 0; k < 6; ++k) wave_max(m[k], mx + k);
+  wave_sum(sa, sums);
+  wave_sum(sb, sums + 1);
 }
 
 } // namespace
@@ -117,10 +127,11 @@ extern "C" {
 // out[7]: mean |chain-sine error|, out[8]: words swept; out[9..14]: word
 // maxima (see k_words), out[15]: (pilot, vcoQ) pairs checked, out[16]: the
 // chain sine's mean phase error (radians, see k_sine), out[17..19]: the forms
-// built (FMX_PLL_CHAIN, FMX_WORD_SINCOS, FMX_PLL_WORDS).  Returns 0, or a
-// negative HIP error.
+// built (FMX_PLL_CHAIN, FMX_WORD_SINCOS, FMX_PLL_WORDS), out[20..21]: the
+// mean |d ca| / |d cb| over the e < 0 pairs.  Returns 0, or a negative HIP
+// error.
 int pllmath_sweep(float alpha, float beta, double *out, int nout) {
-  if (nout < 20) return -100;
+  if (nout < 22) return -100;
   unsigned *d_mx = nullptr;
   double *d_sum = nullptr;
   float *d_vq = nullptr;
@@ -129,19 +140,19 @@ int pllmath_sweep(float alpha, float beta, double *out, int nout) {
   const int nvq = (int)(sizeof(vq) / sizeof(vq[0]));
   hipError_t e;
   if ((e = hipMalloc(&d_mx, sizeof(unsigned) * (kNS + kNW))) != hipSuccess) return -(int)e;
-  if ((e = hipMalloc(&d_sum, sizeof(double) * 3)) != hipSuccess) return -(int)e;
+  if ((e = hipMalloc(&d_sum, sizeof(double) * 5)) != hipSuccess) return -(int)e;
   if ((e = hipMalloc(&d_vq, sizeof(vq))) != hipSuccess) return -(int)e;
   hipMemset(d_mx, 0, sizeof(unsigned) * (kNS + kNW));
-  hipMemset(d_sum, 0, sizeof(double) * 3);
+  hipMemset(d_sum, 0, sizeof(double) * 5);
   hipMemcpy(d_vq, vq, sizeof(vq), hipMemcpyHostToDevice);
   const uint64_t words = 1ull << 32;
   hipLaunchKernelGGL(k_sine, dim3(8192), dim3(256), 0, 0, (uint64_t)0, words, d_mx, d_sum);
   // |pilot| in [2^-30, 2): exponent fields 97 .. 127
   const uint32_t b0 = 97u << 23, nb = 31u << 23;
-  hipLaunchKernelGGL(k_words, dim3(8192), dim3(256), 0, 0, b0, nb, d_vq, nvq, alpha, beta, d_mx + kNS);
+  hipLaunchKernelGGL(k_words, dim3(8192), dim3(256), 0, 0, b0, nb, d_vq, nvq, alpha, beta, d_mx + kNS, d_sum + 3);
   if ((e = hipDeviceSynchronize()) != hipSuccess) return -(int)e;
   unsigned mx[kNS + kNW];
-  double sums[3];
+  double sums[5];
   hipMemcpy(mx, d_mx, sizeof(mx), hipMemcpyDeviceToHost);
   hipMemcpy(sums, d_sum, sizeof(sums), hipMemcpyDeviceToHost);
   hipFree(d_mx);
@@ -158,6 +169,8 @@ int pllmath_sweep(float alpha, float beta, double *out, int nout) {
   out[17] = FMX_PLL_CHAIN;
   out[18] = FMX_WORD_SINCOS;
   out[19] = FMX_PLL_WORDS;
+  out[20] = sums[3] / ((double)nb * nvq); // e < 0: half of the 2 nb nvq pairs
+  out[21] = sums[4] / ((double)nb * nvq);
   return 0;
 }
 

@@ -11,9 +11,11 @@ functions on the GPU and sweeps:
     liquid's nco_crcf_get_phase -- and against the exact phase, in double
     precision; plus the chain sine's mean signed error (its truncation bias);
   * every float pilot with 2^-30 <= |pilot| < 2, both signs, times eight vcoQ
-    values: the chain's two pll_step words (truncating converts of pilot
-    alpha/2pi 2^32 vcoQ, beta likewise) against liquid's constrain of
-    e alpha, e beta (e = pilot vcoQ in float), as fmx_nco_constrain_ref.
+    values: the chain's two pll_step words (round 6: the alpha word as the
+    reference rounds it, 2^32 + x in f32 for e < 0; the beta word a
+    truncating convert) against liquid's constrain of e alpha, e beta (e =
+    pilot vcoQ in float), as fmx_nco_constrain_ref: maxima and, for e < 0,
+    mean errors.
 
 The maxima of the full sweep are committed in tests/golden/pllmath_gpu.json
 (FMX_PLLMATH_OUT=path writes them); the sweep is deterministic hardware
@@ -35,7 +37,7 @@ GOLD = os.path.join(ROOT, "tests", "golden", "pllmath_gpu.json")
 KEYS = ["chain_sin_vs_ref_phase", "chain_sin_vs_exact", "word_sin_vs_ref_phase", "word_cos_vs_ref_phase",
         "word_sin_vs_exact", "word_cos_vs_exact", "chain_sin_mean_err", "chain_sin_mean_abs_err", "words",
         "ca_max_pos", "cb_max_pos", "ca_max_neg", "cb_max_neg", "ca_rel_max", "cb_rel_max", "pairs",
-        "chain_phase_bias", "form_chain", "form_word_sincos", "form_words"]
+        "chain_phase_bias", "form_chain", "form_word_sincos", "form_words", "ca_mean_abs_neg", "cb_mean_abs_neg"]
 # absolute bounds (radian-free: sine units; words: units of 2^-32 turn)
 BOUNDS = {
     # v_sin of the word's top 23 bits as a float in [1, 2): < 2^-23 turn of
@@ -80,6 +82,14 @@ def test_pll_chain_math_exhaustive(torch_cuda):
         assert r[k] <= b, (k, r[k], b)
     # the truncation biases the chain sine by < 2^-24 turn on average
     assert abs(r["chain_sin_mean_err"]) < 4e-7, r
+    # the shipped forms (round 6, fmx_math.h): the chain sine of the word
+    # rounded to 23 bits has no phase bias (the truncated one lagged by
+    # 3.7e-7 rad), and the frequency (alpha) word follows the reference's
+    # 256-word rounding for e < 0 -- a mean error well under a word, where
+    # the truncating convert is off by ~64 on average
+    assert r["form_chain"] == 1 and r["form_words"] == 3, r
+    assert abs(r["chain_phase_bias"]) < 1e-8, r
+    assert r["ca_mean_abs_neg"] < 2.0 and r["cb_mean_abs_neg"] < 128.0, r
     with open(GOLD) as f:
         g = json.load(f)
     for k in KEYS:
