@@ -1061,7 +1061,9 @@ struct AuShared {
   float ws[3][4][2];                           // scan scratch (A, BL, BR per wave)
   float iir[4];                                // de_L, de_R, dc_L, dc_R
   int eb, ee, count;
-  uint16_t lrq[2][2][FMX_LR_QN] __attribute__((aligned(16))); // the L/R FIR tap window (FmxDesign::lr_q16)
+  // the L/R FIR tap window (FmxDesign::lr_q16 [2][2][FMX_LR_QN] u16, whole
+  // 64-dword LDS-DMA pieces)
+  uint32_t lrq[((2 * FMX_LR_QN + 63) / 64) * 64] __attribute__((aligned(16)));
 };
 
 // DPP move of x (CTRL, rows ROWS); lanes that receive nothing get id
@@ -1185,10 +1187,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE)
       S.hT[nn][b] = D->af_h[k];
     }
   }
-  if (lrfir) { // the L/R FIR tap window (read after the chunk loop's first barrier)
-    static_assert(FMX_LR_QN % 2 == 0, "dword copy");
-    for (int h = tid; h < 2 * FMX_LR_QN; h += 256)
-      reinterpret_cast<uint32_t *>(&S.lrq[0][0][0])[h] = reinterpret_cast<const uint32_t *>(&D->lr_q16[0][0][0])[h];
+  if (lrfir) { // the L/R FIR tap window by LDS-DMA (waited for before the FIR's barrier)
+    static_assert(FMX_LR_QN % 2 == 0, "dword window");
+    const float *qs = reinterpret_cast<const float *>(&D->lr_q16[0][0][0]);
+    for (int p = tid >> 6; p < (2 * FMX_LR_QN + 63) / 64; p += 4)
+      dma_dword(qs + min(64 * p + (tid & 63), 2 * FMX_LR_QN - 1), lds_addr(&S.lrq[64 * p]));
   }
   if (tid == 0) {
     S.eb = 0;
@@ -1283,7 +1286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE)
       // L2 loads before): this lane's 8 entries from 32 ks + 8 g + 15 - col
       // in copy (15 - col) & 1, four dwords
       const int qb = 8 * g + 15 - col, qc = qb & 1;
-      const uint32_t *qh = reinterpret_cast<const uint32_t *>(&S.lrq[0][0][0]) + qc * FMX_LR_QN + (qb - qc) / 2;
+      const uint32_t *qh = &S.lrq[0] + qc * FMX_LR_QN + (qb - qc) / 2;
       const uint32_t *ql = qh + FMX_LR_QN / 2;
       auto frag = [&](int ks, const uint32_t *q) __attribute__((always_inline)) {
         return u32x4{q[16 * ks], q[16 * ks + 1], q[16 * ks + 2], q[16 * ks + 3]};
@@ -2485,13 +2488,17 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   // window FmxDesign::dec_q16 (hi, lo: QN entries each) in LDS, read as the
   // A fragments instead of dec_frag from L2 (RS = true keeps dec_frag: no
   // LDS to spare beside its images and resampler bank)
+  // Both windows arrive by LDS-DMA behind the first chunk's (whole 64-dword
+  // pieces: QDP, QIP; the pad past each window takes copies of its last dword)
   static constexpr int KS = (15 * M + L + 1 + 31) / 32;
-  static constexpr int QN = 15 * M + 32 * KS;
+  static constexpr int QN = 15 * M + 32 * KS;                        // window entries the K steps reach
+  static constexpr int QDP = (FMX_DEC_QN + 63) / 64;                 // [2][FMX_DEC_QN] u16 = FMX_DEC_QN dwords
   static constexpr int QT = (SH + (int)sizeof(FeShared) + 15) & ~15;
   // and the channel's IQ FIR design's window FmxDesign::iq_q16 [2][2][FMX_IQ_QN]
-  static constexpr int QI = QT + (RS ? 0 : 2 * QN * 2);
-  static constexpr int BYTES = QI + (RS ? 0 : 2 * 2 * FMX_IQ_QN * 2);
-  static_assert(M % 2 == 0 && QN % 2 == 0 && QN <= FMX_DEC_QN, "dword-aligned fragment reads inside the window");
+  static constexpr int QIP = (2 * FMX_IQ_QN + 63) / 64;              // 2 FMX_IQ_QN dwords
+  static constexpr int QI = QT + (RS ? 0 : QDP * 256);
+  static constexpr int BYTES = QI + (RS ? 0 : QIP * 256);
+  static_assert(M % 2 == 0 && FMX_DEC_QN % 2 == 0 && QN <= FMX_DEC_QN, "dword-aligned fragment reads inside the window");
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
   // (fe8_stg order), in the raw region once every wave has read it; read
@@ -2674,18 +2681,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     if (!rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
   }
   FE_SETUP_STAMP(3)
-  if (!RS) { // the decimator's tap window (read after the first chunk's DMA barrier)
-    const uint32_t *qs = reinterpret_cast<const uint32_t *>(&D->dec_q16[0][0]);
-    uint32_t *qd = reinterpret_cast<uint32_t *>(smem + LY::QT);
-    for (int h = tid; h < LY::QN / 2; h += 256) {
-      qd[h] = qs[h];
-      qd[LY::QN / 2 + h] = qs[FMX_DEC_QN / 2 + h];
-    }
-    static_assert(FMX_IQ_QN % 2 == 0, "dword copy");
-    const uint32_t *is = reinterpret_cast<const uint32_t *>(&D->iq_q16[par.iqsel][0][0][0]);
-    uint32_t *id = reinterpret_cast<uint32_t *>(smem + LY::QI);
-    for (int h = tid; h < 2 * FMX_IQ_QN; h += 256) id[h] = is[h];
-  }
   if (rs) {
     // pair p < 32: (branch p, branch p+1 mod 32) on the same window; pair 32
     // (boundary): branch 31 on the window, branch 0 on the window shifted by
@@ -2720,6 +2715,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   // reach them).  Read where it is used (first chunk only): SGPRs are scarce.
   auto cold_k = [&]() __attribute__((always_inline)) { return (L - 1) - min(max(a.dec_valid[c], 0), L - 1); };
   dma_chunk(0, PAll0{}, PAll{});
+  if (!RS) {
+    // the decimator's and the IQ FIR's tap windows by LDS-DMA behind the
+    // first chunk's bytes (round 6): no register round trip and no wait here
+    // -- they land with the chunk, before its barrier (a copy through
+    // registers waited ~5 us for the loads ahead of the chunk's DMA)
+    static_assert(FMX_IQ_QN % 2 == 0, "dword windows");
+    const float *qs = reinterpret_cast<const float *>(&D->dec_q16[0][0]);
+    const float *is = reinterpret_cast<const float *>(&D->iq_q16[par.iqsel][0][0][0]);
+    for (int p = wave; p < LY::QDP + LY::QIP; p += 4) {
+      const bool dec = p < LY::QDP;
+      const int e = 64 * (dec ? p : p - LY::QDP) + lane;
+      const float *src = dec ? qs + min(e, FMX_DEC_QN - 1) : is + min(e, 2 * FMX_IQ_QN - 1);
+      dma_dword(src, lds_addr(smem + (dec ? LY::QT + 256 * p : LY::QI + 256 * (p - LY::QDP))));
+    }
+  }
   FE_SETUP_STAMP(4)
   int e_pos = 0;
 
@@ -2801,7 +2811,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       // 2 KB per wave and K step, and every K step waited on that load), RS =
       // true from the design's fragment table (16 B per lane)
       const uint32_t *qh = reinterpret_cast<const uint32_t *>(smem + LY::QT) + (15 * M + 8 * g - M * col) / 2;
-      const uint32_t *ql = qh + LY::QN / 2;
+      const uint32_t *ql = qh + FMX_DEC_QN / 2;
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag[0][0][0][0]) + lane;
       auto frag = [&](int ks, int s) __attribute__((always_inline)) {
         if (RS) return fa[128 * ks + 64 * s];
@@ -3410,14 +3420,16 @@ int launch_audio(const AudioArgs &a, void *stream) {
 #ifndef FMX_PILOT_QLDS
 #define FMX_PILOT_QLDS 1 // A fragments from the LDS tap window (round 6; 0: pilot_frag from L2, A/B)
 #endif
+#define PIL_QP ((2 * FMX_PILOT_QN + 63) / 64) // 64-dword pieces of the [2][2][FMX_PILOT_QN] u16 window
 struct PilLds {
   // sample s0 - FMX_HIST + i at [i]: the history (previous call's MPX rows
   // for s < 0), the segment, 32 zero-slack samples (read by K steps past the
   // filter, against zero taps)
   _Float16 xh[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
   _Float16 xl[FMX_HIST + PIL_SEG + 32] __attribute__((aligned(16)));
-  // the tap window FmxDesign::pilot_q16 ([copy][hi, lo][entry])
-  uint16_t q[FMX_PILOT_QLDS ? 2 : 0][2][FMX_PILOT_QN] __attribute__((aligned(16)));
+  // the tap window FmxDesign::pilot_q16 ([copy][hi, lo][entry]; whole 64-dword
+  // LDS-DMA pieces, the pad past it copies of its last dword)
+  uint32_t q[FMX_PILOT_QLDS ? PIL_QP * 64 : 1] __attribute__((aligned(16)));
 };
 #ifndef FMX_PILOT_PRIO
 #define FMX_PILOT_PRIO 0 // k_pilot's wave priority (s_setprio) beside the other streams' waves
@@ -3441,6 +3453,12 @@ __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
   const int KSP = D->pilot_ks;
   const float *mrow = a.mpx + (size_t)c * a.mpx_stride;
   const float *hrow = a.st_hist_rd + (size_t)c * FMX_HIST + FMX_HIST; // hrow[s], s < 0
+  if (FMX_PILOT_QLDS) { // the tap window by LDS-DMA, ahead of the image loads (it lands before their wait)
+    static_assert(FMX_PILOT_QN % 2 == 0, "dword window");
+    const float *qs = reinterpret_cast<const float *>(&D->pilot_q16[0][0][0]);
+    for (int p = wave; p < PIL_QP; p += 4)
+      dma_dword(qs + min(64 * p + lane, 2 * FMX_PILOT_QN - 1), lds_addr(&L.q[64 * p]));
+  }
   // the images from the window's first sample (8-aligned: P8 = 8k + 1), 4
   // samples per thread and pass
   const int i0 = FMX_HIST - (P8 - 1);
@@ -3474,15 +3492,7 @@ __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
     *reinterpret_cast<f16x4_t *>(&L.xh[i]) = hv;
     *reinterpret_cast<f16x4_t *>(&L.xl[i]) = lv;
   }
-  const int QW = 32 * KSP + 16; // window entries the K steps reach
-  if (FMX_PILOT_QLDS) {
-    static_assert(FMX_PILOT_QN % 2 == 0, "dword copy");
-    for (int h = tid; h < 2 * 2 * (QW / 2); h += 256) {
-      const int cs = h / (QW / 2), e = h % (QW / 2); // (copy, split) pair, dword
-      reinterpret_cast<uint32_t *>(&L.q[0][0][0])[cs * (FMX_PILOT_QN / 2) + e] =
-          reinterpret_cast<const uint32_t *>(&D->pilot_q16[0][0][0])[cs * (FMX_PILOT_QN / 2) + e];
-    }
-  }
+  if (FMX_PILOT_QLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the window's moves landed (before the barrier)
   __syncthreads();
   // tiles PIL_TPW w + u: 16 outputs (rows, A = taps, FmxDesign::pilot_frag)
   // of 16 blocks of 16 outputs (columns, B = MPX), K = P8 + 15 inputs
@@ -3494,7 +3504,7 @@ __global__ __launch_bounds__(256) void k_pilot(PilotArgs a) {
   // (FMX_PILOT_QLDS) this lane's 8 window entries from 32 ks + 8 g + 15 - col:
   // in copy (15 - col) & 1 they start on an even entry, four dwords
   const int qb = 8 * g + 15 - col, qc = qb & 1;
-  const uint32_t *qh = reinterpret_cast<const uint32_t *>(&L.q[0][0][0]) + qc * FMX_PILOT_QN + (qb - qc) / 2;
+  const uint32_t *qh = &L.q[0] + qc * FMX_PILOT_QN + (qb - qc) / 2;
   const uint32_t *ql = qh + FMX_PILOT_QN / 2;
   auto frag = [&](int ks, int s) __attribute__((always_inline)) {
     if (!FMX_PILOT_QLDS) return fa[128 * ks + 64 * s];
