@@ -1176,25 +1176,38 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
 #endif
   hipStream_t sPil = FMX_PILOT_ON_B ? h->sB : h->sP;
   if (pil_k && (FMX_PILOT_ON_B || sPil != h->sA)) HIP_TRY(hipStreamWaitEvent(sPil, evFE, 0));
-  if (pil_k) {
+  // FMX_PILOT_SPLIT_PCT (A/B): that share of the channels (rounded down to 8)
+  // has its pilot BPF on sB, ahead of k_pll, the rest stays on sA
+#ifndef FMX_PILOT_SPLIT_PCT
+#define FMX_PILOT_SPLIT_PCT 0
+#endif
+  const int pil_cB = (pil_k && !FMX_PILOT_ON_B && sPil == h->sA && h->sB != h->sA)
+                         ? ((h->C * FMX_PILOT_SPLIT_PCT / 100) & ~7) : 0;
+  auto run_pilot = [&](int c0, int cn, hipStream_t s, hipEvent_t done) -> int {
     PilotArgs p{};
     p.des = h->ddes;
     p.des_pilot_len = h->hdes->pilot_len;
-    p.C = h->C;
+    p.C = cn;
     p.n = n;
-    p.mpx = mpx;
+    p.mpx = mpx + static_cast<size_t>(c0) * mpx_stride;
     p.mpx_stride = mpx_stride;
-    p.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
-    p.out = h->pilot[buf];
+    p.st_hist_rd = h->st_hist + (static_cast<size_t>(h->st_idx) * h->C + c0) * FMX_HIST;
+    p.out = h->pilot[buf] + static_cast<size_t>(c0) * h->cfg.block;
     p.out_stride = h->cfg.block;
-    KBind t(h, FMX_K_PILOT, sPil, h->evP[buf]);
+    KBind t(h, FMX_K_PILOT, s, done);
     if (!FMX_SKIP(pll)) {
-      if ((rc = launch_pilot(p, sPil)) != FMX_OK) {
+      if (launch_pilot(p, s) != FMX_OK) {
         h->err = "pilot launch failed";
-        return rc;
+        return FMX_E_HIP;
       }
       t.launched();
     }
+    return FMX_OK;
+  };
+  if (pil_k && (rc = run_pilot(0, h->C - pil_cB, sPil, h->evP[buf])) != FMX_OK) return rc;
+  if (pil_cB > 0) {
+    HIP_TRY(hipStreamWaitEvent(h->sB, evFE, 0));
+    if ((rc = run_pilot(h->C - pil_cB, pil_cB, h->sB, nullptr)) != FMX_OK) return rc;
   }
   // ---- RDS (sC): the 240k -> 171k resampler (k_rs), then k_rds ----
   // (FMX_RS_ON_A_MAXC: up to that many channels k_rs runs on sA behind
