@@ -162,7 +162,7 @@ struct Handle {
 #if FMX_DIAG
   // diagnostics build only (make variant V=diag KDEFS=-DFMX_DIAG=1): kernels
   // left out of process_block (FMX_DIAG_SKIP=rds,pll,audio; outputs invalid)
-  bool skip_rds = false, skip_pll = false, skip_audio = false;
+  bool skip_rds = false, skip_pll = false, skip_audio = false, skip_krs = false, skip_pilot = false;
   bool nowait_a = false; // FMX_DIAG_NOWAIT=1: the front end skips its cross-stream waits (outputs invalid)
 #endif
   struct Pending {
@@ -808,6 +808,8 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
     h->skip_rds = v.find("rds") != std::string::npos;
     h->skip_pll = v.find("pll") != std::string::npos;
     h->skip_audio = v.find("audio") != std::string::npos;
+    h->skip_krs = v.find("krs") != std::string::npos;      // k_rs alone (the bound of fusing it into k_rds)
+    h->skip_pilot = v.find("pilot") != std::string::npos;  // k_pilot alone
   }
   if (const char *e = std::getenv("FMX_SERIAL"); e && e[0] == '1') serial = true;
   if (const char *e = std::getenv("FMX_DIAG_NOWAIT"); e && e[0] == '1') h->nowait_a = true;
@@ -1195,7 +1197,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     p.out = h->pilot[buf] + static_cast<size_t>(c0) * h->cfg.block;
     p.out_stride = h->cfg.block;
     KBind t(h, FMX_K_PILOT, s, done);
-    if (!FMX_SKIP(pll)) {
+    if (!FMX_SKIP(pll) && !FMX_SKIP(pilot)) {
       if (launch_pilot(p, s) != FMX_OK) {
         h->err = "pilot launch failed";
         return FMX_E_HIP;
@@ -1233,7 +1235,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
     r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
     KBind t(h, FMX_K_RS, s, done);
-    if (!FMX_SKIP(rds)) {
+    if (!FMX_SKIP(rds) && !FMX_SKIP(krs)) {
       if (launch_rs(r, s) != FMX_OK) {
         h->err = "rds resampler launch failed";
         return FMX_E_HIP;
