@@ -1245,7 +1245,13 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     return FMX_OK;
   };
   if (rs_on_a && (rc = run_rs(h->sA, h->evR[buf])) != FMX_OK) return rc;
-  HIP_TRY(hipStreamWaitEvent(h->sC, rs_on_a ? h->evR[buf] : evFE, 0));
+  // FMX_RS_AFTER_PILOT (A/B): the RDS stream starts behind k_pilot instead of
+  // beside it (k_rs then shares the CUs with the next k_fe8 and k_pll, the
+  // co-residency its 16.5 KB LDS was sized for, not with k_pilot)
+#ifndef FMX_RS_AFTER_PILOT
+#define FMX_RS_AFTER_PILOT 0
+#endif
+  HIP_TRY(hipStreamWaitEvent(h->sC, rs_on_a ? h->evR[buf] : ((FMX_RS_AFTER_PILOT && pil_k) ? h->evP[buf] : evFE), 0));
   if ((rc = launch_reset_parts(h, RSP_RDS, h->sC)) != FMX_OK) return rc;
   if (rds) {
     RdsArgs a = rds_args(h, buf);
