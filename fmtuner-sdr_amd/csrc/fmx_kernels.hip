@@ -3585,7 +3585,6 @@ int launch_pilot(const PilotArgs &a0, void *stream) {
 // each) and a k_pll wave (80)
 struct RsLds {
   float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1]; // branch rows, 27 terms oldest sample first
-  FmxSched ssch[RS_TMAX * 16];
   // the tile's MPX window [buffer][channel][column-major samples - k0]:
   // 16.5 KB in all, so a k_rs workgroup fits beside two k_fe8 (52.4 KB each)
   // and one k_pll workgroup (31.2 KB) on a CU
@@ -3597,7 +3596,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   extern __shared__ __align__(16) unsigned char rs_smem[];
   RsLds &RL = *reinterpret_cast<RsLds *>(rs_smem);
   auto &tab = RL.tab;
-  auto &ssch = RL.ssch;
   auto &xs = RL.xs;
   typedef float f32x4_t __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x;
@@ -3622,9 +3620,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   const int ntile = (ns + 15) / 16;
   const int per = (ntile + a.parts - 1) / a.parts;
   const int ta = blockIdx.y * per, tb = min(ntile, ta + per);
-  // this workgroup's schedule entries (rows past the call repeat the last)
-  for (int idx = lane; idx < (tb - ta) * 16; idx += 64) ssch[idx] = sched[min(16 * ta + idx, ns - 1)];
   __syncthreads();
+  // a tile's 16 schedule entries (rows past the call repeat the last), lane l
+  // holding row l & 15, loaded from L2 two tiles ahead of their window's
+  // load (round 6: no LDS staging of the workgroup's entries, so a workgroup
+  // may take any number of tiles); row 0 / row 15 to the wave by readlane
+  auto load_e = [&](int T) __attribute__((always_inline)) {
+    return sched[min(16 * T + (lane & 15), ns - 1)];
+  };
   const int r = lane & 15, kk = lane >> 4; // A: row r, K column kk; B: K row kk, channel column r
   // window loads: lane (channel lc, quarter lq) moves samples k0 + 16 lq .. + 15
   const int lc = lane >> 2, lq = lane & 3;
@@ -3632,15 +3635,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   const bool lcv = cl < a.C;
   const float *mrow = a.mpx + (size_t)(lcv ? cl : c0) * a.mpx_stride; // mrow[k], 0 <= k < n
   const float *wrow = a.win + (size_t)(lcv ? cl : c0) * 32 + 32;       // wrow[k], -32 <= k < 0
-  auto tile_k0 = [&](int T) __attribute__((always_inline)) {
-    const FmxSched e0 = ssch[16 * (T - ta)];
-    const int i0 = e0.packed & 0xFFFF;
-    return ((((e0.packed >> 24) & 1) ? i0 - 1 : i0) - (FMX_RDS_RS_SUB - 1)) & ~3;
+  auto tile_k0 = [&](const FmxSched &e) __attribute__((always_inline)) {
+    const uint32_t p0 = __builtin_amdgcn_readlane(e.packed, 0);
+    const int i0 = p0 & 0xFFFF;
+    return ((((p0 >> 24) & 1) ? i0 - 1 : i0) - (FMX_RDS_RS_SUB - 1)) & ~3;
   };
   // 16 samples of this lane's channel as four 16-B loads (4-sample groups lie
   // wholly in the history, the block or past it: k0 and n are multiples of 4)
-  auto load_w = [&](int T, float4 (&v)[4]) __attribute__((always_inline)) {
-    const int k0 = tile_k0(T);
+  auto load_w = [&](const FmxSched &e, float4 (&v)[4]) __attribute__((always_inline)) {
+    const int k0 = tile_k0(e);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = k0 + 16 * lq + 4 * j;
@@ -3651,8 +3654,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
       v[j] = *reinterpret_cast<const float4 *>(p);
     }
   };
-  auto store_w = [&](int T, int buf, const float4 (&v)[4]) __attribute__((always_inline)) {
-    const int k0 = tile_k0(T);
+  auto store_w = [&](const FmxSched &e, int buf, const float4 (&v)[4]) __attribute__((always_inline)) {
+    const int k0 = tile_k0(e);
     float4 w[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -3665,21 +3668,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     *reinterpret_cast<float4 *>(&xs[buf][lc][2 * RS_XS + 4 * lq]) = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
     *reinterpret_cast<float4 *>(&xs[buf][lc][3 * RS_XS + 4 * lq]) = make_float4(w[0].w, w[1].w, w[2].w, w[3].w);
   };
-  auto tile = [&](int T, int buf) __attribute__((always_inline)) {
-    const FmxSched en = ssch[16 * (T - ta) + r];
+  auto tile = [&](int T, const FmxSched &en, int buf) __attribute__((always_inline)) {
     const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
     const bool bnd = (en.packed >> 24) & 1;
     const int s_r = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // the window's oldest sample
     // pair (branch b, branch b + 1) on one window, or at the boundary branch
     // 31 and branch 0 shifted by one
     const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
-    const int k0 = tile_k0(T);
+    const int k0 = tile_k0(en);
     const int m0 = k0 + kk - s_r; // this lane's tap index at K step 0
     // K steps the tile needs: up to the last row's window end (rows past the
     // call repeat the last entry; the schedule's windows only move forward)
-    const FmxSched e15 = ssch[16 * (T - ta) + 15];
-    const int i15 = e15.packed & 0xFFFF;
-    const int s15 = ((((e15.packed >> 24) & 1) ? i15 - 1 : i15) - (FMX_RDS_RS_SUB - 1));
+    const uint32_t p15 = __builtin_amdgcn_readlane(en.packed, 15);
+    const int i15 = p15 & 0xFFFF;
+    const int s15 = ((((p15 >> 24) & 1) ? i15 - 1 : i15) - (FMX_RDS_RS_SUB - 1));
     const int ks = min(RS_KS, (s15 + FMX_RDS_RS_SUB - k0 + 3) / 4); // wave-uniform
     // row r's two branch filters combined with its interpolation weight:
     // (1 - mu) h_b + mu h_b+1, one MFMA chain (the reference interpolates the
@@ -3720,19 +3722,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   };
   // tile T's window is loaded at tile T-2 (registers), written to LDS at the
   // end of tile T-1: two register sets alternating (static indices)
+  // (schedule entries: tiles T, T + 1 in e0c / e1c, T + 2, T + 3 in e0n / e1n)
+  FmxSched e0c = load_e(ta), e1c = load_e(ta + 1), e0n = load_e(ta + 2), e1n = load_e(ta + 3);
   float4 wa[4], wb[4];
-  if (ta < tb) load_w(ta, wa);
-  if (ta + 1 < tb) load_w(ta + 1, wb);
-  if (ta < tb) store_w(ta, 0, wa);
+  if (ta < tb) load_w(e0c, wa);
+  if (ta + 1 < tb) load_w(e1c, wb);
+  if (ta < tb) store_w(e0c, 0, wa);
   for (int T = ta; T < tb; T += 2) {
-    if (T + 2 < tb) load_w(T + 2, wa);
-    tile(T, 0);
-    if (T + 1 < tb) store_w(T + 1, 1, wb);
+    if (T + 2 < tb) load_w(e0n, wa);
+    tile(T, e0c, 0);
+    if (T + 1 < tb) store_w(e1c, 1, wb);
     if (T + 1 < tb) {
-      if (T + 3 < tb) load_w(T + 3, wb);
-      tile(T + 1, 1);
-      if (T + 2 < tb) store_w(T + 2, 0, wa);
+      if (T + 3 < tb) load_w(e1n, wb);
+      tile(T + 1, e1c, 1);
+      if (T + 2 < tb) store_w(e0n, 0, wa);
     }
+    e0c = e0n;
+    e1c = e1n;
+    e0n = load_e(T + 4);
+    e1n = load_e(T + 5);
   }
 }
 

@@ -64,7 +64,7 @@ class SynthConfig(C.Structure):
 
 
 _lib = None
-_OPTIONAL = {"fmx_build_info"}
+_OPTIONAL = {"fmx_build_info", "fmx_host_stats"}  # absent from older libraries (A/B against past revisions)
 
 
 def lib():
