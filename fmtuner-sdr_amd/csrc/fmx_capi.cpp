@@ -1258,7 +1258,25 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.groups = o->d_groups;
     a.groups_stride = o->d_groups ? o->groups_stride : 0;
     a.group_count = o->d_group_count;
-    if (use_rs && !rs_on_a && (rc = run_rs(h->sC, nullptr)) != FMX_OK) return rc;
+    // FMX_RDS_FUSED: k_rds produces the 171 kHz samples itself (k_rs's MFMA
+    // tiles inside its rounds): no k_rs launch, no 171 kHz rows in HBM
+#ifndef FMX_RDS_FUSED
+#define FMX_RDS_FUSED 0
+#endif
+    const bool fused = FMX_RDS_FUSED && use_rs && !rs_on_a;
+    if (fused) {
+      a.fused = 1;
+      a.n = n;
+      a.mpx = mpx;
+      a.mpx_stride = mpx_stride;
+      a.win = h->rds_win[buf];
+      a.sched = h->t_rds.d_sched[h->t_rds.cur];
+      a.sched_n = h->t_rds.d_count[h->t_rds.cur];
+      a.group = h->t_rds.d_group[h->t_rds.cur];
+      a.sched_stride = h->t_rds.stride;
+    } else if (use_rs && !rs_on_a && (rc = run_rs(h->sC, nullptr)) != FMX_OK) {
+      return rc;
+    }
     KBind t(h, FMX_K_RDS, h->sC, h->evC[buf]);
     if (!FMX_SKIP(rds)) {
       if ((rc = launch_rds_sym(a, h->sC)) != FMX_OK) {

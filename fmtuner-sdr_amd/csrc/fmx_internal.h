@@ -161,6 +161,18 @@ struct RdsArgs {
   int sym_stride;
   int *sym_count;     // [C]
   float *sym_last_im; // [C] the last symbol's imaginary part (BiphaseDecoder's prev)
+  // fused (round 6, FMX_RDS_FUSED): k_rds resamples the MPX to 171 kHz itself
+  // (k_rs's MFMA tiles, produced as the rounds need them) instead of reading
+  // `in`; as RsArgs
+  int fused;
+  int n;                  // MPX samples of the call
+  const float *mpx;
+  int mpx_stride;
+  const float *win;       // [C][32] the previous call's last 32 MPX samples
+  const FmxSched *sched;  // [groups][sched_stride]
+  const int *sched_n;     // [groups]
+  const int *group;       // [C]
+  int sched_stride;
 };
 
 // k_pilot: the 19 kHz pilot BPF of a process_block step (after k_fe8)

@@ -1639,6 +1639,112 @@ __device__ __forceinline__ void rds_bits_store(FmxRdsState &g, const RdsBits &b)
   }
   g.bs_bits_since_lost = b.bs_bits_since_lost;
 }
+/* ---- the RDS resampler's MFMA tile (k_rs; round 6: also the producer
+ * fused into k_rds, FMX_RDS_FUSED) -- see k_rs below for the band-matrix
+ * form ---- */
+#define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
+// the tile's window, sample s of a channel at [c][RS_XS (s mod 4) + s / 4]:
+// a lane's 16 samples of one K column are one 64-B run (4 ds_read_b128
+// instead of 16 ds_read_b32 -- those were 2-way on the 32-bank rows), and the
+// loader's 4 x 4 register transpose stores 16-B runs; rows 80 floats apart,
+// columns 20: 1 extra cycle per read group, stores conflict-free
+// (tools/lds_banks.py)
+#define RS_XP 80
+#define RS_XS 20
+typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
+// the first window sample of a tile (a multiple of 4) from its row-0 entry
+// (lane 0's; wave-uniform)
+__device__ __forceinline__ int rs_tile_k0(const FmxSched &e) {
+  const uint32_t p0 = __builtin_amdgcn_readlane(e.packed, 0);
+  const int i0 = p0 & 0xFFFF;
+  return ((((p0 >> 24) & 1) ? i0 - 1 : i0) - (FMX_RDS_RS_SUB - 1)) & ~3;
+}
+// 16 samples of a channel (quarter lq of the tile's 64) as four 16-B loads
+// (4-sample groups lie wholly in the history, the block or past it: k0 and n
+// are multiples of 4); unconditional loads (a branch here would make the
+// compiler wait for them at the join): samples past the block or a lane
+// without a channel read mrow[0] and are zeroed when written to LDS
+__device__ __forceinline__ void rs_load_w(const float *mrow, const float *wrow, bool lcv, int n, int lq, int k0,
+                                          float4 (&v)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + 16 * lq + 4 * j;
+    const float *p = (!lcv || k >= n) ? mrow : (k < 0 ? wrow + k : mrow + k);
+    v[j] = *reinterpret_cast<const float4 *>(p);
+  }
+}
+// ... written to the channel's window row, transposed (samples 16 lq + 4 j + e:
+// column e, rows 4 lq + j)
+__device__ __forceinline__ void rs_store_w(float *xrow, bool lcv, int n, int lq, int k0, const float4 (&v)[4]) {
+  float4 w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool ok = lcv && k0 + 16 * lq + 4 * j < n;
+    w[j] = ok ? v[j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  *reinterpret_cast<float4 *>(&xrow[4 * lq]) = make_float4(w[0].x, w[1].x, w[2].x, w[3].x);
+  *reinterpret_cast<float4 *>(&xrow[RS_XS + 4 * lq]) = make_float4(w[0].y, w[1].y, w[2].y, w[3].y);
+  *reinterpret_cast<float4 *>(&xrow[2 * RS_XS + 4 * lq]) = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
+  *reinterpret_cast<float4 *>(&xrow[3 * RS_XS + 4 * lq]) = make_float4(w[0].w, w[1].w, w[2].w, w[3].w);
+}
+// one tile: 16 outputs (rows, lane & 15 = r, entry en of row r) x 16
+// channel columns (B: the window row xrow of column r), K = the window in
+// steps of 4 (lane >> 4 = kk); D: lane (column r, outputs 4 kk .. 4 kk + 3)
+__device__ __forceinline__ rs_f32x4 rs_tile(const float (*tab)[FMX_RDS_RS_SUB + 1], const float *xrow,
+                                           const FmxSched &en, int kk) {
+  const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
+  const bool bnd = (en.packed >> 24) & 1;
+  const int s_r = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // the window's oldest sample
+  // pair (branch b, branch b + 1) on one window, or at the boundary branch
+  // 31 and branch 0 shifted by one
+  const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
+  const int k0 = rs_tile_k0(en);
+  const int m0 = k0 + kk - s_r; // this lane's tap index at K step 0
+  // K steps the tile needs: up to the last row's window end (rows past the
+  // call repeat the last entry; the schedule's windows only move forward)
+  const uint32_t p15 = __builtin_amdgcn_readlane(en.packed, 15);
+  const int i15 = p15 & 0xFFFF;
+  const int s15 = ((((p15 >> 24) & 1) ? i15 - 1 : i15) - (FMX_RDS_RS_SUB - 1));
+  const int ks = min(RS_KS, (s15 + FMX_RDS_RS_SUB - k0 + 3) / 4); // wave-uniform
+  // row r's two branch filters combined with its interpolation weight:
+  // (1 - mu) h_b + mu h_b+1, one MFMA chain (the reference interpolates the
+  // two dot products, (1 - mu) y0 + mu y1: the same sum in another order)
+  const float mu = en.mu, mu1 = 1.0f - mu;
+  float hv[RS_KS], xv[RS_KS];
+#pragma unroll
+  for (int q = 0; q < RS_KS / 4; ++q) { // samples 4 st + kk, st = 4 q .. 4 q + 3
+    const float4 x4 = *reinterpret_cast<const float4 *>(&xrow[RS_XS * kk + 4 * q]);
+    xv[4 * q] = x4.x;
+    xv[4 * q + 1] = x4.y;
+    xv[4 * q + 2] = x4.z;
+    xv[4 * q + 3] = x4.w;
+  }
+#pragma unroll
+  for (int st = 0; st < RS_KS; ++st) {
+    const int m = m0 + 4 * st;
+    const int mc = min(max(m, 0), FMX_RDS_RS_SUB);
+    const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
+    hv[st] = in ? mu1 * tab[row0][mc] + mu * tab[row1][mc] : 0.0f;
+  }
+  rs_f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int st = 0; st < RS_KS; ++st)
+    if (st < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[st], xv[st], acc, 0, 0, 0);
+  return acc;
+}
+// the resampler's tap rows: row b < 32 branch b on the window, row 32
+// branch 0 on the window shifted by one (the boundary pair's second branch)
+__device__ __forceinline__ void rs_fill_tab(float (*tab)[FMX_RDS_RS_SUB + 1], const FmxDesign *D, int lane, int nl) {
+  for (int idx = lane; idx < (FMX_NPFB + 1) * (FMX_RDS_RS_SUB + 1); idx += nl) {
+    const int b = idx / (FMX_RDS_RS_SUB + 1), m = idx % (FMX_RDS_RS_SUB + 1);
+    const float *hs = D->rds_rs_h; // [branch][26]
+    float h;
+    if (b < FMX_NPFB) h = m < FMX_RDS_RS_SUB ? hs[b * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
+    else h = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
+    tab[b][m] = h;
+  }
+}
+
 struct RdsLds {
   // tap columns: hq[j0][i][q] = h[23 - (3 j0 + q) + 24 i] (zeros past tap 254),
   // q padded to 4 (one 16-B read per accumulator)
@@ -1651,6 +1757,16 @@ struct RdsLds {
   f32x2 win[2 * FMX_SS_SUB][RDS_CPW];
   float xin[RDS_NR][3][64];        // input ring: round r's sample 3 j0 + q of lane's channel at [r % RDS_NR][q][lane]
 };
+// the fused resampler's LDS (FMX_RDS_FUSED, behind RdsLds): k_rs's tap rows,
+// its window double buffer for the wave's 8 channels, and a ring of the
+// produced 171 kHz samples per channel (output e at [e % RDS_RSR])
+#define RDS_RSR 128
+struct RdsFusedLds {
+  float tab[FMX_NPFB + 1][FMX_RDS_RS_SUB + 1];
+  float xs[2][RDS_CPW][RS_XP] __attribute__((aligned(16)));
+  float rsr[RDS_CPW][RDS_RSR] __attribute__((aligned(16)));
+};
+#define RDS_FOFF ((sizeof(RdsLds) + 15) & ~(size_t)15)
 // k_bits: the bit decoders' LDS (burst-error tables, one bit state per lane)
 struct BitsLds {
   uint32_t esyn[5][52];
@@ -1797,7 +1913,11 @@ __device__ __forceinline__ f32x2 rds_sum8x2(float x, float y) {
 #ifndef FMX_RDS_WPE
 #define FMX_RDS_WPE 3 // k_rds waves per SIMD the register budget allows (A/B switch)
 #endif
-__global__ __launch_bounds__(64, FMX_RDS_WPE) void k_rds(RdsArgs a) {
+// (FUSED: two waves per SIMD's registers -- the producer's window
+// registers; 512 one-wave workgroups at 4096 channels leave it room beside
+// two k_fe8 waves)
+template <bool FUSED>
+__global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) {
 #ifndef FMX_RDS_PRIO
 #define FMX_RDS_PRIO 2
 #endif
@@ -1935,19 +2055,82 @@ __global__ __launch_bounds__(64, FMX_RDS_WPE) void k_rds(RdsArgs a) {
                 xin0 + (uint32_t)(((r & (RDS_NR - 1)) * 3 + q) * 64 * 4));
     }
   };
+  // ---- FUSED: the 240k -> 171k resampler inside (k_rs's MFMA tiles for the
+  // wave's 8 channels, columns 8 .. 15 of a tile unused), produced ahead of
+  // the round that reads them: tile T (outputs 16 T .. 16 T + 15 of the
+  // call, the same schedule entries for every channel) when the latest round
+  // position of the wave's channels reaches it.  The window of tile T + 1 is
+  // in registers and that of tile T in LDS when tile T is computed (k_rs's
+  // two-deep pipeline); the schedule entries two tiles ahead. ----
+  RdsFusedLds &F = *reinterpret_cast<RdsFusedLds *>(rds_smem + RDS_FOFF);
+  const FmxSched *fsched = nullptr;
+  int fns = 0, fntile = 0, ft = 0, o0max = 0;
+  FmxSched feC{}, feN{}, feNN{};
+  float4 fwN[4];
+  const int frr = lane & 15, fkk = lane >> 4, flc = lane >> 2, flq = lane & 3;
+  const bool flcv = flc < RDS_CPW && c0 + flc < a.C;
+  const float *fmrow = nullptr, *fwrow = nullptr;
+  auto f_load_e = [&](int T) __attribute__((always_inline)) { return fsched[min(16 * T + frr, fns - 1)]; };
+  if (FUSED) {
+    rs_fill_tab(F.tab, D, lane, 64);
+    const int fg = a.group[c0];
+    fsched = a.sched + (size_t)fg * a.sched_stride;
+    fns = a.sched_n[fg];
+    fntile = (fns + 15) / 16;
+    const int fch = flcv ? c0 + flc : c0;
+    fmrow = a.mpx + (size_t)fch * a.mpx_stride;
+    fwrow = a.win + (size_t)fch * 32 + 32;
+    o0max = o0;
+    for (int d = 32; d >= 1; d >>= 1) o0max = max(o0max, __shfl_xor(o0max, d));
+    feC = f_load_e(0);
+    feN = f_load_e(1);
+    feNN = f_load_e(2);
+    float4 w0[4];
+    rs_load_w(fmrow, fwrow, flcv, a.n, flq, rs_tile_k0(feC), w0);
+    if (flc < RDS_CPW) rs_store_w(F.xs[0][flc], flcv, a.n, flq, rs_tile_k0(feC), w0);
+    rs_load_w(fmrow, fwrow, flcv, a.n, flq, rs_tile_k0(feN), fwN);
+  }
+  auto produce = [&]() __attribute__((always_inline)) {
+    float4 wNN[4];
+    rs_load_w(fmrow, fwrow, flcv, a.n, flq, rs_tile_k0(feNN), wNN); // tile ft + 2
+    const rs_f32x4 acc = rs_tile(F.tab, F.xs[ft & 1][frr & (RDS_CPW - 1)], feC, fkk);
+    if (frr < RDS_CPW)
+      *reinterpret_cast<float4 *>(&F.rsr[frr][(16 * ft + 4 * fkk) & (RDS_RSR - 1)]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (flc < RDS_CPW) rs_store_w(F.xs[(ft + 1) & 1][flc], flcv, a.n, flq, rs_tile_k0(feN), fwN); // tile ft + 1
 #pragma unroll
-  for (int p = 0; p < RDS_PF; ++p) dma_round(p);
+    for (int j = 0; j < 4; ++j) fwN[j] = wNN[j];
+    feC = feN;
+    feN = feNN;
+    feNN = f_load_e(ft + 3);
+    ++ft;
+  };
+  if (!FUSED) {
+#pragma unroll
+    for (int p = 0; p < RDS_PF; ++p) dma_round(p);
+  }
   __syncthreads(); // LDS tables and per-channel state written
   RDS_STAMP(0)
   for (int r = 0; r < rmax; ++r) {
-    dma_round(r + RDS_PF);
-    // the moves of rounds r + 1 .. r + RDS_PF may stay in flight (anything
-    // the compiler issued after them only makes the wait stricter)
-    // vmcnt(3 RDS_PF) (its bits 3:0 and 15:14), lgkmcnt / expcnt untouched
-    __builtin_amdgcn_s_waitcnt(0x0F70 | ((3 * RDS_PF) & 15) | (((3 * RDS_PF) >> 4) << 14));
     float xr0[3];
+    if (FUSED) {
+      // the wave's latest sample this round: o0 + 24 r of its latest channel
+      const int eneed = min((r == 0) ? o0max : o0max + FMX_RDS_DECIM * r, fns - 1);
+      while (ft < fntile && 16 * ft <= eneed) produce();
+      const int fbase = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) xr0[q] = L.xin[r & (RDS_NR - 1)][q][lane];
+      for (int q = 0; q < 3; ++q) {
+        const int t = fbase + 3 * j0 + q;
+        xr0[q] = F.rsr[g][t & (RDS_RSR - 1)]; // t outside [0, count) is masked below (vq)
+      }
+    } else {
+      dma_round(r + RDS_PF);
+      // the moves of rounds r + 1 .. r + RDS_PF may stay in flight (anything
+      // the compiler issued after them only makes the wait stricter)
+      // vmcnt(3 RDS_PF) (its bits 3:0 and 15:14), lgkmcnt / expcnt untouched
+      __builtin_amdgcn_s_waitcnt(0x0F70 | ((3 * RDS_PF) & 15) | (((3 * RDS_PF) >> 4) << 14));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xr0[q] = L.xin[r & (RDS_NR - 1)][q][lane];
+    }
     // this lane's tap columns for the FIR products below: all eleven reads
     // issued here, ahead of the mix-down, which hides their latency (round 4
     // interleaved one read per accumulator with its packed FMAs: eleven LDS
@@ -3571,16 +3754,7 @@ int launch_pilot(const PilotArgs &a0, void *stream) {
  * 16 x .. 16 x + 15 and the y-th contiguous run of 16-output tiles.  With it,
  * k_fe8 leaves out the resampler: a front end without it ran 0.777 against
  * 0.847 ms per pipelined step (profiles/r03h_ab_lds_history_nors.txt). */
-#define RS_KS 16   // K steps of 4 per 16-output tile: a 64-sample window (fmx_capi.cpp checks that it holds the tile)
 #define RS_TMAX FMX_RS_TMAX // output tiles per workgroup at most (fmx_capi.cpp sizes parts)
-// the tile's window, sample s of a channel at [c][RS_XS (s mod 4) + s / 4]:
-// a lane's 16 samples of one K column are one 64-B run (4 ds_read_b128
-// instead of 16 ds_read_b32 -- those were 2-way on the 32-bank rows), and the
-// loader's 4 x 4 register transpose stores 16-B runs; rows 80 floats apart,
-// columns 20: 1 extra cycle per read group, stores conflict-free
-// (tools/lds_banks.py)
-#define RS_XP 80
-#define RS_XS 20
 // <= 96 VGPRs (five waves per SIMD): a k_rs wave beside two k_fe8 waves (168
 // each) and a k_pll wave (80)
 struct RsLds {
@@ -3597,20 +3771,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   RsLds &RL = *reinterpret_cast<RsLds *>(rs_smem);
   auto &tab = RL.tab;
   auto &xs = RL.xs;
-  typedef float f32x4_t __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x;
   const int c0 = blockIdx.x * 16;
   const FmxDesign *__restrict__ D = a.des;
-  // row b < 32: branch b on the window; row 32: branch 0 on the window
-  // shifted by one (the boundary pair's second branch)
-  for (int idx = lane; idx < (FMX_NPFB + 1) * (FMX_RDS_RS_SUB + 1); idx += 64) {
-    const int b = idx / (FMX_RDS_RS_SUB + 1), m = idx % (FMX_RDS_RS_SUB + 1);
-    const float *hs = D->rds_rs_h; // [branch][26]
-    float h;
-    if (b < FMX_NPFB) h = m < FMX_RDS_RS_SUB ? hs[b * FMX_RDS_RS_SUB + FMX_RDS_RS_SUB - 1 - m] : 0.0f;
-    else h = m >= 1 ? hs[FMX_RDS_RS_SUB - m] : 0.0f;
-    tab[b][m] = h;
-  }
+  rs_fill_tab(tab, D, lane, 64);
   // one schedule for every channel (the RDS timing set is never reset per
   // channel: SubcarrierSet::reset leaves the resampler alone,
   // subcarrier.cpp:108; process_block launches k_rs only with one group)
@@ -3635,78 +3799,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
   const bool lcv = cl < a.C;
   const float *mrow = a.mpx + (size_t)(lcv ? cl : c0) * a.mpx_stride; // mrow[k], 0 <= k < n
   const float *wrow = a.win + (size_t)(lcv ? cl : c0) * 32 + 32;       // wrow[k], -32 <= k < 0
-  auto tile_k0 = [&](const FmxSched &e) __attribute__((always_inline)) {
-    const uint32_t p0 = __builtin_amdgcn_readlane(e.packed, 0);
-    const int i0 = p0 & 0xFFFF;
-    return ((((p0 >> 24) & 1) ? i0 - 1 : i0) - (FMX_RDS_RS_SUB - 1)) & ~3;
-  };
-  // 16 samples of this lane's channel as four 16-B loads (4-sample groups lie
-  // wholly in the history, the block or past it: k0 and n are multiples of 4)
   auto load_w = [&](const FmxSched &e, float4 (&v)[4]) __attribute__((always_inline)) {
-    const int k0 = tile_k0(e);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + 16 * lq + 4 * j;
-      // unconditional load (a branch here would make the compiler wait for it
-      // at the join); lanes past the block or the channels read mrow[0] and
-      // are zeroed when written to LDS
-      const float *p = (!lcv || k >= a.n) ? mrow : (k < 0 ? wrow + k : mrow + k);
-      v[j] = *reinterpret_cast<const float4 *>(p);
-    }
+    rs_load_w(mrow, wrow, lcv, a.n, lq, rs_tile_k0(e), v);
   };
   auto store_w = [&](const FmxSched &e, int buf, const float4 (&v)[4]) __attribute__((always_inline)) {
-    const int k0 = tile_k0(e);
-    float4 w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool ok = lcv && k0 + 16 * lq + 4 * j < a.n;
-      w[j] = ok ? v[j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-    // samples 16 lq + 4 j + e: column e, rows 4 lq + j
-    *reinterpret_cast<float4 *>(&xs[buf][lc][4 * lq]) = make_float4(w[0].x, w[1].x, w[2].x, w[3].x);
-    *reinterpret_cast<float4 *>(&xs[buf][lc][RS_XS + 4 * lq]) = make_float4(w[0].y, w[1].y, w[2].y, w[3].y);
-    *reinterpret_cast<float4 *>(&xs[buf][lc][2 * RS_XS + 4 * lq]) = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
-    *reinterpret_cast<float4 *>(&xs[buf][lc][3 * RS_XS + 4 * lq]) = make_float4(w[0].w, w[1].w, w[2].w, w[3].w);
+    rs_store_w(xs[buf][lc], lcv, a.n, lq, rs_tile_k0(e), v);
   };
   auto tile = [&](int T, const FmxSched &en, int buf) __attribute__((always_inline)) {
-    const int i = en.packed & 0xFFFF, b = (en.packed >> 16) & 0xFF;
-    const bool bnd = (en.packed >> 24) & 1;
-    const int s_r = (bnd ? i - 1 : i) - (FMX_RDS_RS_SUB - 1); // the window's oldest sample
-    // pair (branch b, branch b + 1) on one window, or at the boundary branch
-    // 31 and branch 0 shifted by one
-    const int row0 = bnd ? FMX_NPFB - 1 : b, row1 = bnd ? FMX_NPFB : ((b + 1) & (FMX_NPFB - 1));
-    const int k0 = tile_k0(en);
-    const int m0 = k0 + kk - s_r; // this lane's tap index at K step 0
-    // K steps the tile needs: up to the last row's window end (rows past the
-    // call repeat the last entry; the schedule's windows only move forward)
-    const uint32_t p15 = __builtin_amdgcn_readlane(en.packed, 15);
-    const int i15 = p15 & 0xFFFF;
-    const int s15 = ((((p15 >> 24) & 1) ? i15 - 1 : i15) - (FMX_RDS_RS_SUB - 1));
-    const int ks = min(RS_KS, (s15 + FMX_RDS_RS_SUB - k0 + 3) / 4); // wave-uniform
-    // row r's two branch filters combined with its interpolation weight:
-    // (1 - mu) h_b + mu h_b+1, one MFMA chain (the reference interpolates the
-    // two dot products, (1 - mu) y0 + mu y1: the same sum in another order)
-    const float mu = en.mu, mu1 = 1.0f - mu;
-    float hv[RS_KS], xv[RS_KS];
-#pragma unroll
-    for (int q = 0; q < RS_KS / 4; ++q) { // samples 4 st + kk, st = 4 q .. 4 q + 3
-      const float4 x4 = *reinterpret_cast<const float4 *>(&xs[buf][r][RS_XS * kk + 4 * q]);
-      xv[4 * q] = x4.x;
-      xv[4 * q + 1] = x4.y;
-      xv[4 * q + 2] = x4.z;
-      xv[4 * q + 3] = x4.w;
-    }
-#pragma unroll
-    for (int st = 0; st < RS_KS; ++st) {
-      const int m = m0 + 4 * st;
-      const int mc = min(max(m, 0), FMX_RDS_RS_SUB);
-      const bool in = m >= 0 && m <= FMX_RDS_RS_SUB;
-      hv[st] = in ? mu1 * tab[row0][mc] + mu * tab[row1][mc] : 0.0f;
-    }
-    f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int st = 0; st < RS_KS; ++st)
-      if (st < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[st], xv[st], acc, 0, 0, 0);
+    const rs_f32x4 acc = rs_tile(tab, xs[buf][r], en, kk);
     // D: lane (channel column r, output rows 4 kk .. 4 kk + 3)
     const int cb = c0 + r;
     if (cb < a.C) {
@@ -3753,7 +3853,11 @@ int launch_rds_sym(const RdsArgs &a, void *stream) {
   // two k_fe8 workgroups (2 x 62.5 KB) leave 35 KB of a CU's 160 KB: several
   // k_rds workgroups fit beside them
   static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
-  return fmx_launch(k_rds, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
+  static_assert(RDS_FOFF + sizeof(RdsFusedLds) <= 28 * 1024, "fused k_rds LDS");
+  if (a.fused)
+    return fmx_launch(k_rds<true>, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), RDS_FOFF + sizeof(RdsFusedLds),
+                      static_cast<hipStream_t>(stream), a);
+  return fmx_launch(k_rds<false>, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
 }
 int launch_bits(const RdsArgs &a, void *stream) {
   static_assert(sizeof(BitsLds) <= 16 * 1024, "k_bits LDS");
