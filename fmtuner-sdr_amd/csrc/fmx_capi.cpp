@@ -1145,7 +1145,11 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     use_rs = rds && h->hdes->rds_del <= 2.1f && h->t_rds.G == 1 && fe8;
     // the pilot BPF of a k_fe8 step runs as k_pilot (after it, on sA): k_fe8
     // writes the MPX and the stereo history rows k_pilot starts from
-    pil_k = stereo && fe8;
+    // (FMX_FE_PILOT, A/B: inside k_fe8's RS = true instance, no k_pilot)
+#ifndef FMX_FE_PILOT
+#define FMX_FE_PILOT 0
+#endif
+    pil_k = stereo && fe8 && !FMX_FE_PILOT;
     if (pil_k) {
       a.pilot_out = nullptr;
       a.st_hist_out = 1;

@@ -2812,7 +2812,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   const bool rds = a.rds_out != nullptr;
   // rs: the resampler runs here (else k_rs does it, from the MPX and the
   // previous call's window this kernel hands over in rds_win_out)
-  const bool rs = RS && rds; // the launcher picks RS = false when rds_win_out is set
+  // (RS = true with rds_win_out set: the pilot BPF here, the resampler in
+  // k_rs -- the FMX_FE_PILOT A/B)
+  const bool rs = RS && rds && a.rds_win_out == nullptr;
   const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
   const float dc_c = -dc_a1;
 
@@ -3497,7 +3499,7 @@ template <int M, int TPP, bool RS> static int fe8_launch_rs(const FeArgs &a, hip
 // the resampler in the kernel, or (rds_win_out set) left to k_rs
 // (process_block's variant, RS = false, has no pilot BPF: k_pilot runs it)
 template <int M, int TPP> static int fe8_launch(const FeArgs &a, hipStream_t st) {
-  if (a.rds_out && a.rds_win_out) return a.pilot_out ? FMX_E_INVALID : fe8_launch_rs<M, TPP, false>(a, st);
+  if (a.rds_out && a.rds_win_out && !a.pilot_out) return fe8_launch_rs<M, TPP, false>(a, st);
   return fe8_launch_rs<M, TPP, true>(a, st);
 }
 
