@@ -1236,8 +1236,14 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     r.sched_stride = h->t_rds.stride;
     r.out = h->rds_in[buf];
     r.out_stride = h->rds_stride;
-    // <= FMX_RS_TMAX output tiles per workgroup: 8 parts of 23 tiles at a 4096-sample block
-    r.parts = std::max(1, ((h->t_rds.stride + 15) / 16 + FMX_RS_TMAX - 1) / FMX_RS_TMAX);
+    // <= FMX_RS_TMAX output tiles per workgroup (8 parts of 23 tiles at a
+    // 4096-sample block); from 256 channel groups (4096 channels) on, <= 46:
+    // about half as many workgroups beside the other streams' (round 6, with
+    // k_rs's schedule no longer staged in LDS): 4096 ch 0.5790 -> 0.5707 and
+    // 0.5804 -> 0.5718 ms in two 4-rep A/Bs; at 2048 ch the longer parts were
+    // slower, 0.3453 -> 0.3638 (profiles/r06k_ab_rs_parts_*.txt, r06m_*)
+    const int rs_tiles = (h->t_rds.stride + 15) / 16, rs_tmax = (h->C + 15) / 16 >= 256 ? 46 : FMX_RS_TMAX;
+    r.parts = std::max(1, (rs_tiles + rs_tmax - 1) / rs_tmax);
     KBind t(h, FMX_K_RS, s, done);
     if (!FMX_SKIP(rds) && !FMX_SKIP(krs)) {
       if (launch_rs(r, s) != FMX_OK) {
@@ -1264,9 +1270,6 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.group_count = o->d_group_count;
     // FMX_RDS_FUSED: k_rds produces the 171 kHz samples itself (k_rs's MFMA
     // tiles inside its rounds): no k_rs launch, no 171 kHz rows in HBM
-#ifndef FMX_RDS_FUSED
-#define FMX_RDS_FUSED 0
-#endif
     const bool fused = FMX_RDS_FUSED && use_rs && !rs_on_a;
     if (fused) {
       a.fused = 1;

@@ -161,7 +161,9 @@ struct RdsArgs {
   int sym_stride;
   int *sym_count;     // [C]
   float *sym_last_im; // [C] the last symbol's imaginary part (BiphaseDecoder's prev)
-  // fused (round 6, FMX_RDS_FUSED): k_rds resamples the MPX to 171 kHz itself
+  // fused (round 6, FMX_RDS_FUSED A/B builds only -- measured slower and not
+  // shipped: +20 % step at 4096 channels, +61 % at 2048, profiles/r06l_*):
+  // k_rds resamples the MPX to 171 kHz itself
   // (k_rs's MFMA tiles, produced as the rounds need them) instead of reading
   // `in`; as RsArgs
   int fused;
@@ -223,8 +225,11 @@ int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);      // k_rds then k_bits (one timer over both)
 int launch_rds_sym(const RdsArgs &a, void *stream);  // k_rds alone: the call's symbols
 int launch_bits(const RdsArgs &a, void *stream);     // k_bits alone: the bit decoders
+#ifndef FMX_RDS_FUSED
+#define FMX_RDS_FUSED 0 // A/B: the RDS resampler inside k_rds (RdsArgs::fused)
+#endif
 #ifndef FMX_RS_TMAX
-#define FMX_RS_TMAX 24 // k_rs: output tiles (of 16) per workgroup at most; parts = ceil(tiles / FMX_RS_TMAX)
+#define FMX_RS_TMAX 24 // k_rs: output tiles (of 16) per workgroup at most (46 from 4096 channels on, fmx_capi.cpp)
 #endif
 int launch_rs(const RsArgs &a, void *stream);
 int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,

@@ -3856,9 +3856,11 @@ int launch_rds_sym(const RdsArgs &a, void *stream) {
   // k_rds workgroups fit beside them
   static_assert(sizeof(RdsLds) <= 16 * 1024, "k_rds LDS");
   static_assert(RDS_FOFF + sizeof(RdsFusedLds) <= 28 * 1024, "fused k_rds LDS");
+#if FMX_RDS_FUSED
   if (a.fused)
     return fmx_launch(k_rds<true>, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), RDS_FOFF + sizeof(RdsFusedLds),
                       static_cast<hipStream_t>(stream), a);
+#endif
   return fmx_launch(k_rds<false>, dim3((a.C + RDS_CPW - 1) / RDS_CPW), dim3(64), sizeof(RdsLds), static_cast<hipStream_t>(stream), a);
 }
 int launch_bits(const RdsArgs &a, void *stream) {

@@ -98,7 +98,7 @@ def test_pilot_kernel_budget(tmp_path):
 
 def test_rds_fits_beside_two_front_ends(tmp_path):
     ks = _kernels(tmp_path)
-    for name, f in _find(ks, r"5k_rdsE").items():
+    for name, f in _find(ks, r"5k_rdsILb0E").items():
         assert f.get("vgpr_count", 0) + f.get("agpr_count", 0) <= 512 - 2 * 168, (name, f)
         assert f.get("vgpr_spill_count", 0) == 0, (name, f)
 
