@@ -2680,7 +2680,16 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   // and the channel's IQ FIR design's window FmxDesign::iq_q16 [2][2][FMX_IQ_QN]
   static constexpr int QIP = (2 * FMX_IQ_QN + 63) / 64;              // 2 FMX_IQ_QN dwords
   static constexpr int QI = QT + (RS ? 0 : QDP * 256);
-  static constexpr int BYTES = QI + (RS ? 0 : QIP * 256);
+  // RS = false (round 6): the channel's carried words and decimator history
+  // land here by LDS-DMA with the first chunk (1 KB: dwords 0..63 the words,
+  // 64..255 the history bytes), so the setup waits on no load
+  static constexpr int SU = QI + (RS ? 0 : QIP * 256);
+  static constexpr int SU_H = 64;                                    // history dwords from here
+  static constexpr int BYTES = SU + (RS ? 0 : 1024);
+  static_assert(RS || 2 * (L - 1) <= 4 * (256 - SU_H), "decimator history inside the landing area");
+  // (the IQ FIR history lands in hx as 4 x 64 dwords: the 16 past it in tl32,
+  // which RS = false does not use)
+  static_assert(RS || HX + 1024 <= TL32 + 32 * 4, "IQ FIR history DMA inside hx + tl32");
   static_assert(M % 2 == 0 && FMX_DEC_QN % 2 == 0 && QN <= FMX_DEC_QN, "dword-aligned fragment reads inside the window");
   static constexpr int NPF = (HB + 2 * FE8_T * M + 16 * 256 - 1) / (16 * 256); // 16-B pieces per thread
   // the MFMA decimator's outputs on their way to the 8-per-thread layout
@@ -2817,6 +2826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   const bool rs = RS && rds && a.rds_win_out == nullptr;
   const float dc_a1 = -1.0f + 0.0005f; // iirfilt_rrrf_create_dc_blocker(0.0005)
   const float dc_c = -dc_a1;
+  const float *su = reinterpret_cast<const float *>(smem + LY::SU); // RS = false: the landed words
 
   // ---- zeroed images, carried state ----
   for (int h = tid; h < LY::XW / 2; h += 256) {
@@ -2824,16 +2834,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     reinterpret_cast<uint32_t *>(xl)[h] = 0u;
   }
   if (RS) __syncthreads();
-  for (int h = tid; h < FE_HALO_IQ; h += 256) {
-    const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
-    hx[h] = make_float2(v.x, v.y);
+  if (RS) {
+    for (int h = tid; h < FE_HALO_IQ; h += 256) {
+      const float2_t v = a.iq_hist[(size_t)c * (FMX_IQ_MAXLEN - 1) + h];
+      hx[h] = make_float2(v.x, v.y);
+    }
   }
   FE_SETUP_STAMP(0)
   if (tid == 0) {
-    sh->carry_i = a.dc_v[2 * c];
-    sh->carry_q = a.dc_v[2 * c + 1];
-    sh->fd_re = a.fd_prev[2 * c];
-    sh->fd_im = a.fd_prev[2 * c + 1];
+    if (RS) {
+      sh->carry_i = a.dc_v[2 * c];
+      sh->carry_q = a.dc_v[2 * c + 1];
+      sh->fd_re = a.fd_prev[2 * c];
+      sh->fd_im = a.fd_prev[2 * c + 1];
+    }
     sh->clip = 0;
   }
   FE_SETUP_STAMP(1)
@@ -2848,12 +2862,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
   }
   FE_SETUP_STAMP(2)
   float agc_g = 1.0f, agc_y2p = 1.0f;
-  if (par.agc != 0 && tid == 0) {
+  if (RS && par.agc != 0 && tid == 0) {
     agc_g = a.agc[2 * c];
     agc_y2p = a.agc[2 * c + 1];
   }
   const float agc_bw = (par.agc == 1) ? 0.01f : 0.001f;
-  const uint16_t *iq16 = reinterpret_cast<const uint16_t *>(a.iq + (size_t)c * a.iq_stride);
   const uint8_t *dhist = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
   const FmxSched *sched = nullptr;
   int sched_n = 0;
@@ -2862,8 +2875,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     const int g = a.rds_group[c];
     sched = a.rds_sched + (size_t)g * a.rds_sched_stride;
     sched_n = a.rds_sched_n[g];
-    if (tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
-    if (!rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
+    if (RS && tid < 32) rds_keep = a.rds_hist[(size_t)c * 32 + tid];
+    if (RS && !rs && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = rds_keep;
   }
   FE_SETUP_STAMP(3)
   if (rs) {
@@ -2914,9 +2927,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       const float *src = dec ? qs + min(e, FMX_DEC_QN - 1) : is + min(e, 2 * FMX_IQ_QN - 1);
       dma_dword(src, lds_addr(smem + (dec ? LY::QT + 256 * p : LY::QI + 256 * (p - LY::QDP))));
     }
+    // ... and the carried state (round 6): the IQ FIR history into hx (one
+    // 64-dword piece per wave), the DC / discriminator / AGC words and the
+    // RDS window (wave 0) and the decimator's byte history (waves 1..3) into
+    // the landing area -- read after the chunk's barrier, no wait of their own
+    {
+      const float *ih = reinterpret_cast<const float *>(a.iq_hist + (size_t)c * (FMX_IQ_MAXLEN - 1));
+      dma_dword(ih + min(tid, 2 * FE_HALO_IQ - 1), lds_addr(smem + LY::HX + 256 * wave));
+      const float *w0 = a.dc_v + 2 * c;
+      if (wave == 0) {
+        const float *src = w0;
+        if (lane < 2) src = w0 + lane;
+        else if (lane < 4) src = a.fd_prev + 2 * c + (lane - 2);
+        else if (lane < 6) src = par.agc != 0 ? a.agc + 2 * c + (lane - 4) : w0;
+        else if (lane >= 8 && lane < 40) src = rds ? a.rds_hist + (size_t)c * 32 + (lane - 8) : w0;
+        dma_dword(src, lds_addr(smem + LY::SU));
+      } else {
+        const float *hb = reinterpret_cast<const float *>(dhist);
+        dma_dword(hb + min(64 * (wave - 1) + lane, (2 * (L - 1) + 3) / 4 - 1), lds_addr(smem + LY::SU + 4 * LY::SU_H + 256 * (wave - 1)));
+      }
+    }
   }
   FE_SETUP_STAMP(4)
   int e_pos = 0;
+  uint16_t keep[2] = {0, 0}; // the next call's decimator history (L - 1 <= 511 samples: two per thread)
 
   for (int n0 = 0; n0 < n; n0 += cs) {
     const int cnt = min(cs, n - n0); // samples of this chunk (a multiple of 4)
@@ -2933,12 +2967,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     if (a.dbg && tid == 0) { if (n0 == 0) su_w0 += __builtin_amdgcn_s_memtime() - tw0_; else su_w1 += __builtin_amdgcn_s_memtime() - tw0_; }
 #endif
     FE_STAMP(7) // setup / previous chunk's carry + the DMA wait
+    if (n0 + cnt >= n) {
+      // the call's last L - 1 IQ samples (the next call's decimator history)
+      // from this chunk's bytes in raw (sample n M - (L - 1) + h at u16 cnt M + 1 + h)
+      int k = 0;
+      for (int h = tid; h < L - 1; h += 256) keep[k++] = reinterpret_cast<const uint16_t *>(raw)[cnt * M + 1 + h];
+    }
+    if (!RS && n0 == 0) {
+      if (tid == 0) {
+        sh->carry_i = su[0];
+        sh->carry_q = su[1];
+        sh->fd_re = su[2];
+        sh->fd_im = su[3];
+        if (par.agc != 0) {
+          agc_g = su[4];
+          agc_y2p = su[5];
+        }
+      }
+      if (rds && tid < 32) a.rds_win_out[(size_t)c * 32 + tid] = su[8 + tid];
+    }
     if (n0 == 0) { // halo: a zero lead sample, then the carried L-1 samples (cold ones: byte 128, i.e. b - 128 = 0)
       const int coldk = cold_k();
+      const uint16_t *dh16 = reinterpret_cast<const uint16_t *>(su + LY::SU_H);
       for (int h = tid; h < L; h += 256) {
         const int hh = h - 1;
         uint16_t v = 0;
-        if (hh >= 0) v = hh < coldk ? (uint16_t)0x8080u : (uint16_t)((uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8));
+        if (hh >= 0)
+          v = hh < coldk ? (uint16_t)0x8080u
+                         : (RS ? (uint16_t)((uint16_t)dhist[2 * hh] | ((uint16_t)dhist[2 * hh + 1] << 8)) : dh16[hh]);
         reinterpret_cast<uint16_t *>(raw)[h] = v;
       }
       __syncthreads();
@@ -3419,18 +3475,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
 
   // ---- write back state ----
   {
-    const long total = (long)n * M;
-    uint16_t keep[2];
+    static_assert(L - 1 <= 512, "two history samples per thread");
     int cntk = 0;
-    for (int h = tid; h < L - 1; h += 256) keep[cntk++] = iq16[total - (L - 1) + h];
-    __syncthreads();
-    cntk = 0;
-    uint8_t *dh = a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC;
-    for (int h = tid; h < L - 1; h += 256) {
-      const uint16_t v = keep[cntk++];
-      dh[2 * h] = (uint8_t)(v & 255);
-      dh[2 * h + 1] = (uint8_t)(v >> 8);
-    }
+    uint16_t *dh = reinterpret_cast<uint16_t *>(a.dec_hist + (size_t)c * 2 * FMX_MAX_DEC);
+    for (int h = tid; h < L - 1; h += 256) dh[h] = keep[cntk++];
     if (tid == 0) a.dec_valid[c] = L - 1; // n M >= 1024 M > L - 1 new samples
   }
   for (int h = tid; h < FE_HALO_IQ; h += 256) {
