@@ -149,6 +149,11 @@ struct Handle {
   float *rds_win[FMX_NBUF] = {};  // [C][32] the previous call's last MPX samples, k_fe8 -> k_rs
   float *lraw[FMX_NBUF] = {}, *rraw[FMX_NBUF] = {};
   int rds_stride = 0;
+  // row stride (floats) of the MPX / pilot / raw L/R intermediates: the block
+  // rounded up to 32 and, when that is a multiple of 256 (1 KB), one 128-B
+  // line more (round 6), so that the rows a workgroup reads side by side do
+  // not all fall into the same L2 sets (FMX_ROW_PAD=0: the block itself)
+  int row = 0;
   // the call's PSK2 symbols, k_rds (sC) -> k_bits (sD), per slot (at most one
   // per decimation period)
   float *rds_sym[FMX_NBUF] = {}, *rds_sym_im[FMX_NBUF] = {};
@@ -848,7 +853,12 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
-  const size_t B = static_cast<size_t>(cfg->block);
+  h->row = cfg->block;
+  if (const char *e = std::getenv("FMX_ROW_PAD"); !(e && e[0] == '0')) {
+    h->row = (cfg->block + 31) & ~31;
+    if (h->row % 256 == 0) h->row += 32;
+  }
+  const size_t B = static_cast<size_t>(h->row);
   // parameters: the reference objects as main.cpp:640-710 configures them
   h->hpar.assign(C, FmxChanParam{});
   h->w0.assign(C, 194000);
@@ -1000,7 +1010,7 @@ static void audio_signal_level(Handle *h, AudioArgs &a, const fmx_block_out *o, 
 }
 
 // raw L/R (k_pll -> k_audio) in pair tiles when the block is whole 16-sample tiles
-static int lr_tiled(const Handle *h) { return (h->cfg.block % 16 == 0) ? 1 : 0; }
+static int lr_tiled(const Handle *h) { return (h->row % 16 == 0) ? 1 : 0; }
 
 static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int buf) {
   PllArgs a{};
@@ -1009,13 +1019,13 @@ static PllArgs pll_args(Handle *h, int n, const float *mpx, int mpx_stride, int 
   a.C = h->C;
   a.n = n;
   a.pilot = h->pilot[buf];
-  a.pilot_stride = h->cfg.block;
+  a.pilot_stride = h->row;
   a.mpx = mpx;
   a.mpx_stride = mpx_stride;
   a.st_hist_rd = h->st_hist + static_cast<size_t>(h->st_idx) * h->C * FMX_HIST;
   a.lraw = h->lraw[buf];
   a.rraw = h->rraw[buf];
-  a.lr_stride = h->cfg.block;
+  a.lr_stride = h->row;
   a.lr_tiled = lr_tiled(h);
   a.st = h->st;
   a.dbg = h->dbg ? h->dbg + 16 : nullptr;
@@ -1117,7 +1127,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
   if (rds && (rc = tset_take_or_advance(h, h->t_rds, n, rslot, h->sA)) != FMX_OK) return rc;
   const unsigned spec16 = rds ? tset_speculate(h, h->t_rds, n, nrslot, static_cast<size_t>(h->C) * 256) : 0u;
   float *mpx = o->d_mpx ? o->d_mpx : h->mpx[buf];
-  const int mpx_stride = o->d_mpx ? o->mpx_stride : h->cfg.block;
+  const int mpx_stride = o->d_mpx ? o->mpx_stride : h->row;
   hipEvent_t evFE = h->evF[h->step % FMX_FRING];
   bool use_rs = false, pil_k = false;
   // ---- front end (sA) ----
@@ -1130,7 +1140,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     a.do_demod = 1;
     if (stereo) {
       a.pilot_out = h->pilot[buf];
-      a.pilot_stride = h->cfg.block;
+      a.pilot_stride = h->row;
     }
     if (rds) {
       a.rds_out = h->rds_in[buf];
@@ -1198,8 +1208,8 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     p.mpx = mpx + static_cast<size_t>(c0) * mpx_stride;
     p.mpx_stride = mpx_stride;
     p.st_hist_rd = h->st_hist + (static_cast<size_t>(h->st_idx) * h->C + c0) * FMX_HIST;
-    p.out = h->pilot[buf] + static_cast<size_t>(c0) * h->cfg.block;
-    p.out_stride = h->cfg.block;
+    p.out = h->pilot[buf] + static_cast<size_t>(c0) * h->row;
+    p.out_stride = h->row;
     KBind t(h, FMX_K_PILOT, s, done);
     if (!FMX_SKIP(pll) && !FMX_SKIP(pilot)) {
       if (launch_pilot(p, s) != FMX_OK) {
@@ -1351,7 +1361,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     if (stereo) {
       a.in_l = h->lraw[buf];
       a.in_r = h->rraw[buf];
-      a.in_stride = h->cfg.block;
+      a.in_stride = h->row;
 #ifdef FMX_AB_NO_LR // A/B only: every channel reads the first pair's rows (L2-resident)
       a.in_stride = 0;
 #endif
@@ -1617,7 +1627,7 @@ static int demod_common(Handle *h, int mode, const void *d_in, size_t in_stride,
   if (n == 0) return FMX_OK;
   const int buf = static_cast<int>(h->step % FMX_NBUF);
   float *mpx = d_mpx ? d_mpx : h->mpx[buf];
-  const int ms = d_mpx ? mpx_stride : h->cfg.block;
+  const int ms = d_mpx ? mpx_stride : h->row;
   {
     FeArgs a = fe_args(h, n, mode, buf);
     if (mode == FE_IN_CF) {
@@ -1707,7 +1717,7 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
     a.in_f = d_mpx;
     a.in_stride = mpx_stride;
     a.pilot_out = h->pilot[buf];
-    a.pilot_stride = h->cfg.block;
+    a.pilot_stride = h->row;
     a.do_demod = 0;
     a.clip_out = nullptr;
     KTimer t(h, FMX_K_FRONTEND, h->sA);
@@ -1724,7 +1734,7 @@ int fmx_stereo(void *handle, const float *d_mpx, int mpx_stride, int n, float *d
     AudioArgs a = audio_args(h, n, 4, nullptr);
     a.in_l = h->lraw[buf];
     a.in_r = h->rraw[buf];
-    a.in_stride = h->cfg.block;
+    a.in_stride = h->row;
     a.in_tiled = lr_tiled(h);
     a.lr_out_l = d_left;
     a.lr_out_r = d_right;

@@ -1910,6 +1910,9 @@ __device__ __forceinline__ f32x2 rds_sum8x2(float x, float y) {
   return f32x2{x, y};
 }
 
+#ifndef FMX_RDS_HREG
+#define FMX_RDS_HREG 0
+#endif
 #ifndef FMX_RDS_WPE
 #define FMX_RDS_WPE 3 // k_rds waves per SIMD the register budget allows (A/B switch)
 #endif
@@ -2109,6 +2112,16 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
     for (int p = 0; p < RDS_PF; ++p) dma_round(p);
   }
   __syncthreads(); // LDS tables and per-channel state written
+  // the lane's tap columns: the first FMX_RDS_HREG held in registers for
+  // the whole call, the others read from LDS every round
+  float hr[FMX_RDS_NACC][3];
+#pragma unroll
+  for (int i = 0; i < FMX_RDS_HREG; ++i) {
+    const float4 h = *reinterpret_cast<const float4 *>(&L.hq[j0][i][0]);
+    hr[i][0] = h.x;
+    hr[i][1] = h.y;
+    hr[i][2] = h.z;
+  }
   RDS_STAMP(0)
   for (int r = 0; r < rmax; ++r) {
     float xr0[3];
@@ -2136,9 +2149,8 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
     // interleaved one read per accumulator with its packed FMAs: eleven LDS
     // latencies per round); the scheduling barrier keeps them together, so
     // none lands over the sources of a packed op (tests/test_isa_scan.py)
-    float hr[FMX_RDS_NACC][3];
 #pragma unroll
-    for (int i = 0; i < FMX_RDS_NACC; ++i) {
+    for (int i = FMX_RDS_HREG; i < FMX_RDS_NACC; ++i) {
       const float4 h = *reinterpret_cast<const float4 *>(&L.hq[j0][i][0]);
       hr[i][0] = h.x;
       hr[i][1] = h.y;
