@@ -1910,8 +1910,13 @@ __device__ __forceinline__ f32x2 rds_sum8x2(float x, float y) {
   return f32x2{x, y};
 }
 
+// k_rds's tap columns (11 per lane, three taps each) held in registers for
+// the whole call: the first FMX_RDS_HREG, the rest read from LDS per round
+// (round 6: 6 -- 164 VGPRs, still beside two front-end waves; 2048 channels
+// 0.3533 -> 0.3418 ms, 1024 0.276 -> 0.273, 4096 unchanged; all 11 at two
+// waves per SIMD 0.3428, 8 0.3471: profiles/r06p_ab_rds_tap_registers_*.txt)
 #ifndef FMX_RDS_HREG
-#define FMX_RDS_HREG 0
+#define FMX_RDS_HREG 6
 #endif
 #ifndef FMX_RDS_WPE
 #define FMX_RDS_WPE 3 // k_rds waves per SIMD the register budget allows (A/B switch)
