@@ -152,8 +152,13 @@ struct Handle {
   // row stride (floats) of the MPX / pilot / raw L/R intermediates: the block
   // rounded up to 32 and, when that is a multiple of 256 (1 KB), one 128-B
   // line more (round 6), so that the rows a workgroup reads side by side do
-  // not all fall into the same L2 sets (FMX_ROW_PAD=0: the block itself)
+  // not all fall into the same L2 sets (a build with -DFMX_ROW_PAD=0: the
+  // block itself; 2048 channels 0.3481 -> 0.3412 ms, profiles/r06o_*)
   int row = 0;
+  // the intermediate slot the last k_rds read (its RDS-rate input stays there
+  // until the next RDS call): the ring refill's source (FmxRdsState::ring_ok)
+  int rds_last_buf = -1;
+  int ring_always = 0; // fmx_diag_set(FMX_DIAG_RDS_RING_ALWAYS): k_rds writes the ring every call
   // the call's PSK2 symbols, k_rds (sC) -> k_bits (sD), per slot (at most one
   // per decimation period)
   float *rds_sym[FMX_NBUF] = {}, *rds_sym_im[FMX_NBUF] = {};
@@ -581,6 +586,8 @@ static ResetArgs reset_args(Handle *h) {
   r.mono_iir = h->mono_iir;
   r.rds_hist = h->rds_hist;
   r.mute = h->mute;
+  r.rds_prev = h->rds_last_buf >= 0 ? h->rds_in[h->rds_last_buf] : nullptr;
+  r.rds_stride = h->rds_stride;
   return r;
 }
 
@@ -853,8 +860,11 @@ static int create(const fmx_config *cfg, int n, int device, Handle **out) {
   if ((rc = dalloc(h, &h->ddes, 1)) != FMX_OK) return rc;
   HIP_TRY(hipMemcpy(h->ddes, h->hdes, sizeof(FmxDesign), hipMemcpyHostToDevice));
   const size_t C = static_cast<size_t>(n);
+#ifndef FMX_ROW_PAD
+#define FMX_ROW_PAD 1
+#endif
   h->row = cfg->block;
-  if (const char *e = std::getenv("FMX_ROW_PAD"); !(e && e[0] == '0')) {
+  if (FMX_ROW_PAD) {
     h->row = (cfg->block + 31) & ~31;
     if (h->row % 256 == 0) h->row += 32;
   }
@@ -1048,6 +1058,8 @@ static RdsArgs rds_args(Handle *h, int buf) {
   a.sym_stride = h->sym_stride;
   a.sym_count = h->rds_sym_count[buf];
   a.sym_last_im = h->rds_sym_im[buf];
+  a.in_prev = h->rds_last_buf >= 0 ? h->rds_in[h->rds_last_buf] : nullptr;
+  a.ring_always = h->ring_always;
   return a;
 }
 
@@ -1301,6 +1313,7 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
         return rc;
       }
       t.launched();
+      if (!a.fused) h->rds_last_buf = buf;
     }
   } else {
     if (o->d_group_count) HIP_TRY(hipMemsetAsync(o->d_group_count, 0, sizeof(int) * h->C, h->sC));
@@ -1463,6 +1476,44 @@ int fmx_host_stats(void *handle, double *out, int n) {
   for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
   h->host_waits = h->host_stalls = 0;
   h->host_stall_ms = 0.0;
+  return FMX_OK;
+}
+
+int fmx_diag_set(void *handle, int what, int value) {
+  Handle *h = H(handle);
+  if (!h) return FMX_E_INVALID;
+  if (what != FMX_DIAG_RDS_RING_ALWAYS) {
+    h->err = "unknown diagnostic setting";
+    return FMX_E_INVALID;
+  }
+  h->ring_always = value != 0;
+  return FMX_OK;
+}
+
+int fmx_diag_rds_ring(void *handle, int channel, float *out) {
+  Handle *h = H(handle);
+  if (!h || !out) return FMX_E_INVALID;
+  if (channel < 0 || channel >= h->C) {
+    h->err = "channel out of range";
+    return FMX_E_INVALID;
+  }
+  // every stream's work done, the ring of every checkpointed channel
+  // refilled (a valid state transition: the ring is what k_rds would have
+  // written), then the channel's row oldest first
+  int rc = join_into_A(h);
+  if (rc != FMX_OK) return rc;
+  if ((rc = launch_ring_fill(reset_args(h), h->sA)) != FMX_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(h->sA));
+  std::vector<float> row(2 * FMX_RDS_RING);
+  FmxRdsState st{};
+  HIP_TRY(hipMemcpy(row.data(), h->ring + static_cast<size_t>(channel) * 2 * FMX_RDS_RING, sizeof(float) * row.size(),
+                    hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&st, h->rds + channel, sizeof(st), hipMemcpyDeviceToHost));
+  for (int k = 0; k < FMX_RDS_RING; ++k) {
+    const uint32_t idx = (st.ring_pos - FMX_RDS_RING + static_cast<uint32_t>(k)) & (FMX_RDS_RING - 1);
+    out[2 * k] = row[2 * idx];
+    out[2 * k + 1] = row[2 * idx + 1];
+  }
   return FMX_OK;
 }
 
@@ -1814,6 +1865,7 @@ int fmx_rds(void *handle, const float *d_mpx, int mpx_stride, int n, fmx_rds_gro
   {
     KTimer t(h, FMX_K_RDS, h->sA);
     if ((rc = launch_rds(a, h->sA)) != FMX_OK) return rc;
+    h->rds_last_buf = buf;
   }
   h->block_index++;
   return stage_end(h);

@@ -26,6 +26,7 @@
 #define FMX_SS_SUB 18        // (2*32*3*3+1 - 1) / 32
 #define FMX_HIST 512         // stereo MPX history (>= pilot taps - 1 and delay line)
 #define FMX_RDS_RING 256     // last mixed RDS samples kept for a decimation-phase rebuild
+#define FMX_RDS_CK 12        // k_rds's per-round NCO checkpoints (24 (CK - 1) + 1 >= RING samples)
 #define FMX_PAD 10           // zero taps around padded FIR tap arrays (5 each side)
 #define FMX_DEC_KS_MAX 16    // K steps of the f16 MFMA decimator: ceil((15 M + L + 1) / 32)
 #define FMX_DEC_QN (15 * 10 + 32 * FMX_DEC_KS_MAX) // entries of the flat decimator tap window (M <= 10)
@@ -168,6 +169,17 @@ typedef struct {
   int ss_mf_valid;         // pushes since the matched-filter bank was reset
   float ss_rate, ss_del, ss_tau, ss_q_hat, ss_v1, ss_v2;
   int ss_b, ss_decim;
+  // round 6: the ring as checkpoints.  A call of >= FMX_RDS_RING samples
+  // writes no ring; it records the NCO words its last FMX_RDS_CK rounds
+  // mixed with (round r: sample t = base_r + j mixed at ck_thp + j ck_dth)
+  // and its o0 / rounds / count, and ring_ok = 0.  Whoever needs the ring
+  // (a reset's rebuild, a short call after a long one, fmx_diag_rds_ring)
+  // refills it from those words and the call's RDS-rate input, which stays
+  // in its intermediate slot until the next RDS call after it
+  // (rds_ring_fill: the same mix, bit-identical).  ring_ok = 1: the ring
+  // holds the last FMX_RDS_RING mixed samples
+  uint32_t ck_thp[FMX_RDS_CK], ck_dth[FMX_RDS_CK];
+  int ck_o0, ck_rounds, ck_count, ring_ok;
   // biphase / delta decoders
   float bi_prev_re, bi_prev_im, bi_even, bi_odd;
   uint32_t bi_clock, bi_polarity;

@@ -151,6 +151,10 @@ struct RdsArgs {
   const int *in_count; // [C]
   FmxRdsState *st;
   float *ring; // [C][FMX_RDS_RING][2]
+  // the previous RDS call's input rows (its slot; same stride), for the ring
+  // refill of a short call after a long one (FmxRdsState::ring_ok)
+  const float *in_prev;
+  int ring_always; // write the ring every call (FMX_RDS_RING_ALWAYS=1: the round-5 behaviour, the A/B and test arm)
   fmx_rds_group *groups;
   int groups_stride;
   int *group_count;
@@ -223,7 +227,9 @@ int launch_pll(const PllArgs &a, void *stream);
 int launch_pilot(const PilotArgs &a, void *stream);
 int launch_audio(const AudioArgs &a, void *stream);
 int launch_rds(const RdsArgs &a, void *stream);      // k_rds then k_bits (one timer over both)
+struct ResetArgs;
 int launch_rds_sym(const RdsArgs &a, void *stream);  // k_rds alone: the call's symbols
+int launch_ring_fill(const ResetArgs &a, void *stream); // every channel's RDS ring refilled where ring_ok = 0
 int launch_bits(const RdsArgs &a, void *stream);     // k_bits alone: the bit decoders
 #ifndef FMX_RDS_FUSED
 #define FMX_RDS_FUSED 0 // A/B: the RDS resampler inside k_rds (RdsArgs::fused)
@@ -251,6 +257,8 @@ struct ResetArgs {
   float *lr_hist, *af_win, *af_iir, *mono_win, *mono_iir;
   float *rds_hist;
   int *mute;      // [C][2]
+  const float *rds_prev; // the last RDS call's input rows (the ring refill before a rebuild)
+  int rds_stride;
 };
 // per-step intermediates (MPX, pilot, RDS-rate, raw L/R): front end k runs
 // while stereo/RDS/audio of steps k-1, k-2 drain

@@ -1756,7 +1756,42 @@ struct RdsLds {
   // contiguous (constant read offsets, no wrap per tap)
   f32x2 win[2 * FMX_SS_SUB][RDS_CPW];
   float xin[RDS_NR][3][64];        // input ring: round r's sample 3 j0 + q of lane's channel at [r % RDS_NR][q][lane]
+  uint32_t ck[RDS_CPW][FMX_RDS_CK][2]; // round 6: the NCO words of each channel's last rounds (round r at r % CK)
 };
+static_assert(FMX_RDS_DECIM * (FMX_RDS_CK - 1) + 1 >= FMX_RDS_RING, "the checkpoints cover the ring");
+
+// the mix-down of one RDS-rate sample x with NCO word w (subcarrier.cpp:
+// 153-160: x e^{-j phase}; the word's phase as a signed fraction of a turn,
+// v_sin / v_cos): k_rds's and the ring refill's one formula (bit-identical)
+__device__ __forceinline__ f32x2 rds_mix(float x, uint32_t w) {
+  const float rr = (float)(int32_t)w * 2.3283064365386963e-10f; // w / 2^32 turns
+  const float sn = -__builtin_amdgcn_sinf(rr);
+  const float cs = __builtin_amdgcn_cosf(rr);
+  return f32x2{x, x} * f32x2{cs, sn};
+}
+// Round 6: the RDS ring of one channel rebuilt from the checkpoints of its
+// last call (FmxRdsState::ck_*, that call >= FMX_RDS_RING samples) and that
+// call's RDS-rate input row `prev`: sample t of the call sat in round r
+// (t <= o0: round 0, else 1 + (t - o0 - 1) / 24) at period position t -
+// base_r and was mixed with ck_thp + (t - base_r) ck_dth of that round --
+// k_rds's own words -- and lands where k_rds would have written it
+// ((ring_pos - (count - t)) mod RING).  Threads k0, k0 + dk, ... take the
+// ring's samples; the state is read from memory (a rare path: a reset, a
+// short call after a long one, fmx_diag_rds_ring)
+__device__ void rds_ring_fill(const FmxRdsState *sp, const float *prev, float *ring, int k0, int dk) {
+  const int count = sp->ck_count, o0 = sp->ck_o0, R = sp->ck_rounds;
+  const int first = R > FMX_RDS_CK ? R - FMX_RDS_CK : 0;
+  const uint32_t rp = sp->ring_pos;
+  for (int k = k0; k < FMX_RDS_RING; k += dk) {
+    const int t = count - FMX_RDS_RING + k;
+    const int r = t <= o0 ? 0 : 1 + (t - o0 - 1) / FMX_RDS_DECIM;
+    const int base = r == 0 ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
+    const int i = min(max(r - first, 0), FMX_RDS_CK - 1);
+    const uint32_t w = sp->ck_thp[i] + (uint32_t)(t - base) * sp->ck_dth[i];
+    const uint32_t idx = (rp - (uint32_t)(count - t)) & (FMX_RDS_RING - 1);
+    *reinterpret_cast<f32x2 *>(ring + 2 * idx) = rds_mix(prev[t], w);
+  }
+}
 // the fused resampler's LDS (FMX_RDS_FUSED, behind RdsLds): k_rs's tap rows,
 // its window double buffer for the wave's 8 channels, and a ring of the
 // produced 171 kHz samples per channel (output e at [e % RDS_RSR])
@@ -1969,6 +2004,18 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
   const FmxRdsState G = act ? a.st[c] : FmxRdsState{}; // the compiler loads only the fields used
   const int count = act ? a.in_count[c] : 0;
   float *ring = a.ring + (size_t)(act ? c : 0) * FMX_RDS_RING * 2;
+  // round 6: a call of >= FMX_RDS_RING samples leaves the ring to its
+  // checkpoints (FmxRdsState::ck_*); a shorter one writes its samples into
+  // the ring, which must then hold the previous call's: refilled here first
+  // when that call left checkpoints (the channel's 8 lanes, 32 samples each)
+  const bool ringw = FUSED || a.ring_always || count < FMX_RDS_RING;
+  {
+    const bool refill = act && count > 0 && count < FMX_RDS_RING && !G.ring_ok && a.in_prev != nullptr;
+    if (__ballot(refill)) {
+      if (refill) rds_ring_fill(a.st + c, a.in_prev + (size_t)c * a.in_stride, ring, j0, RDS_LPC);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // before this call's own ring stores
+    }
+  }
   // ---- hot state -> registers ----
   uint32_t theta = G.theta, dtheta = G.dtheta;
   const uint32_t ssr0 = G.sample_since_reset;
@@ -2117,6 +2164,7 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
     for (int p = 0; p < RDS_PF; ++p) dma_round(p);
   }
   __syncthreads(); // LDS tables and per-channel state written
+  int ckp = 0; // checkpoint slot of round r: r % FMX_RDS_CK
   // the lane's tap columns: the first FMX_RDS_HREG held in registers for
   // the whole call, the others read from LDS every round
   float hr[FMX_RDS_NACC][3];
@@ -2165,6 +2213,9 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
     RDS_STAMP(1)
     const bool live = r < R;
     const int base = (r == 0) ? o0 - (FMX_RDS_DECIM - 1) : o0 + 1 + FMX_RDS_DECIM * (r - 1);
+    // this round's NCO words (the checkpoint a ring refill mixes with)
+    if (lead && live) *reinterpret_cast<uint2 *>(&L.ck[g][ckp][0]) = make_uint2(thp, dtheta);
+    ckp = (ckp == FMX_RDS_CK - 1) ? 0 : ckp + 1;
     // ---- mix-down and FIR products of this lane's samples (oldest first) ----
     f32x2 mq[3];
     bool vq[3];
@@ -2174,12 +2225,9 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
       const int t = base + j;
       vq[q] = live && t >= 0 && t < count;
       const uint32_t w = thp + (uint32_t)j * dtheta;
-      const float rr = (float)(int32_t)w * 2.3283064365386963e-10f; // w / 2^32 turns
-      const float sn = -__builtin_amdgcn_sinf(rr);
-      const float cs = __builtin_amdgcn_cosf(rr);
       // samples outside the call contribute nothing (their input reads 0)
-      mq[q] = vq[q] ? f32x2{xr0[q], xr0[q]} * f32x2{cs, sn} : f32x2{0.0f, 0.0f};
-      if (vq[q] && t >= count - FMX_RDS_RING) {
+      mq[q] = vq[q] ? rds_mix(xr0[q], w) : f32x2{0.0f, 0.0f};
+      if (ringw && vq[q] && t >= count - FMX_RDS_RING) {
         const uint32_t idx = (ring0 + (uint32_t)t) & (FMX_RDS_RING - 1);
         *reinterpret_cast<f32x2 *>(ring + 2 * idx) = mq[q];
       }
@@ -2319,6 +2367,21 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
   out->sample_since_reset = ssr0 + (uint32_t)count;
   out->ring_pos = ring0 + (uint32_t)count;
   out->rebuild = 0;
+  if (!ringw) { // the last rounds' words, oldest first (rds_ring_fill)
+    const int first = R > FMX_RDS_CK ? R - FMX_RDS_CK : 0;
+    int slot = first % FMX_RDS_CK;
+    for (int i = 0; i < min(R, FMX_RDS_CK); ++i) {
+      out->ck_thp[i] = L.ck[g][slot][0];
+      out->ck_dth[i] = L.ck[g][slot][1];
+      slot = (slot == FMX_RDS_CK - 1) ? 0 : slot + 1;
+    }
+    out->ck_o0 = o0;
+    out->ck_rounds = R;
+    out->ck_count = count;
+    out->ring_ok = 0;
+  } else if (count > 0) {
+    out->ring_ok = 1;
+  }
   for (int i = 0; i < FMX_RDS_NACC; ++i) {
     out->acc_re[i] = acc[i].x;
     out->acc_im[i] = acc[i].y;
@@ -2474,6 +2537,15 @@ __device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int s
   constexpr int kBitsW = (int)(offsetof(FmxRdsState, bi_prev_re) / 4), kRdsW = (int)(sizeof(FmxRdsState) / 4);
   static_assert(offsetof(FmxRdsState, bi_prev_re) % 4 == 0 && sizeof(FmxRdsState) % 4 == 0, "FmxRdsState parts");
   if ((parts & RSP_RDS) && (create || (m & RS_RDS))) { // sC: k_rds
+    // the rebuild reads the ring: refilled first if the last call left
+    // checkpoints instead (round 6; every thread reads the state before
+    // thread 0 rewrites it)
+    if (!create) {
+      if (!a.rds[c].ring_ok && a.rds_prev != nullptr)
+        rds_ring_fill(a.rds + c, a.rds_prev + (size_t)c * a.rds_stride, a.ring + (size_t)c * 2 * FMX_RDS_RING, tid,
+                      blockDim.x);
+      __syncthreads();
+    }
     if (tid == 0) {
       FmxRdsState s;
       if (create) {
@@ -2485,6 +2557,7 @@ __device__ void reset_channel(const ResetArgs &a, int c, int m, int parts, int s
         s = a.rds[c]; // (the bit decoders' dwords are read but not written back)
         s.rebuild = 1;
       }
+      s.ring_ok = 1; // zeroed at creation, refilled above
       s.theta = 0;
       s.dtheta = D->rds_dtheta0;
       s.sample_since_reset = 0;
@@ -3958,6 +4031,19 @@ int launch_iq_to_u8(const float *in, int in_stride, int C, int n, uint8_t *out, 
   if (C <= 0 || n <= 0) return FMX_OK;
   hipLaunchKernelGGL(k_iq_to_u8, dim3((n + 255) / 256, C), dim3(256), 0, static_cast<hipStream_t>(stream), in,
                      in_stride, n, out, out_stride);
+  return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
+}
+// every channel whose ring is left to checkpoints: refilled (fmx_diag_rds_ring)
+__global__ void k_ring_fill(ResetArgs a) {
+  const int c = blockIdx.x;
+  if (c >= a.C || a.rds[c].ring_ok || a.rds_prev == nullptr) return;
+  rds_ring_fill(a.rds + c, a.rds_prev + (size_t)c * a.rds_stride, a.ring + (size_t)c * 2 * FMX_RDS_RING, threadIdx.x,
+                blockDim.x);
+  __syncthreads();
+  if (threadIdx.x == 0) a.rds[c].ring_ok = 1;
+}
+int launch_ring_fill(const ResetArgs &a, void *stream) {
+  hipLaunchKernelGGL(k_ring_fill, dim3(a.C), dim3(256), 0, static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? FMX_OK : FMX_E_HIP;
 }
 int launch_reset(const ResetArgs &a, void *stream) {

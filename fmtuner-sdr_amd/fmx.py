@@ -64,7 +64,7 @@ class SynthConfig(C.Structure):
 
 
 _lib = None
-_OPTIONAL = {"fmx_build_info", "fmx_host_stats"}  # absent from older libraries (A/B against past revisions)
+_OPTIONAL = {"fmx_build_info", "fmx_host_stats", "fmx_diag_set", "fmx_diag_rds_ring"}  # absent from older libraries (A/B against past revisions)
 
 
 def lib():
@@ -103,6 +103,8 @@ def lib():
         "fmx_timing_enable": (i, [vp, i]),
         "fmx_kernel_times": (i, [vp, C.POINTER(C.c_double), C.POINTER(i), i]),
         "fmx_host_stats": (i, [vp, C.POINTER(C.c_double), i]),
+        "fmx_diag_set": (i, [vp, i, i]),
+        "fmx_diag_rds_ring": (i, [vp, i, fp]),
         "fmx_synth_rds_bits": (i, [C.POINTER(SynthConfig), C.c_uint32, i, vp, vp]),
         "fmx_synth_host": (i, [C.POINTER(SynthConfig), C.c_uint32, i, C.c_int64, i, vp, vp, sz, i]),
         "fmx_synth_device": (i, [vp, C.POINTER(SynthConfig), C.c_uint32, i, C.c_int64, i, vp, vp, sz]),
@@ -245,6 +247,19 @@ class Handle:
         cnt = (C.c_int * nk)()
         self._ck(self.L.fmx_kernel_times(self.h, ms, cnt, nk), "fmx_kernel_times")
         return {KERNEL_NAMES[k]: (ms[k], cnt[k]) for k in range(nk)}
+
+    def diag_set(self, what, value):
+        """fmx_diag_set: what 1 = k_rds writes the RDS ring every call."""
+        self._ck(self.L.fmx_diag_set(self.h, what, value), "fmx_diag_set")
+
+    def diag_rds_ring(self, channel):
+        """The channel's 256-sample RDS FIR ring, oldest first, as a [256, 2]
+        float32 array (synchronous; refilled from checkpoints first)."""
+        import numpy as np
+        out = np.zeros((256, 2), np.float32)
+        self._ck(self.L.fmx_diag_rds_ring(self.h, channel, out.ctypes.data_as(C.POINTER(C.c_float))),
+                 "fmx_diag_rds_ring")
+        return out
 
     def host_stats(self):
         """Host waits on pinned schedule images since the last call: (waits,

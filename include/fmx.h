@@ -38,11 +38,11 @@
 extern "C" {
 #endif
 
-/* ABI history: 8 (round 5) adds FMX_K_BITS (FMX_K_COUNT 8); 7 (round 5) adds fmx_host_stats and FMX_K_FRONTEND_GENERIC (FMX_K_COUNT 7); 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
+/* ABI history: 9 (round 6) adds fmx_diag_set / fmx_diag_rds_ring and fmx_build_info; 8 (round 5) adds FMX_K_BITS (FMX_K_COUNT 8); 7 (round 5) adds fmx_host_stats and FMX_K_FRONTEND_GENERIC (FMX_K_COUNT 7); 6 (round 4) adds FMX_K_PILOT (FMX_K_COUNT 6); 5 (round 4) added FMX_K_RS (FMX_K_COUNT 5; fmx_kernel_times
  * fills at most n entries); 4 (round 3) added fmx_synth_config.level_spread_db,
  * which changed that struct's size: callers must be rebuilt against this
  * header. */
-#define FMX_ABI_VERSION 8
+#define FMX_ABI_VERSION 9
 
 enum {
   FMX_OK = 0,
@@ -245,6 +245,16 @@ int fmx_kernel_times(void *handle, double *ms, int *launches, int n);
  * found it still pending (the host blocked), out[2] milliseconds blocked.
  * Fills at most n (<= 3) entries. */
 int fmx_host_stats(void *handle, double *out, int n);
+/* diagnostics (round 6).  A call of >= 256 RDS-rate samples leaves the RDS
+ * FIR's 256-sample ring (the mixed samples a reset's decimation-phase
+ * rebuild reads) to per-round NCO checkpoints instead of writing it; it is
+ * refilled, bit-identically, when needed.  fmx_diag_set(FMX_DIAG_RDS_RING_ALWAYS,
+ * 1) makes k_rds write it every call (round 5's behaviour; the test arm);
+ * fmx_diag_rds_ring copies the channel's ring, oldest sample first, as 256
+ * (re, im) float pairs to host memory (synchronous; refills it first). */
+enum { FMX_DIAG_RDS_RING_ALWAYS = 1 };
+int fmx_diag_set(void *handle, int what, int value);
+int fmx_diag_rds_ring(void *handle, int channel, float *out);
 
 /* ---- synthetic IQ (bench / tests input; see fmx_synth.h) ---- */
 typedef struct {
