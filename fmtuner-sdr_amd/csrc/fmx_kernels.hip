@@ -1019,18 +1019,6 @@ __device__ __forceinline__ void dma_dwordx3(const float *src, uint32_t lds) {
                : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
                : "memory");
 }
-// non-temporal loads of once-read streams (A/B switch, bit mask): 1 k_fe8's
-// u8 IQ, 2 k_rds's RDS-rate input, 4 k_pll's pilot tiles, 8 k_audio's raw L/R
-#ifndef FMX_NT
-#define FMX_NT 0
-#endif
-__device__ __forceinline__ void dma_dword_nt(const float *src, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p);
 }
@@ -1242,13 +1230,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE)
 #pragma unroll
       for (int k = 0; k < AU2_PT; ++k) {
         const int j = tid + 256 * k;
-        if (FMX_NT & 8) {
-          vl[k] = (j < cnt) ? __builtin_nontemporal_load(&inl[ti(n0 + j)]) : 0.0f;
-          vr[k] = (j < cnt && !mono) ? __builtin_nontemporal_load(&inr[ti(n0 + j)]) : 0.0f;
-        } else {
-          vl[k] = (j < cnt) ? inl[ti(n0 + j)] : 0.0f;
-          vr[k] = (j < cnt && !mono) ? inr[ti(n0 + j)] : 0.0f;
-        }
+        vl[k] = (j < cnt) ? inl[ti(n0 + j)] : 0.0f;
+        vr[k] = (j < cnt && !mono) ? inr[ti(n0 + j)] : 0.0f;
       }
       if (lrfir) {
         // f16 hi / lo images [L hi | L lo | R hi | R lo], index = chunk sample + 120
@@ -2123,7 +2106,7 @@ __global__ __launch_bounds__(64, FUSED ? 2 : FMX_RDS_WPE) void k_rds(RdsArgs a) 
     for (int q = 0; q < 3; ++q) {
       const int t = base + 3 * j0 + q;
       const bool v = act && r < R && t >= 0 && t < count;
-      ((FMX_NT & 2) ? dma_dword_nt : dma_dword)(inb + (act ? g * a.in_stride : 0) + (v ? t : 0),
+      dma_dword(inb + (act ? g * a.in_stride : 0) + (v ? t : 0),
                 xin0 + (uint32_t)(((r & (RDS_NR - 1)) * 3 + q) * 64 * 4));
     }
   };
@@ -2913,7 +2896,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       const int pc = P_LO + wave + 4 * j;
       if (pc < P_HI)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, (FMX_NT & 1) ? 2 : 0);
+            riq, (__attribute__((address_space(3))) void *)(smem + 1024 * pc), 16, off, 0, 0, 0);
       off += 4096u;
       asm volatile("" : "+v"(off));
     }
