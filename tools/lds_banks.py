@@ -73,6 +73,15 @@ def _patterns():
     # k_audio FIR output to f: untransposed float4 pairs, transposed float2
     out.append(("audio f write, untransposed float4", "write_b128", [8 * o for o in untr(0)]))
     out.append(("audio f write, transposed float2", "write_b64", [8 * o for o in tr(0)]))
+    # k_fe8 decimator A fragments from the LDS tap window (round 6, M = 10):
+    # lane (col, g) reads dwords 75 + 4 g - 5 col + k, k = 0..3 (two
+    # ds_read2_b32 = four b32 accesses); one copy, or the odd-g lanes from a
+    # copy 12 dwords along the banks (Fe8Layout::QT2)
+    for k in range(4):
+        out.append((f"fe8 decimator fragment dword {k}, one window", "read_b32",
+                    [4 * (75 + 4 * g[l] - 5 * col[l] + k) for l in lanes]))
+        out.append((f"fe8 decimator fragment dword {k}, odd g from the shifted copy", "read_b32",
+                    [4 * (75 + 4 * g[l] - 5 * col[l] + k + (12 if g[l] & 1 else 0)) for l in lanes]))
     return out
 
 
