@@ -2769,13 +2769,7 @@ template <int M, int TPP, bool RS = true> struct Fe8Layout {
   static constexpr int QT = (SH + (int)sizeof(FeShared) + 15) & ~15;
   // and the channel's IQ FIR design's window FmxDesign::iq_q16 [2][2][FMX_IQ_QN]
   static constexpr int QIP = (2 * FMX_IQ_QN + 63) / 64;              // 2 FMX_IQ_QN dwords
-  // a second copy of the decimator's window for the lanes of odd g (lanes
-  // 16-31, 48-63), 12 dwords further along the 32 banks: a lane (col, g)
-  // reads dword 75 + 4 g - 5 col (M = 10) of its copy, and the lanes of one
-  // ds_read_b32 group (g = 0, 1) then never share a bank (one copy: 2-way,
-  // 7.3 M of k_fe8's 11.5 M conflict cycles per launch; tools/lds_banks.py)
-  static constexpr int QT2 = QT + (RS ? 0 : QDP * 256 + 48);
-  static constexpr int QI = QT2 + (RS ? 0 : QDP * 256);
+  static constexpr int QI = QT + (RS ? 0 : QDP * 256);
   // RS = false (round 6): the channel's carried words and decimator history
   // land here by LDS-DMA with the first chunk (1 KB: dwords 0..63 the words,
   // 64..255 the history bytes), so the setup waits on no load
@@ -3017,12 +3011,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
     static_assert(FMX_IQ_QN % 2 == 0, "dword windows");
     const float *qs = reinterpret_cast<const float *>(&D->dec_q16[0][0]);
     const float *is = reinterpret_cast<const float *>(&D->iq_q16[par.iqsel][0][0][0]);
-    for (int p = wave; p < 2 * LY::QDP + LY::QIP; p += 4) {
-      const bool dec = p < 2 * LY::QDP, second = p >= LY::QDP && dec; // the decimator's window twice (LY::QT2)
-      const int pp = second ? p - LY::QDP : (dec ? p : p - 2 * LY::QDP);
-      const int e = 64 * pp + lane;
+    for (int p = wave; p < LY::QDP + LY::QIP; p += 4) {
+      const bool dec = p < LY::QDP;
+      const int e = 64 * (dec ? p : p - LY::QDP) + lane;
       const float *src = dec ? qs + min(e, FMX_DEC_QN - 1) : is + min(e, 2 * FMX_IQ_QN - 1);
-      dma_dword(src, lds_addr(smem + (dec ? (second ? LY::QT2 : LY::QT) + 256 * pp : LY::QI + 256 * pp)));
+      dma_dword(src, lds_addr(smem + (dec ? LY::QT + 256 * p : LY::QI + 256 * (p - LY::QDP))));
     }
     // ... and the carried state (round 6): the IQ FIR history into hx (one
     // 64-dword piece per wave), the DC / discriminator / AGC words and the
@@ -3148,7 +3141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((M == 8 || 
       // dwords, two ds_read2_b32 per half -- round 5 read dec_frag from L2,
       // 2 KB per wave and K step, and every K step waited on that load), RS =
       // true from the design's fragment table (16 B per lane)
-      const uint32_t *qh = reinterpret_cast<const uint32_t *>(smem + ((g & 1) ? LY::QT2 : LY::QT)) + (15 * M + 8 * g - M * col) / 2;
+      const uint32_t *qh = reinterpret_cast<const uint32_t *>(smem + LY::QT) + (15 * M + 8 * g - M * col) / 2;
       const uint32_t *ql = qh + FMX_DEC_QN / 2;
       const u32x4 *fa = reinterpret_cast<const u32x4 *>(&D->dec_frag[0][0][0][0]) + lane;
       auto frag = [&](int ks, int s) __attribute__((always_inline)) {
