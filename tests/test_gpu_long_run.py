@@ -9,7 +9,7 @@ whole run, RDS groups bit-exact, the stereo flag never flipping on one side
 only, and the PCM error of the last 40 blocks no larger than twice that of
 the first 40 (plus a floor far under the bar) -- a bounded error, not a
 walk.  The pilot level is an integer (tenths of kHz) rounded from a float
-magnitude (stereo_decoder.cpp:281-284): over a noisy run a block whose
+magnitude (stereo_decoder.cpp:283-285): over a noisy run a block whose
 magnitude sits on a rounding boundary can come out one tenth apart (first
 run: 1 block of 240, channel 0, with the PCM at 1.8e-6 RMS), so the long
 runs allow 1 tenth on at most 2 blocks per channel; the short parity tests
