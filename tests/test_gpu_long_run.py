@@ -11,9 +11,9 @@ the first 40 (plus a floor far under the bar) -- a bounded error, not a
 walk.  The pilot level is an integer (tenths of kHz) rounded from a float
 magnitude (stereo_decoder.cpp:283-285): over a noisy run a block whose
 magnitude sits on a rounding boundary can come out one tenth apart (first
-run: 1 block of 240, channel 0, with the PCM at 1.8e-6 RMS), so the long
-runs allow 1 tenth on at most 2 blocks per channel; the short parity tests
-keep it exact."""
+run: 1 block of 240 on a noisy M = 10 channel, 2 of 250 on one M = 8
+channel), so the long runs allow 1 tenth on at most 3 blocks per channel
+(~1 %); the short parity tests keep it exact."""
 import numpy as np
 import pytest
 
@@ -33,15 +33,20 @@ def _window_rms(g, o, c, b0, b1):
     return (sq / max(n, 1)) ** 0.5
 
 
-@pytest.mark.parametrize("noise", [0.0, 0.02])
-def test_four_seconds_no_drift(fmx, oracle, torch_cuda, noise):
-    C, nblk, W = 6, 240, 40
-    iq, _ = make_iq(fmx, 2, C, nblk, noise=noise, ch0=700 if noise else 640)
-    g, outs = run_both(fmx, oracle, torch_cuda, {}, iq, nblk)
+@pytest.mark.parametrize("noise,iq_rate", [(0.0, 2_400_000), (0.02, 2_400_000), (0.0, 2_048_000)])
+def test_four_seconds_no_drift(fmx, oracle, torch_cuda, noise, iq_rate):
+    """M = 10 clean and noisy; M = 8, the reference's own 2.048 MS/s rate
+    (k_fe8's M = 8 instance, 256 kHz MPX: 4 s is 250 blocks)."""
+    C, W = 6, 40
+    M = iq_rate // (240_000 if iq_rate == 2_400_000 else 256_000)
+    nblk = 240 if M == 10 else 250
+    kw = {} if M == 10 else dict(iq_rate=iq_rate, dsp_rate=256_000)
+    iq, _ = make_iq(fmx, 2, C, nblk, iq_rate=iq_rate, M=M, noise=noise, ch0=700 if noise else (640 if M == 10 else 760))
+    g, outs = run_both(fmx, oracle, torch_cuda, kw, iq, nblk)
     ngroups = 0
     for c in range(C):
-        st = check(g, outs[c], c, nblk, f"long_run noise={noise}", pilot_tol=1)
-        assert st["pilot_mismatch"] <= 2, (c, st["pilot_mismatch"])
+        st = check(g, outs[c], c, nblk, f"long_run noise={noise} M={M}", pilot_tol=1)
+        assert st["pilot_mismatch"] <= 3, (c, st["pilot_mismatch"])
         ngroups += len(st["groups_oracle"])
         first = _window_rms(g, outs[c], c, 0, W)
         last = _window_rms(g, outs[c], c, nblk - W, nblk)
