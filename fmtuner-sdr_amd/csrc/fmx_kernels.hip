@@ -1128,10 +1128,12 @@ __device__ __forceinline__ void au_scan_prev(float A, float BL, float BR, float 
 #ifndef FMX_AU_WPE
 #define FMX_AU_WPE 1 // k_audio waves per SIMD the register budget allows (A/B switch; 1 = the compiler's choice)
 #endif
-// one channel (block index b) of k_audio
-__device__ __forceinline__ void k_audio_channel(const AudioArgs &a, int b, unsigned char *au_smem) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE))) void k_audio(AudioArgs a) {
+  // dynamic LDS, as k_rds: a static 45 KB made the backend pad the VGPR
+  // allocation from 111 to 129 (occupancy 3 by LDS)
+  extern __shared__ __align__(16) unsigned char au_smem[];
   AuShared &S = *reinterpret_cast<AuShared *>(au_smem);
-  const int c = au_channel(b, a.C, a.in_tiled != 0);
+  const int c = au_channel(blockIdx.x, a.C, a.in_tiled != 0);
   const int tid = threadIdx.x;
   const FmxDesign *__restrict__ D = a.des;
   const FmxChanParam par = a.par[c];
@@ -1148,8 +1150,8 @@ __device__ __forceinline__ void k_audio_channel(const AudioArgs &a, int b, unsig
   const float dc_a1 = -1.0f + dc_alpha;
   // the step's RF levels: workgroup b evaluates channels 256 b .. 256 b + 255
   // from the front end's byte sums (one thread each)
-  if (a.sig_out && b * 256 < a.C) {
-    const int cs = b * 256 + tid;
+  if (a.sig_out && blockIdx.x * 256 < (unsigned)a.C) {
+    const int cs = blockIdx.x * 256 + tid;
     if (cs < a.C)
       signal_level_eval(a.sig_sums + 6 * (size_t)cs, a.sig_samples, a.sig_par + 4 * (size_t)cs,
                         a.sig_smooth + 2 * (size_t)cs, a.sig_out + cs);
@@ -1498,25 +1500,6 @@ __device__ __forceinline__ void k_audio_channel(const AudioArgs &a, int b, unsig
       a.mute[2 * c] = mrem - mc;
       if (mrem - mc == 0) a.mute[2 * c + 1] = 0;
     }
-  }
-}
-// A/B (FMX_AU_GRID = N > 0): N workgroups, each taking channels b, b + N, ...
-// in turn (fewer k_audio waves in flight beside the front end; N a multiple
-// of 8 keeps au_channel's XCD order)
-#ifndef FMX_AU_GRID
-#define FMX_AU_GRID 0
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMX_AU_WPE))) void k_audio(AudioArgs a) {
-  // dynamic LDS, as k_rds: a static 45 KB made the backend pad the VGPR
-  // allocation from 111 to 129 (occupancy 3 by LDS)
-  extern __shared__ __align__(16) unsigned char au_smem[];
-  if (FMX_AU_GRID > 0) {
-    for (int b = blockIdx.x; b < a.C; b += gridDim.x) {
-      k_audio_channel(a, b, au_smem);
-      __syncthreads(); // the next channel reuses the LDS
-    }
-  } else {
-    k_audio_channel(a, blockIdx.x, au_smem);
   }
 }
 
@@ -3738,8 +3721,7 @@ int launch_pll(const PllArgs &a, void *stream) {
   return fmx_launch(k_pll<24>, dim3((a.C + 23) / 24), dim3(64 * PLL_WAVES(24)), 0, st, a);
 }
 int launch_audio(const AudioArgs &a, void *stream) {
-  const int grid = FMX_AU_GRID > 0 ? std::min(a.C, FMX_AU_GRID) : a.C;
-  return fmx_launch(k_audio, dim3(grid), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
+  return fmx_launch(k_audio, dim3(a.C), dim3(256), sizeof(AuShared), static_cast<hipStream_t>(stream), a);
 }
 /* ================================================================== */
 /* k_pilot: the 19 kHz pilot band-pass (stereo_decoder.cpp:229-230)    */
