@@ -1263,8 +1263,15 @@ static int process_block(Handle *h, const uint8_t *d_iq, size_t iq_stride, int n
     // about half as many workgroups beside the other streams' (round 6, with
     // k_rs's schedule no longer staged in LDS): 4096 ch 0.5790 -> 0.5707 and
     // 0.5804 -> 0.5718 ms in two 4-rep A/Bs; at 2048 ch the longer parts were
-    // slower, 0.3453 -> 0.3638 (profiles/r06k_ab_rs_parts_*.txt, r06m_*)
-    const int rs_tiles = (h->t_rds.stride + 15) / 16, rs_tmax = (h->C + 15) / 16 >= 256 ? 46 : FMX_RS_TMAX;
+    // slower, 0.3453 -> 0.3638 (profiles/r06k_ab_rs_parts_*.txt, r06m_*).
+    // Fewer channels, finer parts: with few channel groups k_rs is latency --
+    // one wave per part walking its tiles -- so below 2048 channels parts of
+    // <= 6 tiles (1024 ch 0.2809 -> 0.2444 ms, 256 ch 0.2465 -> 0.2033) and
+    // <= 12 at 2048 (0.3410 -> 0.3379, 0.3445 -> 0.3420 in r06c)
+    // (profiles/r06z4_*, r06z5_*)
+    const int rs_groups = (h->C + 15) / 16;
+    const int rs_tiles = (h->t_rds.stride + 15) / 16,
+              rs_tmax = rs_groups >= 256 ? 46 : (rs_groups >= 128 ? FMX_RS_TMAX : 6);
     r.parts = std::max(1, (rs_tiles + rs_tmax - 1) / rs_tmax);
     KBind t(h, FMX_K_RS, s, done);
     if (!FMX_SKIP(rds) && !FMX_SKIP(krs)) {

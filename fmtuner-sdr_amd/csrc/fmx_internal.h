@@ -235,7 +235,7 @@ int launch_bits(const RdsArgs &a, void *stream);     // k_bits alone: the bit de
 #define FMX_RDS_FUSED 0 // A/B: the RDS resampler inside k_rds (RdsArgs::fused)
 #endif
 #ifndef FMX_RS_TMAX
-#define FMX_RS_TMAX 24 // k_rs: output tiles (of 16) per workgroup at most (46 from 4096 channels on, fmx_capi.cpp)
+#define FMX_RS_TMAX 12 // k_rs: output tiles (of 16) per workgroup at most from 2048 channels (46 from 4096 on, 6 below 2048: fmx_capi.cpp)
 #endif
 int launch_rs(const RsArgs &a, void *stream);
 int launch_synth(const fmx_synth_config &cfg, uint32_t ch0, int n_ch, int64_t sample0, int n_samples,
